@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident DCCL local combine on MI355X (BASELINE.json metric).
+
+One "step" = one pass of the combine ``recv[i] = recv[i] + send[i]`` over 1 GiB fp32
+operands resident in HBM (BASELINE.json metric: ncclSum fp32, 1 GiB).  Each rank owns its
+own 1 GiB shard pair (the combine is element-wise: no data-path collective), so the
+aggregate is weak scaling.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mib 1024] [--dtype float32] [--op sum]
+
+Rank 0 prints ONE JSON line:
+  value            whole-job HBM traffic rate, GiB/s = N * 3 * bytes_per_operand / t_step
+                   (3 = read send + read recv + write recv; BASELINE.md §2 roofline basis)
+  roofline         dominant kernel (the combine): algorithmic bytes per launch / average
+                   launch duration from HIP events on the launch stream, vs 8.0 TB/s HBM peak;
+                   `traffic` = PMC HBM bytes per launch from profiles/pmc_traffic.json when present
+  cpu_baseline     the reference's own CPU loop (oracle/_ref, Release flags) or the oracle
+                   restatement, single thread, timed on this host on a bounded sample (rank 0, N=1)
+Extra keys: payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
+rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import dccl_amd  # noqa: E402  (fails loudly when the HIP library is missing)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+GIB = float(1 << 30)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--mib", type=int, default=1024, help="MiB per operand per GPU")
+    p.add_argument("--dtype", default="float32", choices=list(dccl_amd.DTYPE_NAMES))
+    p.add_argument("--op", default="sum", choices=["sum", "prod", "max", "min"])
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-host-staged", action="store_true")
+    return p.parse_args()
+
+
+def synth(n: int, dt: int, op: int, seed: int, device) -> torch.Tensor:
+    """Synthetic operand: uniform [-1,1) for Sum/Max/Min, [0.5,2) for Prod; ints full range."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    tdt = dccl_amd.TORCH_DTYPES[dt]
+    if dt in (6, 7, 8, 9):
+        x = torch.rand(n, device=device, generator=g, dtype=torch.float32 if dt != 8 else torch.float64)
+        x = x.mul_(1.5).add_(0.5) if op == 1 else x.mul_(2).sub_(1)
+        return x.to(tdt)
+    raw = torch.randint(-2**31, 2**31 - 1, ((n * dccl_amd.size_of_type(dt) + 3) // 4,), device=device,
+                        generator=g, dtype=torch.int32)
+    return raw.view(torch.uint8)[: n * dccl_amd.size_of_type(dt)].view(torch.int8) if dt in (0, 1) else \
+        raw.view(torch.int64 if dt in (4, 5) else torch.int32)[:n]
+
+
+def cpu_baseline(budget_s: float) -> dict | None:
+    """Reference CPU loop (oracle/_ref) single-threaded, plus all host threads, fp32 Sum."""
+    try:
+        import oracle  # test infrastructure: the CPU baseline leg only
+    except Exception:
+        return None
+    ref = oracle.reference()
+    kind = "reference" if ref is not None else "port"
+    fn = (lambda s, r, n: ref.ref_host_reduce(s, r, n, 7, 0)) if ref is not None else \
+        (lambda s, r, n: oracle.restatement().oracle_host_reduce(s, r, n, 7, 0))
+    n = (256 << 20) // 4  # 256 MiB per operand sample (BASELINE config C2 size)
+    s = oracle.aligned_empty(n, np.float32)
+    r = oracle.aligned_empty(n, np.float32)
+    s[:] = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32)
+    r[:] = 0
+    ps, pr = s.ctypes.data, r.ctypes.data
+    fn(ps, pr, n)  # page in
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s * 0.6:
+        fn(ps, pr, n)
+        reps += 1
+    t1 = (time.perf_counter() - t0) / reps
+    # all host threads: 64-B aligned contiguous slices, one thread each (ctypes drops the GIL)
+    nthr = len(os.sched_getaffinity(0))
+    per = (n // nthr) // 16 * 16
+    bounds = [(i * per, n if i == nthr - 1 else (i + 1) * per) for i in range(nthr)]
+
+    def work(lo, hi):
+        fn(ps + 4 * lo, pr + 4 * lo, hi - lo)
+
+    reps_mt, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s * 0.4 or reps_mt == 0:
+        ts = [threading.Thread(target=work, args=b) for b in bounds]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        reps_mt += 1
+    tmt = (time.perf_counter() - t0) / reps_mt
+    nbytes = n * 4
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(3 * nbytes / t1 / GIB, 2), "unit": "GiB/s (HBM-traffic basis 3*N*4 B, fp32 Sum)",
+        "cores": 1, "kind": kind,
+        "sample": f"fp32 Sum, 256 MiB per operand host buffers (64-B aligned), {reps} passes in "
+                  f"{t1 * reps:.1f}s, Release flags -O3 -mprefer-vector-width=512",
+        "payload_gib_s": round(nbytes / t1 / GIB, 2),
+        "all_cores": {"value": round(3 * nbytes / tmt / GIB, 2), "cores": nthr, "passes": reps_mt,
+                      "payload_gib_s": round(nbytes / tmt / GIB, 2)},
+        "cpu_model": cpu_model,
+    }
+
+
+def host_staged_rate(nbytes: int, dt: int, op: int) -> dict:
+    """Operands in pinned host memory (Derecho's RDMA buffers): H2D + combine + D2H, pipelined."""
+    n = nbytes // dccl_amd.size_of_type(dt)
+    s = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    r = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    s.view(torch.float32).uniform_(-1, 1) if dt == 7 else s.random_()
+    r.zero_()
+    rc = dccl_amd.local_reduce_host(s.data_ptr(), r.data_ptr(), dt, n, op)
+    dccl_amd.check(rc, "dccl_local_reduce_host")
+    reps, t0 = 0, time.perf_counter()
+    while reps < 3 or time.perf_counter() - t0 < 1.0:
+        dccl_amd.check(dccl_amd.local_reduce_host(s.data_ptr(), r.data_ptr(), dt, n, op), "host")
+        reps += 1
+    t = (time.perf_counter() - t0) / reps
+    return {"payload_gib_s": round(nbytes / t / GIB, 2), "ms": round(t * 1e3, 3),
+            "bytes_per_operand": nbytes, "note": "pinned host operands; PCIe H2D 2N + D2H N bytes"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    dt = dccl_amd.DTYPE_NAMES[a.dtype]
+    op = dccl_amd.OP_NAMES[a.op]
+    esz = dccl_amd.size_of_type(dt)
+    nbytes = a.mib << 20
+    n = nbytes // esz
+
+    send = synth(n, dt, op, 0xDCC1 + 2 * rank, dev)
+    recv = synth(n, dt, op, 0xDCC1 + 2 * rank + 1, dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    ps, pr = send.data_ptr(), recv.data_ptr()
+
+    def step():
+        rc = dccl_amd.local_reduce(ps, pr, dt, n, op, sh)
+        if rc:
+            raise dccl_amd.DcclError(rc, "dccl_local_reduce")
+
+    for _ in range(a.warmup):
+        step()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+    else:
+        kern_ms_max = kern_ms
+    ms_per_step = elapsed / a.steps * 1e3
+
+    extra = {}
+    if world > 1:  # the one exchange step of C5: RCCL all-gather of the reduced shards (separate)
+        gathered = torch.empty(world * n, dtype=recv.dtype, device=dev)
+        dist.all_gather_into_tensor(gathered, recv)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        iters = 3
+        for _ in range(iters):
+            dist.all_gather_into_tensor(gathered, recv)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tag = (time.perf_counter() - t0) / iters
+        extra["allgather"] = {"ms": round(tag * 1e3, 3),
+                              "busbw_gb_s": round((world - 1) * nbytes / tag / 1e9, 1),
+                              "note": "RCCL all_gather_into_tensor of the 1 GiB shards over xGMI; not in value"}
+        del gathered
+
+    if rank == 0:
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path) and dt == 7 and op == 0 and a.mib == 1024:
+            try:
+                traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        achieved = 3 * nbytes / (kern_ms * 1e-3) / 1e9
+        res = {
+            "metric": "device-resident reduce GiB/s (ncclSum fp32, 1 GiB) at 1/2/4/8 GPU vs HBM peak",
+            "value": round(world * 3 * nbytes / (ms_per_step * 1e-3) / GIB, 2),
+            "unit": "GiB/s (HBM traffic 3*N*sizeof per combine, summed over GPUs)",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": {0: "i8", 1: "u8", 2: "i32", 3: "u32", 4: "i64", 5: "u64", 6: "f16", 7: "f32", 8: "f64",
+                      9: "bf16"}[dt],
+            "data": "synthetic (seeded uniform [-1,1) operands resident in HBM)",
+            "config": {"workload": f"in-place two-buffer combine recv=op(recv,send), {a.op}, "
+                                   f"{a.mib} MiB per operand per GPU (BASELINE configs C3/C5)",
+                       "bytes_per_operand_per_gpu": nbytes, "op": a.op, "parallelism": f"shard x{world}"},
+            "payload_gib_s": round(world * nbytes / (ms_per_step * 1e-3) / GIB, 2),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "reduce_vec_kernel (dccl_local_reduce)",
+                         "kernel_ms_avg": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_ms_max, 4),
+                         "bytes_per_launch": 3 * nbytes},
+        }
+        res.update(extra)
+        if world == 1 and not a.no_host_staged:
+            res["host_staged"] = host_staged_rate(nbytes, dt, op)
+        if world == 1 and not a.no_cpu:
+            res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,173 @@
+"""dccl_amd — MI355X-native DCCL local bucket-reduction combine.
+
+Python binding of the C-ABI in ``include/dccl/dccl_reduce.h`` (ctypes; plain pointers,
+sizes and enum integers).  The combine itself is hand-written HIP for gfx950 inside
+``dccl_amd/lib/libdccl_amd.so``; there is no CPU fallback: if the shared library is
+missing, importing this package raises.
+
+Enum values are those of the reference's public header
+(/root/reference/include/dccl/dccl.hpp:59-112), with ncclBfloat16 = 9 always present.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+
+try:  # share torch's HIP runtime (same soname libamdhip64.so.7) when torch is around
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is plumbing only
+    torch = None
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "lib", "libdccl_amd.so")
+
+
+class ncclResult_t(enum.IntEnum):
+    ncclSuccess = 0
+    ncclUnhandledCudaError = 1
+    ncclSystemError = 2
+    ncclInternalError = 3
+    ncclInvalidArgument = 4
+    ncclInvalidUsage = 5
+    ncclRemoteError = 6
+    ncclInProgress = 7
+
+
+class ncclDataType_t(enum.IntEnum):
+    ncclInt8 = 0
+    ncclUint8 = 1
+    ncclInt32 = 2
+    ncclUint32 = 3
+    ncclInt64 = 4
+    ncclUint64 = 5
+    ncclFloat16 = 6
+    ncclFloat32 = 7
+    ncclFloat64 = 8
+    ncclBfloat16 = 9
+
+
+class ncclRedOp_t(enum.IntEnum):
+    ncclSum = 0
+    ncclProd = 1
+    ncclMax = 2
+    ncclMin = 3
+    ncclAvg = 4
+
+
+ALL_DTYPES = list(ncclDataType_t)
+ALL_OPS = [ncclRedOp_t.ncclSum, ncclRedOp_t.ncclProd, ncclRedOp_t.ncclMax, ncclRedOp_t.ncclMin]
+
+DTYPE_NAMES = {
+    "int8": 0, "uint8": 1, "int32": 2, "uint32": 3, "int64": 4, "uint64": 5,
+    "float16": 6, "float32": 7, "float64": 8, "bfloat16": 9,
+}
+OP_NAMES = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
+
+
+class DcclError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        super().__init__(f"{what} failed: {code} ({result_string(code)})")
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"dccl_amd: native library {LIB_PATH} is missing; build it with "
+            "`python -m dccl_amd.build` (hipcc, gfx950). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    c_int, c_size_t, c_void_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
+    sig = {
+        "dccl_local_reduce": (c_int, [c_void_p, c_void_p, c_int, c_size_t, c_int, c_void_p]),
+        "dccl_local_reduce_multi": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_size_t,
+                                            c_int, c_void_p]),
+        "dccl_local_reduce_host": (c_int, [c_void_p, c_void_p, c_int, c_size_t, c_int]),
+        "dccl_register_host_memory": (c_int, [c_void_p, c_size_t]),
+        "dccl_deregister_host_memory": (c_int, [c_void_p]),
+        "dccl_size_of_type": (c_size_t, [c_int]),
+        "dccl_result_string": (ctypes.c_char_p, [c_int]),
+        "dccl_version": (c_int, []),
+        "dccl_tune_reduce_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_size_t, c_void_p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+#: every symbol the C-ABI headers declare (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = [
+    "dccl_local_reduce", "dccl_local_reduce_multi", "dccl_local_reduce_host",
+    "dccl_register_host_memory", "dccl_deregister_host_memory", "dccl_size_of_type",
+    "dccl_result_string", "dccl_version", "dccl_tune_reduce_f32_sum",
+]
+
+
+def result_string(code: int) -> str:
+    return lib.dccl_result_string(int(code)).decode()
+
+
+def size_of_type(dtype: int) -> int:
+    return int(lib.dccl_size_of_type(int(dtype)))
+
+
+def version() -> int:
+    return int(lib.dccl_version())
+
+
+def local_reduce(send_ptr: int, recv_ptr: int, dtype: int, count: int, op: int, stream: int = 0) -> int:
+    """Device combine recv = op(recv, send); returns the ncclResult_t code (no raise)."""
+    return int(lib.dccl_local_reduce(send_ptr, recv_ptr, int(dtype), int(count), int(op), stream or None))
+
+
+def local_reduce_multi(send_ptrs, recv_ptr: int, dtype: int, count: int, op: int, stream: int = 0) -> int:
+    arr = (ctypes.c_void_p * len(send_ptrs))(*send_ptrs)
+    return int(lib.dccl_local_reduce_multi(arr, len(send_ptrs), recv_ptr, int(dtype), int(count), int(op),
+                                           stream or None))
+
+
+def local_reduce_host(send_ptr: int, recv_ptr: int, dtype: int, count: int, op: int) -> int:
+    """Host-pointer combine (staged through the current GPU); synchronous."""
+    return int(lib.dccl_local_reduce_host(send_ptr, recv_ptr, int(dtype), int(count), int(op)))
+
+
+def register_host_memory(ptr: int, size: int) -> int:
+    return int(lib.dccl_register_host_memory(ptr, size))
+
+
+def deregister_host_memory(ptr: int) -> int:
+    return int(lib.dccl_deregister_host_memory(ptr))
+
+
+def check(code: int, what: str = "dccl") -> None:
+    if code != 0:
+        raise DcclError(code, what)
+
+
+# --------------------------------------------------------------------------------------
+# torch conveniences (device memory and streams are torch's; the compute is ours)
+# --------------------------------------------------------------------------------------
+if torch is not None:
+    TORCH_DTYPES = {
+        0: torch.int8, 1: torch.uint8, 2: torch.int32, 3: torch.uint32 if hasattr(torch, "uint32") else None,
+        4: torch.int64, 5: torch.uint64 if hasattr(torch, "uint64") else None, 6: torch.float16,
+        7: torch.float32, 8: torch.float64, 9: torch.bfloat16,
+    }
+    _TORCH_TO_DCCL = {v: k for k, v in TORCH_DTYPES.items() if v is not None}
+
+    def dccl_dtype_of(t) -> int:
+        return _TORCH_TO_DCCL[t.dtype]
+
+    def reduce_(recv, send, op: int = 0, dtype: int | None = None, stream=None) -> None:
+        """In place ``recv = op(recv, send)`` on CUDA tensors through the HIP kernel."""
+        if not (recv.is_cuda and send.is_cuda):
+            raise ValueError("reduce_ expects device tensors")
+        if recv.numel() != send.numel() or not recv.is_contiguous() or not send.is_contiguous():
+            raise ValueError("reduce_ expects contiguous tensors of equal numel")
+        dt = dccl_dtype_of(recv) if dtype is None else dtype
+        s = (stream or torch.cuda.current_stream(recv.device)).cuda_stream
+        check(local_reduce(send.data_ptr(), recv.data_ptr(), dt, recv.numel(), op, s), "dccl_local_reduce")

@@ -1,0 +1,71 @@
+"""Build ``dccl_amd/lib/libdccl_amd.so`` in-tree with hipcc for gfx950.
+
+One shared library holds the HIP kernels, the C-ABI (include/dccl/dccl_reduce.h) and the
+C++ ``namespace dccl`` API (include/dccl/dccl.hpp).  Sources compile in parallel; the
+link is a plain ``hipcc -shared``.  No fast-math / FTZ flags: the combine must keep
+fp32/fp16 denormals (SURVEY.md §7 "Bit-exact semantics").
+
+    python -m dccl_amd.build [--force]
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OUT_DIR = os.path.join(PKG, "lib")
+OBJ_DIR = os.path.join(ROOT, "build", "obj")
+LIB = os.path.join(OUT_DIR, "libdccl_amd.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("DCCL_OFFLOAD_ARCH", "gfx950")
+
+COMMON = ["-std=c++17", "-O3", "-fPIC", "-Wall", "-Wno-unused-command-line-argument",
+          f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
+
+
+def _sources() -> list[str]:
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
+
+
+def _headers() -> list[str]:
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    inc = os.path.join(ROOT, "include", "dccl")
+    hs += [os.path.join(inc, f) for f in os.listdir(inc)]
+    return hs
+
+
+def _compile(src: str) -> str:
+    obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+    newest_dep = max(os.path.getmtime(p) for p in _headers() + [src, __file__])
+    if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
+        return obj
+    cmd = [HIPCC, *COMMON, f"--offload-arch={ARCH}", "-c", src, "-o", obj]
+    if src.endswith(".hip"):
+        cmd[1:1] = ["-x", "hip"]
+    subprocess.run(cmd, check=True)
+    return obj
+
+
+def build(force: bool = False) -> str:
+    os.makedirs(OUT_DIR, exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    srcs = _sources()
+    if force:
+        for f in os.listdir(OBJ_DIR):
+            os.remove(os.path.join(OBJ_DIR, f))
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(_compile, srcs))
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        tmp = LIB + ".tmp"
+        subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp,
+                        "-Wl,-soname,libdccl_amd.so"], check=True)
+        os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

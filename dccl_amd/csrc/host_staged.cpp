@@ -1,0 +1,225 @@
+// dccl_amd/csrc/host_staged.cpp — the combine for host-resident chunks.
+//
+// In the reference the ring reduce-scatter combines chunks that live in host memory
+// (Derecho's RDMA receive scratchpad, /root/reference/src/core/dccl.cpp:102-150) with the
+// single-threaded CPU loop do_host_reduce<DT> (/root/reference/src/core/internal_common.hpp:496-586,
+// called at /root/reference/src/core/reduce_scatter_ring.cpp:91-94).  Here the same call runs
+// on the MI355X: the operands are cut into chunks and pushed through a three-stage pipeline
+//     copy-in stream : H2D(send chunk), H2D(recv chunk)
+//     compute stream : dccl_local_reduce on the staged chunk
+//     copy-out stream: D2H(recv chunk)
+// over NSLOT device slots, so PCIe in both directions and the HBM combine overlap
+// (SURVEY.md §8(f) row 1).  Page-locked user buffers (dccl_register_host_memory, the
+// analogue of dcclRegisterCacheMemory, dccl.cpp:503-549) are DMA'd directly; pageable ones
+// are bounced through per-thread pinned staging buffers by the calling thread.
+//
+// Per-thread state (like the reference's thread_local scratchpads, dccl.cpp:67-83): no
+// locks, no global mutable state; each thread owns its streams and slots per device.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "dccl/dccl_reduce.h"
+#include "dispatch.hpp"
+
+namespace dccl_amd {
+namespace {
+
+constexpr int kSlots = 3;
+constexpr size_t kChunkBytes = size_t(16) << 20;  // per operand per slot
+
+struct Slot {
+    void* d_send = nullptr;
+    void* d_recv = nullptr;
+    void* h_send = nullptr;  // pinned bounce buffers, used only for pageable user memory
+    void* h_recv = nullptr;
+    hipEvent_t in_done = nullptr, comp_done = nullptr, out_done = nullptr;
+    size_t pending_bytes = 0;    // bytes of an unfinished D2H into h_recv
+    unsigned char* pending_dst = nullptr;
+};
+
+class Stager {
+public:
+    explicit Stager(int device) : device_(device) {}
+    ~Stager() { release(); }
+
+    int init() {
+        if (ready_) return DCCL_SUCCESS;
+        if (hipSetDevice(device_) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
+        for (hipStream_t* s : {&in_, &comp_, &out_})
+            if (hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) return fail();
+        for (Slot& sl : slots_) {
+            if (hipMalloc(&sl.d_send, kChunkBytes) != hipSuccess) return fail();
+            if (hipMalloc(&sl.d_recv, kChunkBytes) != hipSuccess) return fail();
+            if (hipHostMalloc(&sl.h_send, kChunkBytes, hipHostMallocDefault) != hipSuccess) return fail();
+            if (hipHostMalloc(&sl.h_recv, kChunkBytes, hipHostMallocDefault) != hipSuccess) return fail();
+            for (hipEvent_t* e : {&sl.in_done, &sl.comp_done, &sl.out_done})
+                if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return fail();
+        }
+        ready_ = true;
+        return DCCL_SUCCESS;
+    }
+
+    int run(const unsigned char* send, unsigned char* recv, int dtype, size_t count, int op);
+
+private:
+    int fail() { release(); return DCCL_UNHANDLED_DEVICE_ERROR; }
+    void release() {
+        for (Slot& sl : slots_) {
+            if (sl.d_send) (void)hipFree(sl.d_send);
+            if (sl.d_recv) (void)hipFree(sl.d_recv);
+            if (sl.h_send) (void)hipHostFree(sl.h_send);
+            if (sl.h_recv) (void)hipHostFree(sl.h_recv);
+            for (hipEvent_t e : {sl.in_done, sl.comp_done, sl.out_done})
+                if (e) (void)hipEventDestroy(e);
+            sl = Slot{};
+        }
+        for (hipStream_t s : {in_, comp_, out_})
+            if (s) (void)hipStreamDestroy(s);
+        in_ = comp_ = out_ = nullptr;
+        ready_ = false;
+    }
+    int drain_slot(Slot& sl) {  // finish a bounced D2H: wait, then copy to user memory
+        if (!sl.pending_dst) return DCCL_SUCCESS;
+        if (hipEventSynchronize(sl.out_done) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
+        std::memcpy(sl.pending_dst, sl.h_recv, sl.pending_bytes);
+        sl.pending_dst = nullptr;
+        sl.pending_bytes = 0;
+        return DCCL_SUCCESS;
+    }
+
+    int device_;
+    bool ready_ = false;
+    hipStream_t in_ = nullptr, comp_ = nullptr, out_ = nullptr;
+    Slot slots_[kSlots];
+};
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();  // unregistered pageable memory reports an error: clear it
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+int Stager::run(const unsigned char* send, unsigned char* recv, int dtype, size_t count, int op) {
+    const size_t esz = size_of_dtype(dtype);
+    const size_t per_chunk = kChunkBytes / esz;
+    const bool send_pinned = is_pinned(send), recv_pinned = is_pinned(recv);
+    int rc = DCCL_SUCCESS;
+    size_t k = 0;
+    for (size_t off = 0; off < count && rc == DCCL_SUCCESS; off += per_chunk, ++k) {
+        const size_t n = (count - off < per_chunk) ? count - off : per_chunk;
+        const size_t bytes = n * esz;
+        Slot& sl = slots_[k % kSlots];
+        // Slot reuse: the previous occupant's D2H must be done (and unbounced).
+        if ((rc = drain_slot(sl)) != DCCL_SUCCESS) break;
+        if (hipStreamWaitEvent(in_, sl.out_done, 0) != hipSuccess) { rc = DCCL_UNHANDLED_DEVICE_ERROR; break; }
+        const unsigned char* src_s = send + off * esz;
+        const unsigned char* src_r = recv + off * esz;
+        if (!send_pinned) { std::memcpy(sl.h_send, src_s, bytes); src_s = static_cast<unsigned char*>(sl.h_send); }
+        if (!recv_pinned) {
+            // h_recv is also the D2H landing zone of this slot: its previous use was drained above.
+            std::memcpy(sl.h_recv, src_r, bytes);
+            src_r = static_cast<unsigned char*>(sl.h_recv);
+        }
+        if (hipMemcpyAsync(sl.d_send, src_s, bytes, hipMemcpyHostToDevice, in_) != hipSuccess ||
+            hipMemcpyAsync(sl.d_recv, src_r, bytes, hipMemcpyHostToDevice, in_) != hipSuccess ||
+            hipEventRecord(sl.in_done, in_) != hipSuccess ||
+            hipStreamWaitEvent(comp_, sl.in_done, 0) != hipSuccess) {
+            rc = DCCL_UNHANDLED_DEVICE_ERROR;
+            break;
+        }
+        if ((rc = dccl_local_reduce(sl.d_send, sl.d_recv, dtype, n, op, comp_)) != DCCL_SUCCESS) break;
+        unsigned char* dst = recv + off * esz;
+        if (hipEventRecord(sl.comp_done, comp_) != hipSuccess ||
+            hipStreamWaitEvent(out_, sl.comp_done, 0) != hipSuccess ||
+            hipMemcpyAsync(recv_pinned ? dst : sl.h_recv, sl.d_recv, bytes, hipMemcpyDeviceToHost, out_) !=
+                hipSuccess ||
+            hipEventRecord(sl.out_done, out_) != hipSuccess) {
+            rc = DCCL_UNHANDLED_DEVICE_ERROR;
+            break;
+        }
+        if (!recv_pinned) { sl.pending_dst = dst; sl.pending_bytes = bytes; }
+        // With pageable send, the CPU memcpy of the next chunk into this slot's h_send must not
+        // race the in-flight H2D: wait for the copy-in of the slot we are about to reuse.
+        if (!send_pinned || !recv_pinned) {
+            Slot& next = slots_[(k + 1) % kSlots];
+            if (hipEventSynchronize(next.in_done) != hipSuccess) { rc = DCCL_UNHANDLED_DEVICE_ERROR; break; }
+        }
+    }
+    // Always drain: no slot may be left with work in flight, even after an error.
+    for (Slot& sl : slots_) {
+        const int d = drain_slot(sl);
+        if (rc == DCCL_SUCCESS) rc = d;
+    }
+    if (hipStreamSynchronize(out_) != hipSuccess && rc == DCCL_SUCCESS) rc = DCCL_UNHANDLED_DEVICE_ERROR;
+    if (hipStreamSynchronize(comp_) != hipSuccess && rc == DCCL_SUCCESS) rc = DCCL_UNHANDLED_DEVICE_ERROR;
+    return rc;
+}
+
+struct ThreadStagers {
+    std::vector<std::unique_ptr<Stager>> per_device;
+    Stager* get(int dev) {
+        if (dev < 0) return nullptr;
+        if (static_cast<size_t>(dev) >= per_device.size()) per_device.resize(dev + 1);
+        if (!per_device[dev]) per_device[dev] = std::make_unique<Stager>(dev);
+        return per_device[dev].get();
+    }
+};
+
+thread_local ThreadStagers t_stagers;
+
+}  // namespace
+}  // namespace dccl_amd
+
+using namespace dccl_amd;
+
+extern "C" int dccl_local_reduce_host(const void* send, void* recv, int dtype, size_t count, int op) {
+    const int v = validate(dtype, op);
+    if (v != DCCL_SUCCESS) return v;
+    if (count == 0) return DCCL_SUCCESS;
+    if (send == nullptr || recv == nullptr) return DCCL_INVALID_ARGUMENT;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
+    Stager* st = t_stagers.get(dev);
+    if (st == nullptr) return DCCL_UNHANDLED_DEVICE_ERROR;
+    int rc = st->init();
+    if (rc != DCCL_SUCCESS) return rc;
+    rc = st->run(static_cast<const unsigned char*>(send), static_cast<unsigned char*>(recv), dtype, count, op);
+    (void)hipSetDevice(dev);
+    return rc;
+}
+
+extern "C" int dccl_register_host_memory(void* buffer, size_t size) {
+    if (buffer == nullptr || size == 0) return DCCL_INVALID_ARGUMENT;
+    return hipHostRegister(buffer, size, hipHostRegisterDefault) == hipSuccess ? DCCL_SUCCESS
+                                                                               : DCCL_UNHANDLED_DEVICE_ERROR;
+}
+
+extern "C" int dccl_deregister_host_memory(void* buffer) {
+    if (buffer == nullptr) return DCCL_INVALID_ARGUMENT;
+    return hipHostUnregister(buffer) == hipSuccess ? DCCL_SUCCESS : DCCL_UNHANDLED_DEVICE_ERROR;
+}
+
+extern "C" size_t dccl_size_of_type(int dtype) { return size_of_dtype(dtype); }
+
+extern "C" const char* dccl_result_string(int result) {
+    switch (result) {
+    case 0: return "ncclSuccess";
+    case 1: return "ncclUnhandledCudaError (HIP runtime failure)";
+    case 2: return "ncclSystemError";
+    case 3: return "ncclInternalError";
+    case 4: return "ncclInvalidArgument";
+    case 5: return "ncclInvalidUsage";
+    case 6: return "ncclRemoteError";
+    case 7: return "ncclInProgress";
+    default: return "unknown result";
+    }
+}
+
+extern "C" int dccl_version(void) { return 1 * 10000 + 0 * 100 + 0; }

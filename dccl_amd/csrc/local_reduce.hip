@@ -1,0 +1,371 @@
+// dccl_amd/csrc/local_reduce.hip — the MI355X (gfx950) local bucket-reduction combine.
+//
+//   recv[i] = op(recv[i], send[i]),  i in [0, count)
+//
+// Replaces the reference's single CUDA kernel reduce_kernel<DT> and its launcher
+// do_device_reduce (/root/reference/src/core/reduce.cu:9-100).  That kernel moves one
+// scalar element per thread per iteration through a runtime op switch on a grid of
+// num_SMs x 256 threads; this one is an HBM stream:
+//   * 16-byte (global_load_dwordx4 / global_store_dwordx4) accesses of both operands,
+//     UNROLL vectors per thread in flight before the first use, 256-thread blocks,
+//     one 16 KiB (x UNROLL/4) tile of each operand per block, >> 256 blocks per launch;
+//   * dtype and op are template parameters (no per-element switch);
+//   * the single-use `send` stream is read with non-temporal loads;
+//   * unaligned head / tail elements are folded into block 0 of the same launch.
+// No LDS and no MFMA: each element is touched once (BASELINE.json north_star).
+//
+// Roofline: HBM, 3 * count * sizeof(T) algorithmic bytes (read send, read recv, write recv).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+
+#include "combine.hpp"
+#include "dccl/dccl_reduce.h"
+#include "dccl/dccl_reduce_tuning.h"
+#include "dispatch.hpp"
+
+namespace dccl_amd {
+
+constexpr int kBlock = 256;
+
+// Cache policy bits of the vector kernel.
+enum : int {
+    kNtSend = 1,   // non-temporal load of send (read once)
+    kNtRecv = 2,   // non-temporal load of recv
+    kNtStore = 4,  // non-temporal store of recv
+};
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+// Scalar element access that is correct for any alignment of the operand bases.
+template <typename T, bool ALIGNED>
+__device__ __forceinline__ T ld_elem(const unsigned char* base, size_t i) {
+    if constexpr (ALIGNED) return reinterpret_cast<const T*>(base)[i];
+    T v;
+    __builtin_memcpy(&v, base + i * sizeof(T), sizeof(T));
+    return v;
+}
+template <typename T, bool ALIGNED>
+__device__ __forceinline__ void st_elem(unsigned char* base, size_t i, T v) {
+    if constexpr (ALIGNED) { reinterpret_cast<T*>(base)[i] = v; return; }
+    __builtin_memcpy(base + i * sizeof(T), &v, sizeof(T));
+}
+
+// ---------------------------------------------------------------------------------
+// Vector kernel.  Operands are split as [head scalars | nvec 16-B vectors | tail
+// scalars]; head aligns recv (and, by construction, send) to 16 B.
+// ---------------------------------------------------------------------------------
+template <typename T, int OP, int UNROLL, int POLICY>
+__device__ __forceinline__ void full_tile(const u32x4* __restrict__ vs, u32x4* __restrict__ vr, size_t base) {
+    u32x4 s[UNROLL], r[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) s[u] = ld16<(POLICY & kNtSend) != 0>(vs + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) r[u] = ld16<(POLICY & kNtRecv) != 0>(vr + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+        const u32x4 o = combine16<T, OP>(r[u], s[u]);
+        if constexpr ((POLICY & kNtStore) != 0) __builtin_nontemporal_store(o, vr + base + u * kBlock);
+        else vr[base + u * kBlock] = o;
+    }
+}
+
+template <typename T, int OP, int UNROLL, int POLICY>
+__device__ __noinline__ void partial_tile(const u32x4* __restrict__ vs, u32x4* __restrict__ vr, size_t base,
+                                          size_t nvec) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+        const size_t i = base + u * kBlock;
+        if (i < nvec) vr[i] = combine16<T, OP>(vr[i], vs[i]);
+    }
+}
+
+template <typename T, int OP, int UNROLL, int POLICY>
+__global__ __launch_bounds__(kBlock) void reduce_vec_kernel(const unsigned char* __restrict__ send,
+                                                            unsigned char* __restrict__ recv,
+                                                            size_t head, size_t nvec, size_t tail) {
+    constexpr size_t kTile = size_t(kBlock) * UNROLL;
+    const u32x4* __restrict__ vs = reinterpret_cast<const u32x4*>(send + head * sizeof(T));
+    u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
+    const size_t nfull = nvec / kTile;
+
+    // Full tiles: no bounds checks, all 2*UNROLL loads in flight before the first use.
+    for (size_t t = blockIdx.x; t < nfull; t += gridDim.x)
+        full_tile<T, OP, UNROLL, POLICY>(vs, vr, t * kTile + threadIdx.x);
+
+    // The partial last tile goes to the block after the last full one (mod grid).
+    if (nfull * kTile < nvec && blockIdx.x == nfull % gridDim.x)
+        partial_tile<T, OP, UNROLL, POLICY>(vs, vr, nfull * kTile + threadIdx.x, nvec);
+
+    // Scalar head [0, head) and tail [head + nvec*V, count): < 16 elements each.
+    if (blockIdx.x == 0 && threadIdx.x < head + tail) {
+        const size_t i = threadIdx.x < head ? threadIdx.x
+                                            : head + nvec * Pack<T>::N + (threadIdx.x - head);
+        const T a = ld_elem<T, true>(recv, i), b = ld_elem<T, true>(send, i);
+        st_elem<T, true>(recv, i, Combine<T, OP>::apply(a, b));
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Scalar fallback for operands whose 16-B phases differ (ALIGNED) or that are not
+// even element-aligned (!ALIGNED).  Grid-stride, 4 independent elements per thread.
+// ---------------------------------------------------------------------------------
+template <typename T, int OP, bool ALIGNED>
+__global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(const unsigned char* __restrict__ send,
+                                                               unsigned char* __restrict__ recv,
+                                                               size_t count) {
+    const size_t stride = size_t(gridDim.x) * kBlock;
+    for (size_t i0 = size_t(blockIdx.x) * kBlock * 4 + threadIdx.x; i0 < count; i0 += stride * 4) {
+        T a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t i = i0 + u * kBlock;
+            if (i < count) { a[u] = ld_elem<T, ALIGNED>(recv, i); b[u] = ld_elem<T, ALIGNED>(send, i); }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t i = i0 + u * kBlock;
+            if (i < count) st_elem<T, ALIGNED>(recv, i, Combine<T, OP>::apply(a[u], b[u]));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// k-way vector kernel: recv = op(...op(op(recv, s0), s1)..., s{K-1}), one pass.
+// ---------------------------------------------------------------------------------
+struct SendList { const unsigned char* p[8]; };
+
+template <typename T, int OP, int K>
+__global__ __launch_bounds__(kBlock) void reduce_multi_vec_kernel(SendList sends, unsigned char* __restrict__ recv,
+                                                                  size_t head, size_t nvec, size_t tail) {
+    constexpr int UNROLL = 2;
+    constexpr size_t kTile = size_t(kBlock) * UNROLL;
+    u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
+    const size_t ntiles = (nvec + kTile - 1) / kTile;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t base = t * kTile + threadIdx.x;
+        u32x4 r[UNROLL], s[K][UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const size_t i = base + u * kBlock;
+            if (i < nvec) {
+                r[u] = vr[i];
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    s[k][u] = __builtin_nontemporal_load(
+                        reinterpret_cast<const u32x4*>(sends.p[k] + head * sizeof(T)) + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const size_t i = base + u * kBlock;
+            if (i < nvec) {
+                u32x4 acc = r[u];
+#pragma unroll
+                for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, s[k][u]);
+                vr[i] = acc;
+            }
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < head + tail) {
+        const size_t i = threadIdx.x < head ? threadIdx.x
+                                            : head + nvec * Pack<T>::N + (threadIdx.x - head);
+        T acc = ld_elem<T, true>(recv, i);
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, true>(sends.p[k], i));
+        st_elem<T, true>(recv, i, acc);
+    }
+}
+
+template <typename T, int OP, bool ALIGNED>
+__global__ __launch_bounds__(kBlock) void reduce_multi_scalar_kernel(SendList sends, int nsend,
+                                                                     unsigned char* __restrict__ recv,
+                                                                     size_t count) {
+    const size_t stride = size_t(gridDim.x) * kBlock;
+    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < count; i += stride) {
+        T acc = ld_elem<T, ALIGNED>(recv, i);
+        for (int k = 0; k < nsend; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, ALIGNED>(sends.p[k], i));
+        st_elem<T, ALIGNED>(recv, i, acc);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Host-side launch helpers
+// ---------------------------------------------------------------------------------
+namespace {
+
+// Default configuration of the shipped kernel (chosen by tools/tune on MI355X).
+constexpr int kDefaultUnroll = 4;
+constexpr int kDefaultPolicy = kNtSend;
+constexpr size_t kMaxGrid = size_t(1) << 22;  // grid-stride beyond this
+
+inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream) {
+    if (grid == 0) return DCCL_SUCCESS;
+    if (grid > kMaxGrid) grid = kMaxGrid;
+    const hipError_t e = hipLaunchKernel(fn, dim3(static_cast<unsigned>(grid)), dim3(kBlock), args, 0, stream);
+    return e == hipSuccess ? DCCL_SUCCESS : DCCL_UNHANDLED_DEVICE_ERROR;
+}
+
+inline size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }
+
+struct Split {
+    size_t head, nvec, tail;
+};
+
+template <typename T>
+inline Split split_for_vectors(uintptr_t recv, size_t count) {
+    constexpr size_t V = Pack<T>::N;
+    size_t head = ((16 - (recv & 15)) & 15) / sizeof(T);
+    if (head > count) head = count;
+    const size_t rest = count - head;
+    const size_t nvec = rest / V;
+    return Split{head, nvec, rest - nvec * V};
+}
+
+template <typename T, int OP, int UNROLL, int POLICY>
+int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t stream, size_t grid_cap) {
+    size_t grid = ceil_div(sp.nvec, size_t(kBlock) * UNROLL);
+    if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    if (grid_cap && grid > grid_cap) grid = grid_cap;
+    void* args[] = {&s, &r, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&reduce_vec_kernel<T, OP, UNROLL, POLICY>), grid, args, stream);
+}
+
+template <typename T, int OP>
+int launch_scalar(const unsigned char* s, unsigned char* r, size_t count, bool elem_aligned, hipStream_t stream) {
+    const size_t grid = ceil_div(count, size_t(kBlock) * 4);
+    void* args[] = {&s, &r, &count};
+    const void* fn = elem_aligned ? reinterpret_cast<const void*>(&reduce_scalar_kernel<T, OP, true>)
+                                  : reinterpret_cast<const void*>(&reduce_scalar_kernel<T, OP, false>);
+    return launch(fn, grid, args, stream);
+}
+
+template <typename T, int OP>
+int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream) {
+    const auto s = static_cast<const unsigned char*>(send);
+    const auto r = static_cast<unsigned char*>(recv);
+    const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
+    if ((as | ar) % sizeof(T)) return launch_scalar<T, OP>(s, r, count, false, stream);
+    if ((as ^ ar) & 15) return launch_scalar<T, OP>(s, r, count, true, stream);
+    return launch_vec<T, OP, kDefaultUnroll, kDefaultPolicy>(s, r, split_for_vectors<T>(ar, count), stream, 0);
+}
+
+template <typename T, int OP, int K>
+int launch_multi_vec(SendList sl, unsigned char* r, Split sp, hipStream_t stream) {
+    size_t grid = ceil_div(sp.nvec, size_t(kBlock) * 2);
+    if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K>), grid, args, stream);
+}
+
+template <typename T, int OP>
+int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t count, hipStream_t stream) {
+    SendList sl{};
+    const uintptr_t ar = reinterpret_cast<uintptr_t>(recv);
+    bool vec_ok = (ar % sizeof(T)) == 0, elem_ok = vec_ok;
+    for (int k = 0; k < nsend; ++k) {
+        sl.p[k] = static_cast<const unsigned char*>(sends[k]);
+        const uintptr_t a = reinterpret_cast<uintptr_t>(sends[k]);
+        if (a % sizeof(T)) elem_ok = vec_ok = false;
+        if ((a ^ ar) & 15) vec_ok = false;
+    }
+    auto r = static_cast<unsigned char*>(recv);
+    if (!vec_ok) {
+        const size_t grid = ceil_div(count, size_t(kBlock));
+        void* args[] = {&sl, &nsend, &r, &count};
+        const void* fn = elem_ok ? reinterpret_cast<const void*>(&reduce_multi_scalar_kernel<T, OP, true>)
+                                 : reinterpret_cast<const void*>(&reduce_multi_scalar_kernel<T, OP, false>);
+        return launch(fn, grid, args, stream);
+    }
+    const Split sp = split_for_vectors<T>(ar, count);
+    switch (nsend) {
+    case 1: return launch_multi_vec<T, OP, 1>(sl, r, sp, stream);
+    case 2: return launch_multi_vec<T, OP, 2>(sl, r, sp, stream);
+    case 3: return launch_multi_vec<T, OP, 3>(sl, r, sp, stream);
+    case 4: return launch_multi_vec<T, OP, 4>(sl, r, sp, stream);
+    case 5: return launch_multi_vec<T, OP, 5>(sl, r, sp, stream);
+    case 6: return launch_multi_vec<T, OP, 6>(sl, r, sp, stream);
+    case 7: return launch_multi_vec<T, OP, 7>(sl, r, sp, stream);
+    case 8: return launch_multi_vec<T, OP, 8>(sl, r, sp, stream);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+
+struct ReduceFn {
+    template <typename T, int OP>
+    static int run(const void* send, void* recv, size_t count, hipStream_t stream) {
+        return reduce_typed<T, OP>(send, recv, count, stream);
+    }
+};
+
+struct ReduceMultiFn {
+    template <typename T, int OP>
+    static int run(const void* const* sends, int nsend, void* recv, size_t count, hipStream_t stream) {
+        return reduce_multi_typed<T, OP>(sends, nsend, recv, count, stream);
+    }
+};
+
+}  // namespace
+}  // namespace dccl_amd
+
+using namespace dccl_amd;
+
+extern "C" int dccl_local_reduce(const void* send, void* recv, int dtype, size_t count, int op, void* stream) {
+    const int v = validate(dtype, op);
+    if (v != DCCL_SUCCESS) return v;
+    if (count == 0) return DCCL_SUCCESS;
+    if (send == nullptr || recv == nullptr) return DCCL_INVALID_ARGUMENT;
+    return dispatch<ReduceFn>(dtype, op, send, recv, count, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dccl_local_reduce_multi(const void* const* sends, int nsend, void* recv, int dtype, size_t count,
+                                       int op, void* stream) {
+    const int v = validate(dtype, op);
+    if (v != DCCL_SUCCESS) return v;
+    if (nsend < 1 || nsend > 8 || sends == nullptr) return DCCL_INVALID_ARGUMENT;
+    if (count == 0) return DCCL_SUCCESS;
+    if (recv == nullptr) return DCCL_INVALID_ARGUMENT;
+    for (int k = 0; k < nsend; ++k)
+        if (sends[k] == nullptr) return DCCL_INVALID_ARGUMENT;
+    return dispatch<ReduceMultiFn>(dtype, op, sends, nsend, recv, count, static_cast<hipStream_t>(stream));
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning entry: fp32 Sum with an explicit kernel variant (include/dccl/dccl_reduce_tuning.h).
+// ---------------------------------------------------------------------------------
+namespace {
+template <int UNROLL>
+int tune_policy(int policy, const unsigned char* s, unsigned char* r, Split sp, hipStream_t st, size_t cap) {
+    switch (policy) {
+    case 0: return launch_vec<float, kSum, UNROLL, 0>(s, r, sp, st, cap);
+    case 1: return launch_vec<float, kSum, UNROLL, 1>(s, r, sp, st, cap);
+    case 3: return launch_vec<float, kSum, UNROLL, 3>(s, r, sp, st, cap);
+    case 5: return launch_vec<float, kSum, UNROLL, 5>(s, r, sp, st, cap);
+    case 7: return launch_vec<float, kSum, UNROLL, 7>(s, r, sp, st, cap);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+}  // namespace
+
+extern "C" int dccl_tune_reduce_f32_sum(const void* send, void* recv, size_t count, int unroll, int policy,
+                                        size_t grid_cap, void* stream) {
+    if (count == 0) return DCCL_SUCCESS;
+    const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
+    if (((as | ar) & 3) || ((as ^ ar) & 15)) return DCCL_INVALID_ARGUMENT;
+    const auto s = static_cast<const unsigned char*>(send);
+    const auto r = static_cast<unsigned char*>(recv);
+    const Split sp = split_for_vectors<float>(ar, count);
+    const auto st = static_cast<hipStream_t>(stream);
+    switch (unroll) {
+    case 1: return tune_policy<1>(policy, s, r, sp, st, grid_cap);
+    case 2: return tune_policy<2>(policy, s, r, sp, st, grid_cap);
+    case 4: return tune_policy<4>(policy, s, r, sp, st, grid_cap);
+    case 8: return tune_policy<8>(policy, s, r, sp, st, grid_cap);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}

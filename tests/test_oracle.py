@@ -1,0 +1,197 @@
+"""CPU tests: the oracle restatement is pinned to the reference and to the golden fixtures.
+
+Pinning chain (DESIGN.md "Oracle"):
+  reference do_host_reduce (compiled from /root/reference, oracle/_ref)  ==  oracle/host_reduce.c
+  reference outputs frozen in tests/golden/host_reduce_ref.npz            ==  oracle/host_reduce.c
+  numpy float16 / torch bfloat16 (tests/golden/host_reduce_half.npz)      ==  oracle/host_reduce.c
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from tests import ringsim
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+HOST_DTYPES = [0, 1, 2, 3, 4, 5, 7, 8]
+
+
+def fp_equal(a: np.ndarray, b: np.ndarray, dt: int) -> bool:
+    """Bit-exact, except that any NaN matches any NaN (payloads are not part of the contract)."""
+    if a.tobytes() == b.tobytes():
+        return True
+    if dt in (6, 9):
+        fa = a.astype(np.uint32)
+        exp = 0x7C00 if dt == 6 else 0x7F80
+        mask = 0x03FF if dt == 6 else 0x007F
+        na = ((a & exp) == exp) & ((a & mask) != 0)
+        nb = ((b & exp) == exp) & ((b & mask) != 0)
+        return bool(np.array_equal(na, nb) and np.array_equal(fa[~na], b.astype(np.uint32)[~nb]))
+    if dt in (7, 8):
+        na, nb = np.isnan(a), np.isnan(b)
+        return bool(np.array_equal(na, nb) and a[~na].tobytes() == b[~nb].tobytes())
+    return False
+
+
+def with_pad(a: np.ndarray, pad: int) -> np.ndarray:
+    """The view plus the ``pad`` slack elements that follow it (see oracle.aligned_empty)."""
+    start = a.ctypes.data - a.base.ctypes.data
+    return a.base[start:start + (a.size + pad) * a.itemsize]
+
+
+def test_restatement_matches_golden_fixtures():
+    z = np.load(os.path.join(GOLDEN, "host_reduce_ref.npz"))
+    checked = 0
+    for key in z.files:
+        if not key.endswith("_out"):
+            continue
+        d, n, o, _ = key.split("_")
+        dt, op = int(d[1:]), int(o[2:])
+        send = z[f"{d}_{n}_send"]
+        recv = oracle.aligned_empty(send.size, send.dtype)
+        recv[:] = z[f"{d}_{n}_recv"]
+        assert oracle.host_reduce(np.ascontiguousarray(send), recv, dt, op) == 0
+        assert recv.tobytes() == z[key].tobytes(), key
+        checked += 1
+    assert checked == 8 * 7 * 4
+
+
+def test_restatement_matches_half_fixtures():
+    z = np.load(os.path.join(GOLDEN, "host_reduce_half.npz"))
+    for key in z.files:
+        if not key.endswith("_out"):
+            continue
+        d, n, o, _ = key.split("_")
+        dt, op = int(d[1:]), int(o[2:])
+        out = oracle.combine(z[f"{d}_{n}_send"], z[f"{d}_{n}_recv"], dt, op)
+        assert fp_equal(out, z[key], dt), key
+
+
+def test_return_codes_match_reference_fixture():
+    cases = json.load(open(os.path.join(GOLDEN, "rc_cases.json")))
+    for c in cases:
+        npd = oracle.NP_DTYPES[c["dtype"]]
+        s = oracle.aligned_empty(max(c["count"], 1), npd)
+        r = oracle.aligned_empty(max(c["count"], 1), npd)
+        assert oracle.host_reduce(s, r, c["dtype"], c["op"], count=c["count"]) == c["rc"], c
+
+
+@pytest.mark.skipif(oracle.reference() is None, reason="oracle/_ref not built (no /root/reference)")
+@pytest.mark.parametrize("dt", HOST_DTYPES)
+def test_restatement_matches_reference_fuzz(dt):
+    rng = np.random.default_rng(1234 + dt)
+    npd = oracle.NP_DTYPES[dt]
+    for op in range(6):
+        for n in [0, 1, 7, 63, 64, 65, 129, 1000, 4099]:
+            if np.issubdtype(npd, np.integer):
+                info = np.iinfo(npd)
+                s = rng.integers(info.min, info.max, n, dtype=npd, endpoint=True)
+                r = rng.integers(info.min, info.max, n, dtype=npd, endpoint=True)
+            else:
+                s = (rng.standard_normal(n) * 1e3).astype(npd)
+                r = (rng.standard_normal(n) * 1e3).astype(npd)
+            for off in [0, np.dtype(npd).itemsize * 3]:  # 64-B aligned and misaligned recv
+                # pad so the reference's misalignment overrun stays in bounds
+                a = oracle.aligned_empty(n, npd, offset_bytes=off, pad_elems=64)
+                b = oracle.aligned_empty(n, npd, offset_bytes=off, pad_elems=64)
+                sa = oracle.aligned_empty(n, npd, offset_bytes=off, pad_elems=64)
+                a[:] = r
+                b[:] = r
+                sa[:] = s
+                assert oracle.host_reduce(sa, a, dt, op) == oracle.ref_reduce(sa, b, dt, op)
+                assert with_pad(a, 64).tobytes() == with_pad(b, 64).tobytes(), (dt, op, n, off)
+
+
+def test_misalignment_overrun_is_reproduced():
+    """fp32, recv 32 B past a line, count 100 -> 12 elements combined twice."""
+    n = 100
+    s = oracle.aligned_empty(n, np.float32, offset_bytes=32, pad_elems=32)
+    r = oracle.aligned_empty(n, np.float32, offset_bytes=32, pad_elems=32)
+    s[:] = 1.0
+    r[:] = 0.0
+    assert oracle.host_reduce(s, r, 7, 0) == 0
+    assert int((r == 2.0).sum()) == 12  # the tail re-applied
+    exp = oracle.aligned_empty(n, np.float32)
+    exp[:] = 0.0
+    sx = oracle.aligned_empty(n, np.float32)
+    sx[:] = 1.0
+    oracle.expected_reduce(sx, exp, 7, 0)
+    assert np.all(exp == 1.0)
+
+
+def test_edge_semantics():
+    """Known answers of SURVEY.md 8(c)."""
+    def one(dt, op, r, s):
+        npd = oracle.NP_DTYPES[dt]
+        return oracle.combine(np.array([s], npd), np.array([r], npd), dt, op)[0]
+    assert one(0, 0, 100, 100) == -56
+    assert one(0, 1, 100, 3) == 44
+    assert one(2, 0, 2**31 - 1, 1) == -2**31
+    assert np.isnan(one(7, 3, np.nan, 1.0))
+    assert one(7, 3, 1.0, np.nan) == 1.0
+    assert one(7, 2, 2.0, np.nan) == 2.0
+    z = one(7, 3, 0.0, -0.0)
+    assert z == 0 and not np.signbit(z)
+    z = one(7, 2, -0.0, 0.0)
+    assert z == 0 and np.signbit(z)
+
+
+def test_half_conversions_against_numpy():
+    lib = oracle.restatement()
+    bits = np.arange(0, 1 << 16, dtype=np.uint32).astype(np.uint16)
+    f = bits.view(np.float16).astype(np.float32)
+    got = np.array([lib.oracle_half_to_float(int(b)) for b in bits[::97]], dtype=np.float32)
+    ref = f[::97]
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert got[~np.isnan(got)].tobytes() == ref[~np.isnan(ref)].tobytes()
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.standard_normal(3000).astype(np.float32) * 10.0 ** rng.integers(-9, 6, 3000),
+                         np.array([65504.0, 65520.0, 65519.99, 2.98e-8, 2.99e-8, 5.96e-8, -0.0, np.inf],
+                                  dtype=np.float32)]).astype(np.float32)
+    with np.errstate(over="ignore"):
+        want = xs.astype(np.float16).view(np.uint16)
+    got = np.array([lib.oracle_float_to_half(float(x)) for x in xs], dtype=np.uint16)
+    assert np.array_equal(got, want)
+
+
+def test_bf16_conversion_against_torch():
+    torch = pytest.importorskip("torch")
+    lib = oracle.restatement()
+    rng = np.random.default_rng(8)
+    xs = np.concatenate([rng.standard_normal(3000).astype(np.float32) * 10.0 ** rng.integers(-38, 38, 3000),
+                         np.array([3.4e38, -0.0, np.inf, 1e-40, 1.0000001], dtype=np.float32)])
+    xs = xs.astype(np.float32)
+    want = torch.from_numpy(xs).bfloat16().view(torch.int16).numpy().view(np.uint16)
+    got = np.array([lib.oracle_float_to_bf16(float(x)) for x in xs], dtype=np.uint16)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("kind", ["float32", "uint32"])
+def test_c1_ring_goldens_with_oracle(kind):
+    """The dccl_cli all_reduce known answers, reproduced by the ring choreography + oracle."""
+    g = json.load(open(os.path.join(GOLDEN, "c1_ring.json")))
+    W, n = g["world_size"], g["count"]
+    dt = 7 if kind == "float32" else 3
+    npd = oracle.NP_DTYPES[dt]
+    bufs = []
+    for r in range(W):
+        b = oracle.aligned_empty(n, npd)
+        b.view(np.uint8)[:] = r  # memset(sendbuf, rank), cli.cpp:380
+        bufs.append(b)
+
+    def combine(send, recv):
+        assert oracle.host_reduce(np.ascontiguousarray(send), recv, dt, 0) == 0
+
+    def copy(dst, src):
+        dst[:] = src
+
+    done = 0
+    for target in sorted(int(k) for k in g[kind]):
+        while done < target:
+            ringsim.ring_allreduce(bufs, combine, copy)
+            done += 1
+        want = int(g[kind][str(target)], 16)
+        for b in bufs:
+            assert np.all(b.view(np.uint32) == want), (kind, target, hex(int(b.view(np.uint32)[0])))
