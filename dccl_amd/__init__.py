@@ -75,7 +75,7 @@ def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"dccl_amd: native library {LIB_PATH} is missing; build it with "
-            "`python -m dccl_amd.build` (hipcc, gfx950). There is no CPU fallback.")
+            "`python dccl_amd/build.py` (hipcc, gfx950). There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH)
     c_int, c_size_t, c_void_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
     sig = {
@@ -88,7 +88,10 @@ def _load():
         "dccl_size_of_type": (c_size_t, [c_int]),
         "dccl_result_string": (ctypes.c_char_p, [c_int]),
         "dccl_version": (c_int, []),
-        "dccl_tune_reduce_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_size_t, c_void_p]),
+        "dccl_tune_reduce_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_size_t, c_void_p]),
+        "dccl_tune_num_variants": (c_int, []),
+        "dccl_tune_asm_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+        "dccl_tune_variant_info": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -103,8 +106,18 @@ lib = _load()
 EXPORTED_SYMBOLS = [
     "dccl_local_reduce", "dccl_local_reduce_multi", "dccl_local_reduce_host",
     "dccl_register_host_memory", "dccl_deregister_host_memory", "dccl_size_of_type",
-    "dccl_result_string", "dccl_version", "dccl_tune_reduce_f32_sum",
+    "dccl_result_string", "dccl_version", "dccl_tune_reduce_f32_sum", "dccl_tune_num_variants",
+    "dccl_tune_variant_info", "dccl_tune_asm_f32_sum",
 ]
+
+
+def tune_variants() -> list[dict]:
+    out = []
+    for v in range(lib.dccl_tune_num_variants()):
+        vals = [ctypes.c_int() for _ in range(4)]
+        lib.dccl_tune_variant_info(v, *[ctypes.byref(x) for x in vals])
+        out.append(dict(zip(("block", "unroll", "policy", "xcd"), (x.value for x in vals))))
+    return out
 
 
 def result_string(code: int) -> str:

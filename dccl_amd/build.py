@@ -5,7 +5,7 @@ C++ ``namespace dccl`` API (include/dccl/dccl.hpp).  Sources compile in parallel
 link is a plain ``hipcc -shared``.  No fast-math / FTZ flags: the combine must keep
 fp32/fp16 denormals (SURVEY.md §7 "Bit-exact semantics").
 
-    python -m dccl_amd.build [--force]
+    python dccl_amd/build.py [--force]      (by path: importing the package loads the library)
 """
 from __future__ import annotations
 
@@ -20,6 +20,9 @@ CSRC = os.path.join(PKG, "csrc")
 OUT_DIR = os.path.join(PKG, "lib")
 OBJ_DIR = os.path.join(ROOT, "build", "obj")
 LIB = os.path.join(OUT_DIR, "libdccl_amd.so")
+BIN_DIR = os.path.join(PKG, "bin")
+CLI_SRC = os.path.join(ROOT, "tools", "dccl_cli.cpp")
+CLI = os.path.join(BIN_DIR, "dccl_cli")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DCCL_OFFLOAD_ARCH", "gfx950")
 
@@ -64,6 +67,12 @@ def build(force: bool = False) -> str:
         subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp,
                         "-Wl,-soname,libdccl_amd.so"], check=True)
         os.replace(tmp, LIB)
+    # the dccl_cli harness (C++ on the namespace-dccl API), rpath'd to the in-tree library
+    os.makedirs(BIN_DIR, exist_ok=True)
+    if force or not os.path.exists(CLI) or os.path.getmtime(CLI) < max(os.path.getmtime(LIB),
+                                                                          os.path.getmtime(CLI_SRC)):
+        subprocess.run([HIPCC, *COMMON, CLI_SRC, "-o", CLI, f"-L{OUT_DIR}", "-ldccl_amd",
+                        "-Wl,-rpath,$ORIGIN/../lib", "-pthread"], check=True)
     return LIB
 
 

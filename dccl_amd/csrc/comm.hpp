@@ -1,0 +1,116 @@
+// dccl_amd/csrc/comm.hpp — communicator and rank-to-rank transport of the MI355X build.
+//
+// The reference moves chunks between ranks with Derecho's out-of-band RDMA
+// (dccl_oob_send / dccl_oob_recv / wait, /root/reference/src/core/internal_common.hpp:698-792):
+// a send posts a buffer, the peer's recv lands it in the peer's buffer, and both sides wait.
+// Here the ranks of a group are threads of one process (one per GPU on a node, or several
+// on one GPU for tests) and the same four verbs are implemented as:
+//   send(peer, buf)    post {buf, ready-event recorded on the sender's stream} to peer
+//   recv(peer, dst)    take the matching post; device: the receiver's stream waits on the
+//                      ready event and copies D2D (an xGMI peer copy across GPUs); host: memcpy;
+//                      then acknowledge with a done-event
+//   wait_send(peer)    take the acknowledgement; device: the sender's stream waits on the
+//                      done event, so later writes to the buffer are ordered after the copy
+//   wait_recv(peer)    nothing left to do: the copy is already stream-ordered
+// No host-side stream synchronisation happens between ring steps (the reference syncs the
+// stream after every device combine, reduce_scatter_ring.cpp:88 — SURVEY.md §8(f) row 2).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "dccl/dccl.hpp"
+
+namespace dccl_amd {
+
+struct Message {
+    const void* ptr = nullptr;
+    size_t bytes = 0;
+    bool device = false;
+    hipEvent_t ready = nullptr;  // recorded on the sender's stream (device messages)
+};
+
+struct Ack {
+    hipEvent_t done = nullptr;  // recorded on the receiver's stream after its copy
+};
+
+// One directed channel src -> dst: messages flow forward, acknowledgements back.
+struct Channel {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Message> msgs;
+    std::deque<Ack> acks;
+};
+
+class Group {
+public:
+    explicit Group(uint32_t world);
+    uint32_t world() const { return world_; }
+    Channel& channel(uint32_t src, uint32_t dst) { return *chan_[src * world_ + dst]; }
+    // Rendezvous: blocks until every rank arrived (used by init / finalize).
+    void barrier();
+
+    // join bookkeeping (guarded by the registry mutex)
+    std::vector<bool> taken;
+    uint32_t joined = 0;
+    uint32_t left = 0;
+
+private:
+    uint32_t world_;
+    std::vector<std::unique_ptr<Channel>> chan_;
+    std::mutex bmu_;
+    std::condition_variable bcv_;
+    uint32_t barrier_count_ = 0;
+    uint64_t barrier_gen_ = 0;
+};
+
+}  // namespace dccl_amd
+
+// The opaque communicator of include/dccl/dccl.hpp.
+struct dccl::dcclComm {
+    std::shared_ptr<dccl_amd::Group> group;
+    uint32_t rank = 0;
+    uint32_t world = 1;
+    int device = -1;  // HIP device current at init
+    // Per-peer event pairs for the stream-ordered device transport (reused every step:
+    // a stream wait captures the event's state at the time of the wait).
+    std::vector<hipEvent_t> ready_events;  // indexed by destination rank
+    std::vector<hipEvent_t> done_events;   // indexed by source rank
+    // Scratchpads (the reference keeps thread_local ones, /root/reference/src/core/dccl.cpp:57-84)
+    void* dev_scratch = nullptr;
+    size_t dev_scratch_bytes = 0;
+    void* host_scratch = nullptr;
+    size_t host_scratch_bytes = 0;
+    void* dev_work = nullptr;  // full-size work buffer (ReduceScatter's copy of sendbuff)
+    size_t dev_work_bytes = 0;
+    void* host_work = nullptr;
+    size_t host_work_bytes = 0;
+};
+
+namespace dccl_amd {
+
+using dccl::ncclResult_t;
+
+// Transport verbs (see the file comment).  `stream` is used for device messages only.
+ncclResult_t xport_send(dccl::dcclComm* c, uint32_t peer, const void* buf, size_t bytes, bool device,
+                        hipStream_t stream);
+ncclResult_t xport_recv(dccl::dcclComm* c, uint32_t peer, void* dst, size_t bytes, bool device,
+                        hipStream_t stream);
+ncclResult_t xport_wait_send(dccl::dcclComm* c, uint32_t peer, bool device, hipStream_t stream);
+
+// Scratch management (grown on demand, page/line rounded; never shrinks until finalize).
+ncclResult_t ensure_scratch(dccl::dcclComm* c, size_t bytes, bool device);
+ncclResult_t ensure_work(dccl::dcclComm* c, size_t bytes, bool device);
+
+// Local combine on either side of the host/device boundary.
+ncclResult_t combine(const void* send, void* recv, int dtype, size_t count, int op, bool device,
+                     hipStream_t stream);
+
+}  // namespace dccl_amd

@@ -1,0 +1,338 @@
+// dccl_amd/csrc/dccl_api.cpp — the namespace-dccl API (include/dccl/dccl.hpp) of the MI355X build.
+//
+// Entry glue mirrors /root/reference/src/core/dccl.cpp:
+//   ncclAllReduce      :344-501  host/device decision by pointer attributes, in-place copy,
+//                                scratchpad sizing (total/W), ring algorithm
+//   ncclReduceScatter  :551-698  full-size copy of sendbuff, ring RS with rank maps
+//                                (orank+W-1)%W / (nrank+1)%W, copy slot `rank` out
+//   ncclReduce         :745-846  ring RS with the same maps, then gather slots at root
+//   ncclAllGather      :849-862  copy into own slot, ring AG
+//   ncclSend/Recv      :865-911  one transfer, waited
+//   ncclBroadcast/Bcast:701-743  root -> every rank
+// Deliberate differences: op/dtype are validated before any buffer is touched
+// (ncclAvg -> ncclInvalidUsage even at W = 1; unknown dtype -> ncclInvalidArgument), a null comm
+// throws std::runtime_error for every call (the reference's VALIDATE_COMM, dccl.cpp:32-36),
+// device paths are stream-ordered (no per-step stream sync), and every API supports device
+// buffers.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
+#include "algorithms.hpp"
+#include "comm.hpp"
+#include "dccl/dccl.hpp"
+#include "dccl/dccl_reduce.h"
+
+using dccl::dcclComm;
+using dccl::ncclResult_t;
+using namespace dccl_amd;
+
+namespace {
+
+// Process-wide rendezvous: the group currently being formed.
+struct Registry {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::shared_ptr<Group> forming;
+};
+Registry& registry() {
+    static Registry r;
+    return r;
+}
+
+void validate_comm(const dcclComm* c, const char* fn) {
+    if (c == nullptr) throw std::runtime_error(std::string(fn) + ": invalid (null) DCCL communicator");
+}
+
+bool is_device_ptr(const void* p) {
+    if (p == nullptr) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+ncclResult_t check_op_dtype(int dtype, int op) {
+    return static_cast<ncclResult_t>(validate(dtype, op));
+}
+
+ncclResult_t copy_bytes(void* dst, const void* src, size_t bytes, bool device, hipStream_t st) {
+    if (dst == src || bytes == 0) return dccl::ncclSuccess;
+    if (device)
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st) == hipSuccess
+                   ? dccl::ncclSuccess
+                   : dccl::ncclUnhandledCudaError;
+    std::memmove(dst, src, bytes);
+    return dccl::ncclSuccess;
+}
+
+ncclResult_t placement(const void* send, const void* recv, bool* device) {
+    const bool sd = is_device_ptr(send), rd = is_device_ptr(recv);
+    if (send != nullptr && recv != nullptr && sd != rd) return dccl::ncclInvalidArgument;  // dccl.cpp:358-366
+    *device = rd || sd;
+    return dccl::ncclSuccess;
+}
+
+ncclResult_t join(dcclComm** out, uint32_t world, int64_t want_rank) {
+    if (world == 0) return dccl::ncclInvalidArgument;
+    if (want_rank >= int64_t(world)) return dccl::ncclInvalidArgument;
+    auto c = std::make_unique<dcclComm>();
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = -1;
+    }
+    c->device = dev;
+    std::shared_ptr<Group> g;
+    {
+        Registry& R = registry();
+        std::unique_lock<std::mutex> lk(R.mu);
+        if (!R.forming || R.forming->world() != world) R.forming = std::make_shared<Group>(world);
+        g = R.forming;
+        uint32_t rank;
+        if (want_rank >= 0) {
+            if (g->taken[want_rank]) return dccl::ncclInvalidUsage;
+            rank = static_cast<uint32_t>(want_rank);
+        } else {
+            rank = 0;
+            while (rank < world && g->taken[rank]) ++rank;
+        }
+        g->taken[rank] = true;
+        c->rank = rank;
+        if (++g->joined == world) R.forming.reset();  // group complete: the next init starts a new one
+    }
+    c->group = g;
+    c->world = world;
+    c->ready_events.assign(world, nullptr);
+    c->done_events.assign(world, nullptr);
+    if (dev >= 0) {
+        for (uint32_t p = 0; p < world; ++p) {
+            if (hipEventCreateWithFlags(&c->ready_events[p], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->done_events[p], hipEventDisableTiming) != hipSuccess)
+                return dccl::ncclUnhandledCudaError;
+        }
+    }
+    g->barrier();  // like Derecho's group formation: returns once every member joined
+    *out = c.release();
+    return dccl::ncclSuccess;
+}
+
+}  // namespace
+
+namespace dccl {
+
+ncclResult_t ncclCommInit(ncclComm_t* comm) {
+    if (comm == nullptr) return ncclInvalidArgument;
+    const char* ws = std::getenv("DCCL_WORLD_SIZE");
+    const long w = ws ? std::strtol(ws, nullptr, 10) : 1;
+    if (w <= 0) return ncclInvalidArgument;
+    return join(comm, static_cast<uint32_t>(w), -1);
+}
+
+ncclResult_t dcclCommInitRank(ncclComm_t* comm, uint32_t world_size, uint32_t rank) {
+    if (comm == nullptr) return ncclInvalidArgument;
+    return join(comm, world_size, rank);
+}
+
+ncclResult_t ncclCommFinalize(ncclComm_t comm) {
+    validate_comm(comm, __func__);
+    ncclResult_t rc = ncclSuccess;
+    if (comm->device >= 0 && hipDeviceSynchronize() != hipSuccess) rc = ncclUnhandledCudaError;
+    comm->group->barrier();  // no peer may still be reading our buffers
+    for (hipEvent_t e : comm->ready_events)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : comm->done_events)
+        if (e) (void)hipEventDestroy(e);
+    if (comm->dev_scratch) (void)hipFree(comm->dev_scratch);
+    if (comm->dev_work) (void)hipFree(comm->dev_work);
+    for (void* h : {comm->host_scratch, comm->host_work}) {
+        if (h) {
+            (void)hipHostUnregister(h);
+            std::free(h);
+        }
+    }
+    delete comm;
+    return rc;
+}
+
+uint32_t dcclGetWorldSize(ncclComm_t comm) {
+    validate_comm(comm, __func__);
+    return comm->world;
+}
+
+uint32_t dcclGetMyRank(ncclComm_t comm) {
+    validate_comm(comm, __func__);
+    return comm->rank;
+}
+
+ncclResult_t dcclRegisterCacheMemory(ncclComm_t comm, void* buffer, size_t size) {
+    validate_comm(comm, __func__);
+    if (buffer == nullptr || reinterpret_cast<uintptr_t>(buffer) % kCachelineSize || size % kCachelineSize)
+        return ncclInvalidArgument;  // dccl.cpp:506-514
+    if (is_device_ptr(buffer)) return ncclSuccess;
+    if (hipHostRegister(buffer, size, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();  // already registered / pinned: nothing to do
+    }
+    return ncclSuccess;
+}
+
+ncclResult_t dcclDeregisterCacheMemory(ncclComm_t comm, void* buffer, size_t) {
+    validate_comm(comm, __func__);
+    if (buffer == nullptr) return ncclInvalidArgument;
+    if (!is_device_ptr(buffer) && hipHostUnregister(buffer) != hipSuccess) (void)hipGetLastError();
+    return ncclSuccess;
+}
+
+ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                           ncclRedOp_t op, ncclComm_t comm, hipStream_t stream) {
+    validate_comm(comm, __func__);
+    ncclResult_t rc = check_op_dtype(datatype, op);
+    if (rc != ncclSuccess) return rc;
+    if (count == 0) return ncclSuccess;
+    if (sendbuff == nullptr || recvbuff == nullptr) return ncclInvalidArgument;
+    bool dev = false;
+    if ((rc = placement(sendbuff, recvbuff, &dev)) != ncclSuccess) return rc;
+    const size_t total = count * size_of_dtype(datatype);
+    const uint32_t W = comm->world;
+    if (W > 1 && (count < W || count % W)) return ncclInvalidArgument;
+    if ((rc = copy_bytes(recvbuff, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:393-408
+    if (W == 1) return ncclSuccess;
+    if ((rc = ensure_scratch(comm, total / W, dev)) != ncclSuccess) return rc;
+    void* scratch = dev ? comm->dev_scratch : comm->host_scratch;
+    return all_reduce_ring(comm, recvbuff, scratch, count, datatype, op, dev, stream);
+}
+
+ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recvcount, ncclDataType_t datatype,
+                               ncclRedOp_t op, ncclComm_t comm, hipStream_t stream) {
+    validate_comm(comm, __func__);
+    ncclResult_t rc = check_op_dtype(datatype, op);
+    if (rc != ncclSuccess) return rc;
+    if (recvcount == 0) return ncclSuccess;
+    if (sendbuff == nullptr || recvbuff == nullptr) return ncclInvalidArgument;
+    bool dev = false;
+    if ((rc = placement(sendbuff, recvbuff, &dev)) != ncclSuccess) return rc;
+    const uint32_t W = comm->world, r = comm->rank;
+    const size_t slot = recvcount * size_of_dtype(datatype), total = slot * W;
+    if ((rc = ensure_work(comm, total, dev)) != ncclSuccess) return rc;
+    void* work = dev ? comm->dev_work : comm->host_work;
+    if ((rc = copy_bytes(work, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:585-609
+    if (W > 1) {
+        if ((rc = ensure_scratch(comm, slot, dev)) != ncclSuccess) return rc;
+        void* scratch = dev ? comm->dev_scratch : comm->host_scratch;
+        rc = reduce_scatter_ring(comm, work, scratch, recvcount * W, datatype, op, dev, stream,
+                                 [W](uint32_t o) { return (o + W - 1) % W; },
+                                 [W](uint32_t n) { return (n + 1) % W; });
+        if (rc != ncclSuccess) return rc;
+    }
+    return copy_bytes(recvbuff, static_cast<unsigned char*>(work) + size_t(r) * slot, slot, dev, stream);
+}
+
+ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                        ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream) {
+    validate_comm(comm, __func__);
+    ncclResult_t rc = check_op_dtype(datatype, op);
+    if (rc != ncclSuccess) return rc;
+    const uint32_t W = comm->world, r = comm->rank;
+    if (root < 0 || uint32_t(root) >= W) return ncclInvalidArgument;
+    if (count == 0) return ncclSuccess;
+    if (count % W) return ncclInvalidArgument;  // dccl.cpp:762-767
+    const bool iamroot = r == uint32_t(root);
+    if (sendbuff == nullptr || (iamroot && recvbuff == nullptr)) return ncclInvalidArgument;
+    bool dev = false;
+    if ((rc = placement(sendbuff, iamroot ? recvbuff : sendbuff, &dev)) != ncclSuccess) return rc;
+    const size_t total = count * size_of_dtype(datatype), slot = total / W;
+    void* rbuf = recvbuff;
+    if (!iamroot) {
+        if ((rc = ensure_work(comm, total, dev)) != ncclSuccess) return rc;
+        rbuf = dev ? comm->dev_work : comm->host_work;
+    }
+    if ((rc = copy_bytes(rbuf, sendbuff, total, dev, stream)) != ncclSuccess) return rc;
+    if (W == 1) return ncclSuccess;
+    if ((rc = ensure_scratch(comm, slot, dev)) != ncclSuccess) return rc;
+    void* scratch = dev ? comm->dev_scratch : comm->host_scratch;
+    rc = reduce_scatter_ring(comm, rbuf, scratch, count, datatype, op, dev, stream,
+                             [W](uint32_t o) { return (o + W - 1) % W; }, [W](uint32_t n) { return (n + 1) % W; });
+    if (rc != ncclSuccess) return rc;
+    auto at = [&](uint32_t i) { return static_cast<unsigned char*>(rbuf) + size_t(i) * slot; };
+    if (iamroot) {
+        for (uint32_t p = 0; p < W; ++p)
+            if (p != r && (rc = xport_recv(comm, p, at(p), slot, dev, stream)) != ncclSuccess) return rc;
+        return ncclSuccess;
+    }
+    if ((rc = xport_send(comm, uint32_t(root), at(r), slot, dev, stream)) != ncclSuccess) return rc;
+    return xport_wait_send(comm, uint32_t(root), dev, stream);
+}
+
+ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcount, ncclDataType_t datatype,
+                           ncclComm_t comm, hipStream_t stream) {
+    validate_comm(comm, __func__);
+    const size_t esz = size_of_dtype(datatype);
+    if (esz == 0) return ncclInvalidArgument;
+    if (sendcount == 0) return ncclSuccess;
+    if (sendbuff == nullptr || recvbuff == nullptr) return ncclInvalidArgument;
+    bool dev = false;
+    ncclResult_t rc = placement(sendbuff, recvbuff, &dev);
+    if (rc != ncclSuccess) return rc;
+    void* slot = static_cast<unsigned char*>(recvbuff) + sendcount * comm->rank * esz;
+    if ((rc = copy_bytes(slot, sendbuff, sendcount * esz, dev, stream)) != ncclSuccess) return rc;
+    const RankMap id = [](uint32_t x) { return x; };
+    return all_gather_ring(comm, recvbuff, sendcount, datatype, dev, stream, id, id);
+}
+
+ncclResult_t ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype, int root,
+                           ncclComm_t comm, hipStream_t stream) {
+    validate_comm(comm, __func__);
+    const size_t esz = size_of_dtype(datatype);
+    const uint32_t W = comm->world, r = comm->rank;
+    if (esz == 0 || root < 0 || uint32_t(root) >= W) return ncclInvalidArgument;
+    if (count == 0) return ncclSuccess;
+    const size_t bytes = count * esz;
+    bool dev = false;
+    ncclResult_t rc = placement(r == uint32_t(root) ? sendbuff : recvbuff, recvbuff, &dev);
+    if (rc != ncclSuccess) return rc;
+    if (r == uint32_t(root)) {
+        for (uint32_t p = 0; p < W; ++p)
+            if (p != r && (rc = xport_send(comm, p, sendbuff, bytes, dev, stream)) != ncclSuccess) return rc;
+        if ((rc = copy_bytes(recvbuff, sendbuff, bytes, dev, stream)) != ncclSuccess) return rc;
+        for (uint32_t p = 0; p < W; ++p)
+            if (p != r && (rc = xport_wait_send(comm, p, dev, stream)) != ncclSuccess) return rc;
+        return ncclSuccess;
+    }
+    return xport_recv(comm, uint32_t(root), recvbuff, bytes, dev, stream);
+}
+
+ncclResult_t ncclBcast(void* buff, size_t count, ncclDataType_t datatype, int root, ncclComm_t comm,
+                       hipStream_t stream) {
+    return ncclBroadcast(buff, buff, count, datatype, root, comm, stream);
+}
+
+ncclResult_t ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatype, int peer, ncclComm_t comm,
+                      hipStream_t stream) {
+    validate_comm(comm, __func__);
+    const size_t esz = size_of_dtype(datatype);
+    if (esz == 0 || peer < 0 || uint32_t(peer) >= comm->world || uint32_t(peer) == comm->rank)
+        return ncclInvalidArgument;  // dccl.cpp:869-872
+    const bool dev = is_device_ptr(sendbuff);
+    ncclResult_t rc = xport_send(comm, uint32_t(peer), sendbuff, count * esz, dev, stream);
+    if (rc != ncclSuccess) return rc;
+    return xport_wait_send(comm, uint32_t(peer), dev, stream);
+}
+
+ncclResult_t ncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int peer, ncclComm_t comm,
+                      hipStream_t stream) {
+    validate_comm(comm, __func__);
+    const size_t esz = size_of_dtype(datatype);
+    if (esz == 0 || peer < 0 || uint32_t(peer) >= comm->world || uint32_t(peer) == comm->rank)
+        return ncclInvalidArgument;  // dccl.cpp:893-896
+    return xport_recv(comm, uint32_t(peer), recvbuff, count * esz, is_device_ptr(recvbuff), stream);
+}
+
+}  // namespace dccl

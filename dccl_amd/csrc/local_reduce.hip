@@ -60,47 +60,63 @@ __device__ __forceinline__ void st_elem(unsigned char* base, size_t i, T v) {
 // Vector kernel.  Operands are split as [head scalars | nvec 16-B vectors | tail
 // scalars]; head aligns recv (and, by construction, send) to 16 B.
 // ---------------------------------------------------------------------------------
-template <typename T, int OP, int UNROLL, int POLICY>
+// Kernel shape: BLOCK threads, UNROLL 16-B vectors per thread per operand, cache POLICY
+// bits, XCD: remap block ids so that each XCD's blocks walk one contiguous range.
+template <int BLOCK_, int UNROLL_, int POLICY_, bool XCD_>
+struct VecCfg {
+    static constexpr int BLOCK = BLOCK_, UNROLL = UNROLL_, POLICY = POLICY_;
+    static constexpr bool XCD = XCD_;
+    static constexpr size_t TILE = size_t(BLOCK_) * UNROLL_;
+};
+
+template <typename T, int OP, typename C>
 __device__ __forceinline__ void full_tile(const u32x4* __restrict__ vs, u32x4* __restrict__ vr, size_t base) {
-    u32x4 s[UNROLL], r[UNROLL];
+    u32x4 s[C::UNROLL], r[C::UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) s[u] = ld16<(POLICY & kNtSend) != 0>(vs + base + u * kBlock);
+    for (int u = 0; u < C::UNROLL; ++u) s[u] = ld16<(C::POLICY & kNtSend) != 0>(vs + base + u * C::BLOCK);
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) r[u] = ld16<(POLICY & kNtRecv) != 0>(vr + base + u * kBlock);
+    for (int u = 0; u < C::UNROLL; ++u) r[u] = ld16<(C::POLICY & kNtRecv) != 0>(vr + base + u * C::BLOCK);
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
+    for (int u = 0; u < C::UNROLL; ++u) {
         const u32x4 o = combine16<T, OP>(r[u], s[u]);
-        if constexpr ((POLICY & kNtStore) != 0) __builtin_nontemporal_store(o, vr + base + u * kBlock);
-        else vr[base + u * kBlock] = o;
+        if constexpr ((C::POLICY & kNtStore) != 0) __builtin_nontemporal_store(o, vr + base + u * C::BLOCK);
+        else vr[base + u * C::BLOCK] = o;
     }
 }
 
-template <typename T, int OP, int UNROLL, int POLICY>
+template <typename T, int OP, typename C>
 __device__ __noinline__ void partial_tile(const u32x4* __restrict__ vs, u32x4* __restrict__ vr, size_t base,
                                           size_t nvec) {
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-        const size_t i = base + u * kBlock;
+    for (int u = 0; u < C::UNROLL; ++u) {
+        const size_t i = base + u * C::BLOCK;
         if (i < nvec) vr[i] = combine16<T, OP>(vr[i], vs[i]);
     }
 }
 
-template <typename T, int OP, int UNROLL, int POLICY>
-__global__ __launch_bounds__(kBlock) void reduce_vec_kernel(const unsigned char* __restrict__ send,
-                                                            unsigned char* __restrict__ recv,
-                                                            size_t head, size_t nvec, size_t tail) {
-    constexpr size_t kTile = size_t(kBlock) * UNROLL;
+// Bijective XCD-aware remap (cdna_hip_programming.md, "XCD swizzle must be bijective"):
+// blocks b and b+8 share an XCD, so give each group {b : b % 8 == x} one contiguous range.
+__device__ __forceinline__ size_t xcd_remap(size_t b, size_t nb) {
+    const size_t q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+template <typename T, int OP, typename C>
+__global__ __launch_bounds__(C::BLOCK) void reduce_vec_kernel(const unsigned char* __restrict__ send,
+                                                              unsigned char* __restrict__ recv,
+                                                              size_t head, size_t nvec, size_t tail) {
     const u32x4* __restrict__ vs = reinterpret_cast<const u32x4*>(send + head * sizeof(T));
     u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
-    const size_t nfull = nvec / kTile;
+    const size_t nfull = nvec / C::TILE;
+    const size_t bid = C::XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
 
     // Full tiles: no bounds checks, all 2*UNROLL loads in flight before the first use.
-    for (size_t t = blockIdx.x; t < nfull; t += gridDim.x)
-        full_tile<T, OP, UNROLL, POLICY>(vs, vr, t * kTile + threadIdx.x);
+    for (size_t t = bid; t < nfull; t += gridDim.x)
+        full_tile<T, OP, C>(vs, vr, t * C::TILE + threadIdx.x);
 
     // The partial last tile goes to the block after the last full one (mod grid).
-    if (nfull * kTile < nvec && blockIdx.x == nfull % gridDim.x)
-        partial_tile<T, OP, UNROLL, POLICY>(vs, vr, nfull * kTile + threadIdx.x, nvec);
+    if (nfull * C::TILE < nvec && bid == nfull % gridDim.x)
+        partial_tile<T, OP, C>(vs, vr, nfull * C::TILE + threadIdx.x, nvec);
 
     // Scalar head [0, head) and tail [head + nvec*V, count): < 16 elements each.
     if (blockIdx.x == 0 && threadIdx.x < head + tail) {
@@ -200,14 +216,13 @@ __global__ __launch_bounds__(kBlock) void reduce_multi_scalar_kernel(SendList se
 namespace {
 
 // Default configuration of the shipped kernel (chosen by tools/tune on MI355X).
-constexpr int kDefaultUnroll = 4;
-constexpr int kDefaultPolicy = kNtSend;
+using DefaultCfg = VecCfg<256, 1, kNtSend | kNtRecv | kNtStore, false>;
 constexpr size_t kMaxGrid = size_t(1) << 22;  // grid-stride beyond this
 
-inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream) {
+inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream, int block = kBlock) {
     if (grid == 0) return DCCL_SUCCESS;
     if (grid > kMaxGrid) grid = kMaxGrid;
-    const hipError_t e = hipLaunchKernel(fn, dim3(static_cast<unsigned>(grid)), dim3(kBlock), args, 0, stream);
+    const hipError_t e = hipLaunchKernel(fn, dim3(static_cast<unsigned>(grid)), dim3(block), args, 0, stream);
     return e == hipSuccess ? DCCL_SUCCESS : DCCL_UNHANDLED_DEVICE_ERROR;
 }
 
@@ -227,13 +242,13 @@ inline Split split_for_vectors(uintptr_t recv, size_t count) {
     return Split{head, nvec, rest - nvec * V};
 }
 
-template <typename T, int OP, int UNROLL, int POLICY>
+template <typename T, int OP, typename C>
 int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t stream, size_t grid_cap) {
-    size_t grid = ceil_div(sp.nvec, size_t(kBlock) * UNROLL);
+    size_t grid = ceil_div(sp.nvec, C::TILE);
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     if (grid_cap && grid > grid_cap) grid = grid_cap;
     void* args[] = {&s, &r, &sp.head, &sp.nvec, &sp.tail};
-    return launch(reinterpret_cast<const void*>(&reduce_vec_kernel<T, OP, UNROLL, POLICY>), grid, args, stream);
+    return launch(reinterpret_cast<const void*>(&reduce_vec_kernel<T, OP, C>), grid, args, stream, C::BLOCK);
 }
 
 template <typename T, int OP>
@@ -252,7 +267,7 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
     const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
     if ((as | ar) % sizeof(T)) return launch_scalar<T, OP>(s, r, count, false, stream);
     if ((as ^ ar) & 15) return launch_scalar<T, OP>(s, r, count, true, stream);
-    return launch_vec<T, OP, kDefaultUnroll, kDefaultPolicy>(s, r, split_for_vectors<T>(ar, count), stream, 0);
+    return launch_vec<T, OP, DefaultCfg>(s, r, split_for_vectors<T>(ar, count), stream, 0);
 }
 
 template <typename T, int OP, int K>
@@ -339,33 +354,93 @@ extern "C" int dccl_local_reduce_multi(const void* const* sends, int nsend, void
 // Tuning entry: fp32 Sum with an explicit kernel variant (include/dccl/dccl_reduce_tuning.h).
 // ---------------------------------------------------------------------------------
 namespace {
-template <int UNROLL>
-int tune_policy(int policy, const unsigned char* s, unsigned char* r, Split sp, hipStream_t st, size_t cap) {
-    switch (policy) {
-    case 0: return launch_vec<float, kSum, UNROLL, 0>(s, r, sp, st, cap);
-    case 1: return launch_vec<float, kSum, UNROLL, 1>(s, r, sp, st, cap);
-    case 3: return launch_vec<float, kSum, UNROLL, 3>(s, r, sp, st, cap);
-    case 5: return launch_vec<float, kSum, UNROLL, 5>(s, r, sp, st, cap);
-    case 7: return launch_vec<float, kSum, UNROLL, 7>(s, r, sp, st, cap);
-    default: return DCCL_INVALID_ARGUMENT;
-    }
+using TuneFn = int (*)(const unsigned char*, unsigned char*, Split, hipStream_t, size_t);
+template <int B, int U, int P, bool X>
+int tune_one(const unsigned char* s, unsigned char* r, Split sp, hipStream_t st, size_t cap) {
+    return launch_vec<float, kSum, VecCfg<B, U, P, X>>(s, r, sp, st, cap);
 }
+struct TuneEntry { int block, unroll, policy, xcd; TuneFn fn; };
+#define DCCL_TV(B, U, P, X) TuneEntry{B, U, P, X, &tune_one<B, U, P, X>}
+const TuneEntry kTune[] = {
+    DCCL_TV(64, 1, 7, 0),  DCCL_TV(64, 1, 5, 0),  DCCL_TV(64, 1, 6, 0),  DCCL_TV(64, 1, 3, 0),
+    DCCL_TV(64, 1, 1, 0),  DCCL_TV(64, 1, 7, 1),  DCCL_TV(64, 2, 7, 0),  DCCL_TV(64, 4, 7, 0),
+    DCCL_TV(128, 1, 7, 0), DCCL_TV(128, 1, 5, 0), DCCL_TV(128, 1, 6, 0), DCCL_TV(128, 1, 7, 1),
+    DCCL_TV(256, 1, 7, 0), DCCL_TV(256, 1, 7, 1), DCCL_TV(256, 4, 7, 0), DCCL_TV(1024, 1, 7, 0),
+    DCCL_TV(256, 4, 1, 0),
+};
+#undef DCCL_TV
 }  // namespace
 
-extern "C" int dccl_tune_reduce_f32_sum(const void* send, void* recv, size_t count, int unroll, int policy,
+extern "C" int dccl_tune_num_variants(void) { return int(sizeof(kTune) / sizeof(kTune[0])); }
+
+extern "C" int dccl_tune_variant_info(int v, int* block, int* unroll, int* policy, int* xcd) {
+    if (v < 0 || v >= dccl_tune_num_variants()) return DCCL_INVALID_ARGUMENT;
+    *block = kTune[v].block; *unroll = kTune[v].unroll; *policy = kTune[v].policy; *xcd = kTune[v].xcd;
+    return DCCL_SUCCESS;
+}
+
+extern "C" int dccl_tune_reduce_f32_sum(const void* send, void* recv, size_t count, int variant,
                                         size_t grid_cap, void* stream) {
+    if (variant < 0 || variant >= dccl_tune_num_variants()) return DCCL_INVALID_ARGUMENT;
     if (count == 0) return DCCL_SUCCESS;
     const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
     if (((as | ar) & 3) || ((as ^ ar) & 15)) return DCCL_INVALID_ARGUMENT;
-    const auto s = static_cast<const unsigned char*>(send);
-    const auto r = static_cast<unsigned char*>(recv);
-    const Split sp = split_for_vectors<float>(ar, count);
-    const auto st = static_cast<hipStream_t>(stream);
-    switch (unroll) {
-    case 1: return tune_policy<1>(policy, s, r, sp, st, grid_cap);
-    case 2: return tune_policy<2>(policy, s, r, sp, st, grid_cap);
-    case 4: return tune_policy<4>(policy, s, r, sp, st, grid_cap);
-    case 8: return tune_policy<8>(policy, s, r, sp, st, grid_cap);
-    default: return DCCL_INVALID_ARGUMENT;
-    }
+    return kTune[variant].fn(static_cast<const unsigned char*>(send), static_cast<unsigned char*>(recv),
+                             split_for_vectors<float>(ar, count), static_cast<hipStream_t>(stream), grid_cap);
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning only: one-wave blocks, one 16-B vector per lane and operand, cache-policy bits
+// chosen in inline asm (the builtins only expose `nt`).  Requires count % 256 == 0 and
+// 16-B aligned operands; fp32 Sum.
+// ---------------------------------------------------------------------------------
+namespace {
+#define DCCL_ASM_LS(BITS_S, BITS_R)                                                              \
+    asm volatile("global_load_dwordx4 %0, %2, off " BITS_S "\n\t"                                \
+                 "global_load_dwordx4 %1, %3, off " BITS_R "\n\t"                                \
+                 "s_waitcnt vmcnt(0)"                                                            \
+                 : "=&v"(a), "=&v"(b)                                                            \
+                 : "v"(ps), "v"(pr)                                                              \
+                 : "memory")
+#define DCCL_ASM_ST(BITS) asm volatile("global_store_dwordx4 %0, %1, off " BITS :: "v"(pr), "v"(o) : "memory")
+
+template <int FLAVOR>
+__global__ __launch_bounds__(64) void tune_asm_kernel(const u32x4* __restrict__ s, u32x4* __restrict__ r,
+                                                      size_t nvec) {
+    const size_t i = size_t(blockIdx.x) * 64 + threadIdx.x;
+    if (i >= nvec) return;
+    const u32x4* ps = s + i;
+    u32x4* pr = r + i;
+    u32x4 a, b;
+    if constexpr (FLAVOR == 0) DCCL_ASM_LS("nt", "nt");
+    if constexpr (FLAVOR == 1) DCCL_ASM_LS("sc1 nt", "sc1 nt");
+    if constexpr (FLAVOR == 2) DCCL_ASM_LS("sc0 sc1 nt", "sc0 sc1 nt");
+    if constexpr (FLAVOR == 3) DCCL_ASM_LS("nt", "nt");
+    if constexpr (FLAVOR == 4) DCCL_ASM_LS("sc1", "sc1");
+    if constexpr (FLAVOR == 5) DCCL_ASM_LS("nt", "nt");
+    if constexpr (FLAVOR == 6) DCCL_ASM_LS("sc0 sc1", "nt");
+    const u32x4 o = combine16<float, kSum>(b, a);
+    if constexpr (FLAVOR == 0) DCCL_ASM_ST("nt");
+    if constexpr (FLAVOR == 1) DCCL_ASM_ST("sc1 nt");
+    if constexpr (FLAVOR == 2) DCCL_ASM_ST("sc0 sc1 nt");
+    if constexpr (FLAVOR == 3) DCCL_ASM_ST("sc0 sc1 nt");
+    if constexpr (FLAVOR == 4) DCCL_ASM_ST("nt");
+    if constexpr (FLAVOR == 5) DCCL_ASM_ST("sc1");
+    if constexpr (FLAVOR == 6) DCCL_ASM_ST("nt");
+}
+#undef DCCL_ASM_LS
+#undef DCCL_ASM_ST
+}  // namespace
+
+extern "C" int dccl_tune_asm_f32_sum(const void* send, void* recv, size_t count, int flavor, void* stream) {
+    if (count % 256 || ((reinterpret_cast<uintptr_t>(send) | reinterpret_cast<uintptr_t>(recv)) & 15))
+        return DCCL_INVALID_ARGUMENT;
+    const size_t nvec = count / 4;
+    const void* fns[] = {reinterpret_cast<const void*>(&tune_asm_kernel<0>), reinterpret_cast<const void*>(&tune_asm_kernel<1>),
+                         reinterpret_cast<const void*>(&tune_asm_kernel<2>), reinterpret_cast<const void*>(&tune_asm_kernel<3>),
+                         reinterpret_cast<const void*>(&tune_asm_kernel<4>), reinterpret_cast<const void*>(&tune_asm_kernel<5>),
+                         reinterpret_cast<const void*>(&tune_asm_kernel<6>)};
+    if (flavor < 0 || flavor >= int(sizeof(fns) / sizeof(fns[0]))) return DCCL_INVALID_ARGUMENT;
+    void* args[] = {&send, &recv, const_cast<size_t*>(&nvec)};
+    return launch(fns[flavor], nvec / 64, args, static_cast<hipStream_t>(stream), 64);
 }

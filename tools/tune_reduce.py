@@ -1,11 +1,15 @@
 #!/usr/bin/env python3
 """A/B the fp32-Sum combine kernel variants in ONE process, interleaved rounds (MI355X).
 
-Variants: UNROLL (16-B vectors per thread per operand in flight) x cache policy
-(nt send / nt recv / nt store) x grid shape (one block per tile vs persistent grid).
+Variants (include/dccl/dccl_reduce_tuning.h):
+  * template variants: block threads x UNROLL x cache policy (nt send / nt recv / nt store)
+    x XCD-contiguous remap, one block per tile or a persistent grid;
+  * asm flavours: one-wave blocks with explicit sc0/sc1/nt bits on loads and stores;
+  * placement: the best template variant with `send` placed at several byte offsets from
+    `recv` inside one allocation (HBM channel/bank sensitivity to the operands' distance).
 Prints a JSON table of median / min kernel times and achieved HBM GB/s (3N bytes).
 
-    python tools/tune_reduce.py [--mib 1024] [--rounds 7] [--iters 10]
+    python tools/tune_reduce.py [--mib 1024] [--rounds 7] [--iters 10] [--out file]
 """
 import argparse
 import json
@@ -31,38 +35,57 @@ def main():
     r = torch.rand(n, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    variants = []
-    for unroll in (1, 2, 4, 8):
-        for policy in (0, 1, 3, 5, 7):
-            variants.append((unroll, policy, 0))
-    for unroll in (2, 4, 8):
-        for k in (2, 4, 8, 16):
-            variants.append((unroll, 1, cus * k))
-    times = {v: [] for v in variants}
-    for v in variants:  # warm
-        assert dccl_amd.lib.dccl_tune_reduce_f32_sum(s.data_ptr(), r.data_ptr(), n, v[0], v[1], v[2], st) == 0
+    info = dccl_amd.tune_variants()
+    lib = dccl_amd.lib
+
+    # placement experiment: one allocation, send at recv + n*4 + delta
+    big = torch.empty(2 * n + (8 << 20) // 4, device="cuda")
+    deltas = [0, 4096, 65536, (1 << 20) + 4096, 3 << 20]
+
+    cases = {}
+    for v, inf in enumerate(info):
+        cases[("tpl", v, 0)] = (lambda v=v: lib.dccl_tune_reduce_f32_sum(s.data_ptr(), r.data_ptr(), n, v, 0, st),
+                                {**inf, "kind": "template", "grid_cap": 0})
+        if inf["block"] == 256 and inf["unroll"] == 4 and inf["policy"] == 7:
+            for k in (4, 16):
+                cap = cus * k
+                cases[("tpl", v, cap)] = (
+                    lambda v=v, cap=cap: lib.dccl_tune_reduce_f32_sum(s.data_ptr(), r.data_ptr(), n, v, cap, st),
+                    {**inf, "kind": "template", "grid_cap": cap})
+    for fl in range(7):
+        cases[("asm", fl)] = (lambda fl=fl: lib.dccl_tune_asm_f32_sum(s.data_ptr(), r.data_ptr(), n, fl, st),
+                              {"kind": "asm", "flavor": fl})
+    for d in deltas:
+        rp = big.data_ptr()
+        sp = rp + n * 4 + d
+        cases[("place", d)] = (lambda sp=sp, rp=rp: lib.dccl_tune_reduce_f32_sum(sp, rp, n, 0, 0, st),
+                               {"kind": "placement", "variant": info[0], "send_minus_recv_end": d})
+    for k, (fn, _) in cases.items():
+        assert fn() == 0, k
     torch.cuda.synchronize()
+    times = {k: [] for k in cases}
     for _ in range(a.rounds):
-        for v in variants:
+        for k, (fn, _) in cases.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.iters):
-                dccl_amd.lib.dccl_tune_reduce_f32_sum(s.data_ptr(), r.data_ptr(), n, v[0], v[1], v[2], st)
+                fn()
             e1.record()
             e1.synchronize()
-            times[v].append(e0.elapsed_time(e1) / a.iters)
+            times[k].append(e0.elapsed_time(e1) / a.iters)
     rows = []
-    for v, ts in times.items():
+    for k, ts in times.items():
         med = statistics.median(ts)
-        rows.append({"unroll": v[0], "policy": v[1], "grid_cap": v[2], "ms_median": round(med, 4),
-                     "ms_min": round(min(ts), 4), "gb_s": round(3 * n * 4 / (med * 1e-3) / 1e9, 1)})
+        rows.append({**cases[k][1], "ms_median": round(med, 4), "ms_min": round(min(ts), 4),
+                     "gb_s": round(3 * n * 4 / (med * 1e-3) / 1e9, 1)})
     rows.sort(key=lambda x: x["ms_median"])
     out = {"mib": a.mib, "cus": cus, "rows": rows}
     txt = json.dumps(out, indent=1)
-    print(txt)
     if a.out:
         with open(a.out, "w") as f:
             f.write(txt)
+    for row in rows:
+        print(json.dumps(row))
 
 
 if __name__ == "__main__":
