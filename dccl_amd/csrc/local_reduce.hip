@@ -156,35 +156,34 @@ __global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(const unsigned ch
 // ---------------------------------------------------------------------------------
 struct SendList { const unsigned char* p[8]; };
 
-template <typename T, int OP, int K>
-__global__ __launch_bounds__(kBlock) void reduce_multi_vec_kernel(SendList sends, unsigned char* __restrict__ recv,
-                                                                  size_t head, size_t nvec, size_t tail) {
-    constexpr int UNROLL = 2;
-    constexpr size_t kTile = size_t(kBlock) * UNROLL;
+template <typename T, int OP, int K, typename C>
+__global__ __launch_bounds__(C::BLOCK) void reduce_multi_vec_kernel(SendList sends, unsigned char* __restrict__ recv,
+                                                                    size_t head, size_t nvec, size_t tail) {
     u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
-    const size_t ntiles = (nvec + kTile - 1) / kTile;
+    const size_t ntiles = (nvec + C::TILE - 1) / C::TILE;
     for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const size_t base = t * kTile + threadIdx.x;
-        u32x4 r[UNROLL], s[K][UNROLL];
+        const size_t base = t * C::TILE + threadIdx.x;
+        u32x4 r[C::UNROLL], s[K][C::UNROLL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const size_t i = base + u * kBlock;
+        for (int u = 0; u < C::UNROLL; ++u) {
+            const size_t i = base + u * C::BLOCK;
             if (i < nvec) {
-                r[u] = vr[i];
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    s[k][u] = __builtin_nontemporal_load(
+                    s[k][u] = ld16<(C::POLICY & kNtSend) != 0>(
                         reinterpret_cast<const u32x4*>(sends.p[k] + head * sizeof(T)) + i);
+                r[u] = ld16<(C::POLICY & kNtRecv) != 0>(vr + i);
             }
         }
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const size_t i = base + u * kBlock;
+        for (int u = 0; u < C::UNROLL; ++u) {
+            const size_t i = base + u * C::BLOCK;
             if (i < nvec) {
                 u32x4 acc = r[u];
 #pragma unroll
                 for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, s[k][u]);
-                vr[i] = acc;
+                if constexpr ((C::POLICY & kNtStore) != 0) __builtin_nontemporal_store(acc, vr + i);
+                else vr[i] = acc;
             }
         }
     }
@@ -216,8 +215,10 @@ __global__ __launch_bounds__(kBlock) void reduce_multi_scalar_kernel(SendList se
 namespace {
 
 // Default configuration of the shipped kernel (chosen by tools/tune on MI355X).
-using DefaultCfg = VecCfg<256, 1, kNtSend | kNtRecv | kNtStore, false>;
-constexpr size_t kMaxGrid = size_t(1) << 22;  // grid-stride beyond this
+// One-wave blocks, one 16-B vector per lane and operand, every access non-temporal: the
+// fastest shape measured on MI355X at 1 GiB (tools/tune_reduce.py, profiles/r1_tune.json).
+using DefaultCfg = VecCfg<64, 1, kNtSend | kNtRecv | kNtStore, false>;
+constexpr size_t kMaxGrid = size_t(1) << 24;  // grid-stride beyond this (2^24 x 64 threads)
 
 inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream, int block = kBlock) {
     if (grid == 0) return DCCL_SUCCESS;
@@ -272,10 +273,11 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
 
 template <typename T, int OP, int K>
 int launch_multi_vec(SendList sl, unsigned char* r, Split sp, hipStream_t stream) {
-    size_t grid = ceil_div(sp.nvec, size_t(kBlock) * 2);
+    using C = DefaultCfg;
+    size_t grid = ceil_div(sp.nvec, C::TILE);
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
-    return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K>), grid, args, stream);
+    return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, C>), grid, args, stream, C::BLOCK);
 }
 
 template <typename T, int OP>

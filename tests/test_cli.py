@@ -52,12 +52,18 @@ def inputs(W, n, dtype, device):
     return sends, recvs
 
 
-def expected(api, W, n, dtype, op, device, repeat=1):
+def expected(api, W, n, dtype, op, device, repeat=1, faithful=False):
+    """What the API must leave in each rank's buffer.
+
+    faithful=False combines with the intended semantics (oracle.expected_reduce): the build's
+    contract.  faithful=True uses the reference's own loop split, which mis-combines chunks whose
+    recv is not 64-B aligned — used only to demonstrate that divergence."""
     dt = DT[dtype]
     sends, recvs = inputs(W, n, dtype, device)
+    fn = oracle.host_reduce if faithful else oracle.expected_reduce
 
     def combine(s, r):
-        assert oracle.host_reduce(np.ascontiguousarray(s), r, dt, op) == 0
+        assert fn(np.ascontiguousarray(s), r, dt, op) == 0
 
     def copy(d, s):
         d[:] = s
@@ -100,6 +106,19 @@ def check_api(api, W, n, dtype, op, gpu_flag, device):
 
 
 # ------------------------------------------------------------------------------- CPU
+def test_reference_ring_misalignment_divergence():
+    """SURVEY.md A.4 at ring level: uint64, W=5, count 385 -> 616-B slots, some chunks start
+    off a 64-B line and the reference loop combines their tails twice.  The build is correct;
+    the faithful simulation shows the reference's result differs (documented divergence).
+    Buffers are padded: the faithful loop also writes past the chunk (into the next one)."""
+    right = expected("all_reduce", 5, 385, "uint64", 0, False)
+    wrong = expected("all_reduce", 5, 385, "uint64", 0, False, faithful=True)
+    assert all(np.all(b == 0x0A0A0A0A0A0A0A0A) for b in right)
+    assert any(not np.array_equal(a, b) for a, b in zip(right, wrong))
+    aligned_ok = expected("all_reduce", 4, 1024, "uint32", 0, False, faithful=True)
+    assert all(np.all(b == 0x06060606) for b in aligned_ok)  # aligned slots: identical
+
+
 def test_cli_all_gather_host_cpu():
     check_api("all_gather", 4, 1024, "uint32", 0, -1, False)
     check_api("all_gather", 3, 999, "float64", 0, -1, False)

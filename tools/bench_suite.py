@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Secondary measurements of the combine on one MI355X (BASELINE.json configs C2-C4 and §8(f)).
+
+  c3     every op x {fp16, bf16, fp32, int32, int64} (+ the other dtypes) at 1 GiB per operand
+  c4     size sweep 4 KiB - 4 GiB, fp32 Sum, GiB/s vs the HBM roofline; points whose working set
+         (send + recv) fits the 256 MiB Infinity Cache are labelled "mall"
+  c2     256 MiB fp32 Sum
+  kway   dccl_local_reduce_multi, k = 1..8 sends at 256 MiB per operand: (k+2)N bytes
+  host   host-resident operands (pinned and pageable): H2D + combine + D2H rate
+
+All device timings are HIP events on the launch stream around back-to-back launches
+(median of rounds); operands rotate over enough buffer sets that each launch reads cold data
+when the working set is below 512 MiB.  Writes one JSON document (--out) and prints a summary.
+
+    python tools/bench_suite.py [--parts c3,c4,c2,kway,host] [--out file.json]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import dccl_amd  # noqa: E402
+
+PEAK = 8000.0  # GB/s
+MALL = 256 << 20
+NAMES = {0: "int8", 1: "uint8", 2: "int32", 3: "uint32", 4: "int64", 5: "uint64", 6: "float16",
+         7: "float32", 8: "float64", 9: "bfloat16"}
+OPS = {0: "sum", 1: "prod", 2: "max", 3: "min"}
+
+
+def fill(nbytes, dt, op, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    if dt in (6, 7, 8, 9):
+        f = {6: torch.float16, 7: torch.float32, 8: torch.float64, 9: torch.bfloat16}[dt]
+        x = torch.rand(nbytes // t.new_empty(0, dtype=f).element_size(), device="cuda", generator=g)
+        x = x.mul_(1.5).add_(0.5) if op == 1 else x.mul_(2).sub_(1)
+        t.view(f).copy_(x.to(f))
+    else:
+        t.view(torch.int32)[: nbytes // 4].random_(generator=g)
+    return t
+
+
+def time_launches(fns, rounds=7, min_ms=20.0):
+    """Median per-launch ms of cycling through fns back to back."""
+    st = torch.cuda.current_stream()
+    for f in fns:
+        f()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    fns[0]()
+    e1.record(st)
+    e1.synchronize()
+    one = max(e0.elapsed_time(e1), 1e-3)
+    reps = max(len(fns), int(min_ms / one) // len(fns) * len(fns))
+    res = []
+    for _ in range(rounds):
+        e0.record(st)
+        for i in range(reps):
+            fns[i % len(fns)]()
+        e1.record(st)
+        e1.synchronize()
+        res.append(e0.elapsed_time(e1) / reps)
+    return statistics.median(res), min(res)
+
+
+def c3(results, mib=1024):
+    st = torch.cuda.current_stream().cuda_stream
+    nbytes = mib << 20
+    rows = []
+    for dt in [7, 6, 9, 2, 4, 0, 1, 3, 5, 8]:
+        n = nbytes // dccl_amd.size_of_type(dt)
+        for op in range(4):
+            s, r = fill(nbytes, dt, op, 1), fill(nbytes, dt, op, 2)
+            fn = lambda: dccl_amd.check(dccl_amd.local_reduce(s.data_ptr(), r.data_ptr(), dt, n, op, st))
+            med, mn = time_launches([fn], rounds=5)
+            gbs = 3 * nbytes / (med * 1e-3) / 1e9
+            rows.append({"dtype": NAMES[dt], "op": OPS[op], "ms": round(med, 4), "gb_s": round(gbs, 1),
+                         "gib_s_traffic": round(3 * nbytes / (med * 1e-3) / 2**30, 1), "frac": round(gbs / PEAK, 4)})
+            del s, r
+        print("c3", NAMES[dt], [x["gb_s"] for x in rows[-4:]], flush=True)
+    results["c3"] = {"bytes_per_operand": nbytes, "rows": rows}
+
+
+def c4(results):
+    st = torch.cuda.current_stream().cuda_stream
+    rows = []
+    for lg in range(12, 33):
+        nbytes = 1 << lg
+        n = nbytes // 4
+        sets = max(1, min(64, (512 << 20) // (2 * nbytes)))  # rotate so launches read cold lines
+        if nbytes >= 1 << 32:
+            sets = 1
+        bufs = [(fill(nbytes, 7, 0, 2 * i), fill(nbytes, 7, 0, 2 * i + 1)) for i in range(sets)]
+        fns = [lambda s=s, r=r: dccl_amd.local_reduce(s.data_ptr(), r.data_ptr(), 7, n, 0, st) for s, r in bufs]
+        med, mn = time_launches(fns)
+        gbs = 3 * nbytes / (med * 1e-3) / 1e9
+        rows.append({"bytes_per_operand": nbytes, "ms": round(med, 5), "gb_s": round(gbs, 1),
+                     "gib_s_traffic": round(3 * nbytes / (med * 1e-3) / 2**30, 1), "frac": round(gbs / PEAK, 4),
+                     "buffer_sets": sets, "regime": "mall" if 2 * nbytes * sets <= MALL else "hbm"})
+        print("c4", nbytes, rows[-1]["gb_s"], rows[-1]["regime"], flush=True)
+        del bufs, fns
+        torch.cuda.empty_cache()
+    results["c4"] = rows
+
+
+def c2(results):
+    st = torch.cuda.current_stream().cuda_stream
+    nbytes = 256 << 20
+    n = nbytes // 4
+    s, r = fill(nbytes, 7, 0, 1), fill(nbytes, 7, 0, 2)
+    s2, r2 = fill(nbytes, 7, 0, 3), fill(nbytes, 7, 0, 4)
+    fns = [lambda: dccl_amd.local_reduce(s.data_ptr(), r.data_ptr(), 7, n, 0, st),
+           lambda: dccl_amd.local_reduce(s2.data_ptr(), r2.data_ptr(), 7, n, 0, st)]
+    med, mn = time_launches(fns)
+    gbs = 3 * nbytes / (med * 1e-3) / 1e9
+    results["c2"] = {"bytes_per_operand": nbytes, "ms": round(med, 4), "gb_s": round(gbs, 1),
+                     "frac": round(gbs / PEAK, 4), "note": "2 buffer sets rotated (1 GiB working set)"}
+    print("c2", results["c2"], flush=True)
+
+
+def kway(results, mib=256):
+    st = torch.cuda.current_stream().cuda_stream
+    nbytes = mib << 20
+    n = nbytes // 4
+    sends = [fill(nbytes, 7, 0, 10 + k) for k in range(8)]
+    r = fill(nbytes, 7, 0, 99)
+    rows = []
+    for k in range(1, 9):
+        ptrs = [x.data_ptr() for x in sends[:k]]
+        fn = lambda ptrs=ptrs: dccl_amd.local_reduce_multi(ptrs, r.data_ptr(), 7, n, 0, st)
+        med, _ = time_launches([fn])
+        seq = lambda ptrs=ptrs: [dccl_amd.local_reduce(p, r.data_ptr(), 7, n, 0, st) for p in ptrs]
+        med_seq, _ = time_launches([seq])
+        gbs = (k + 2) * nbytes / (med * 1e-3) / 1e9
+        rows.append({"k": k, "ms": round(med, 4), "gb_s": round(gbs, 1), "frac": round(gbs / PEAK, 4),
+                     "ms_k_single_launches": round(med_seq, 4), "speedup": round(med_seq / med, 2)})
+        print("kway", rows[-1], flush=True)
+    results["kway"] = {"bytes_per_operand": nbytes, "rows": rows}
+
+
+def host(results):
+    import numpy as np
+    rows = []
+    for mib in (1, 16, 256, 1024):
+        nbytes = mib << 20
+        n = nbytes // 4
+        for pinned in (True, False):
+            if pinned:
+                s = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+                r = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+                ps, pr = s.data_ptr(), r.data_ptr()
+            else:
+                s = np.ones(n, np.float32)
+                r = np.zeros(n, np.float32)
+                ps, pr = s.ctypes.data, r.ctypes.data
+            dccl_amd.check(dccl_amd.local_reduce_host(ps, pr, 7, n, 0))
+            reps, t0 = 0, time.perf_counter()
+            while reps < 3 or time.perf_counter() - t0 < 0.5:
+                dccl_amd.check(dccl_amd.local_reduce_host(ps, pr, 7, n, 0))
+                reps += 1
+            t = (time.perf_counter() - t0) / reps
+            rows.append({"bytes_per_operand": nbytes, "pinned": pinned, "ms": round(t * 1e3, 3),
+                         "payload_gib_s": round(nbytes / t / 2**30, 2)})
+            print("host", rows[-1], flush=True)
+    results["host_staged"] = rows
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--parts", default="c3,c4,c2,kway,host")
+    p.add_argument("--out", default="")
+    a = p.parse_args()
+    results = {"device": torch.cuda.get_device_name(0), "peak_gb_s": PEAK}
+    for part in a.parts.split(","):
+        {"c3": c3, "c4": c4, "c2": c2, "kway": kway, "host": host}[part](results)
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump(results, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
