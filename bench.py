@@ -25,8 +25,8 @@ import argparse
 import json
 import os
 import sys
-import threading
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -46,7 +46,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--mib", type=int, default=1024, help="MiB per operand per GPU")
+    p.add_argument("--mib", type=int, default=1024, help="MiB per operand per GPU (weak scaling)")
+    p.add_argument("--total-gib", type=float, default=0.0,
+                   help="BASELINE C5: one buffer of this many GiB per operand sharded over the GPUs (strong)")
     p.add_argument("--dtype", default="float32", choices=list(dccl_amd.DTYPE_NAMES))
     p.add_argument("--op", default="sum", choices=["sum", "prod", "max", "min"])
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
@@ -91,23 +93,23 @@ def cpu_baseline(budget_s: float) -> dict | None:
         fn(ps, pr, n)
         reps += 1
     t1 = (time.perf_counter() - t0) / reps
-    # all host threads: 64-B aligned contiguous slices, one thread each (ctypes drops the GIL)
-    nthr = len(os.sched_getaffinity(0))
+    # the box's CPU share (OMP_NUM_THREADS; 16 per GPU on the pool): 64-B aligned contiguous
+    # slices, one persistent thread each (ctypes drops the GIL during the call)
+    nthr = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
     per = (n // nthr) // 16 * 16
     bounds = [(i * per, n if i == nthr - 1 else (i + 1) * per) for i in range(nthr)]
 
-    def work(lo, hi):
-        fn(ps + 4 * lo, pr + 4 * lo, hi - lo)
+    def work(b):
+        fn(ps + 4 * b[0], pr + 4 * b[0], b[1] - b[0])
 
-    reps_mt, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s * 0.4 or reps_mt == 0:
-        ts = [threading.Thread(target=work, args=b) for b in bounds]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-        reps_mt += 1
-    tmt = (time.perf_counter() - t0) / reps_mt
+    reps_mt = 0
+    with ThreadPoolExecutor(max_workers=nthr) as pool:
+        list(pool.map(work, bounds))  # warm the threads
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget_s * 0.4 or reps_mt == 0:
+            list(pool.map(work, bounds))
+            reps_mt += 1
+        tmt = (time.perf_counter() - t0) / reps_mt
     nbytes = n * 4
     cpu_model = ""
     try:
@@ -159,8 +161,17 @@ def main():
     dt = dccl_amd.DTYPE_NAMES[a.dtype]
     op = dccl_amd.OP_NAMES[a.op]
     esz = dccl_amd.size_of_type(dt)
-    nbytes = a.mib << 20
-    n = nbytes // esz
+    strong = a.total_gib > 0
+    if strong:  # C5: contiguous 256-B aligned shards of one buffer (dccl_amd/shard.py)
+        from dccl_amd.shard import all_bounds
+        total_count = int(a.total_gib * GIB) // esz
+        bounds = all_bounds(total_count, esz, world)
+        n = bounds[rank][1] - bounds[rank][0]
+        total_bytes = total_count * esz
+    else:
+        n = (a.mib << 20) // esz
+        total_bytes = world * n * esz
+    nbytes = n * esz
 
     send = synth(n, dt, op, 0xDCC1 + 2 * rank, dev)
     recv = synth(n, dt, op, 0xDCC1 + 2 * rank + 1, dev)
@@ -201,26 +212,30 @@ def main():
 
     extra = {}
     if world > 1:  # the one exchange step of C5: RCCL all-gather of the reduced shards (separate)
-        gathered = torch.empty(world * n, dtype=recv.dtype, device=dev)
-        dist.all_gather_into_tensor(gathered, recv)
+        width = max(b - a_ for a_, b in bounds) if strong else n
+        src = recv if width == n else torch.cat([recv, recv.new_zeros(width - n)])
+        gathered = torch.empty(world * width, dtype=recv.dtype, device=dev)
+        dist.all_gather_into_tensor(gathered, src)
         torch.cuda.synchronize(dev)
         dist.barrier()
         t0 = time.perf_counter()
         iters = 3
         for _ in range(iters):
-            dist.all_gather_into_tensor(gathered, recv)
+            dist.all_gather_into_tensor(gathered, src)
         torch.cuda.synchronize(dev)
         dist.barrier()
         tag = (time.perf_counter() - t0) / iters
         extra["allgather"] = {"ms": round(tag * 1e3, 3),
-                              "busbw_gb_s": round((world - 1) * nbytes / tag / 1e9, 1),
-                              "note": "RCCL all_gather_into_tensor of the 1 GiB shards over xGMI; not in value"}
-        del gathered
+                              "busbw_gb_s": round((world - 1) * width * esz / tag / 1e9, 1),
+                              "combine_plus_allgather_ms": round(ms_per_step + tag * 1e3, 3),
+                              "note": "RCCL all_gather_into_tensor of the reduced shards over xGMI "
+                                      "(every GPU ends with the full result); not in value"}
+        del gathered, src
 
     if rank == 0:
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path) and dt == 7 and op == 0 and a.mib == 1024:
+        if os.path.exists(pmc_path) and dt == 7 and op == 0 and nbytes == 1 << 30:
             try:
                 traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
@@ -228,18 +243,21 @@ def main():
         achieved = 3 * nbytes / (kern_ms * 1e-3) / 1e9
         res = {
             "metric": "device-resident reduce GiB/s (ncclSum fp32, 1 GiB) at 1/2/4/8 GPU vs HBM peak",
-            "value": round(world * 3 * nbytes / (ms_per_step * 1e-3) / GIB, 2),
+            "value": round(3 * total_bytes / (ms_per_step * 1e-3) / GIB, 2),
             "unit": "GiB/s (HBM traffic 3*N*sizeof per combine, summed over GPUs)",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": {0: "i8", 1: "u8", 2: "i32", 3: "u32", 4: "i64", 5: "u64", 6: "f16", 7: "f32", 8: "f64",
                       9: "bf16"}[dt],
             "data": "synthetic (seeded uniform [-1,1) operands resident in HBM)",
-            "config": {"workload": f"in-place two-buffer combine recv=op(recv,send), {a.op}, "
-                                   f"{a.mib} MiB per operand per GPU (BASELINE configs C3/C5)",
-                       "bytes_per_operand_per_gpu": nbytes, "op": a.op, "parallelism": f"shard x{world}"},
-            "payload_gib_s": round(world * nbytes / (ms_per_step * 1e-3) / GIB, 2),
+            "config": {"workload": (f"C5: {a.total_gib:g} GiB per operand sharded over {world} GPU(s), "
+                                    f"in-place combine recv=op(recv,send), {a.op}") if strong else
+                                   (f"in-place two-buffer combine recv=op(recv,send), {a.op}, "
+                                    f"{a.mib} MiB per operand per GPU (BASELINE metric / config C3)"),
+                       "bytes_per_operand_per_gpu": nbytes, "bytes_per_operand_total": total_bytes,
+                       "op": a.op, "parallelism": f"shard x{world}"},
+            "payload_gib_s": round(total_bytes / (ms_per_step * 1e-3) / GIB, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "reduce_vec_kernel (dccl_local_reduce)",
