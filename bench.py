@@ -154,10 +154,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; DCCL_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (CPU collectives)
+    backend = os.environ.get("DCCL_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     dt = dccl_amd.DTYPE_NAMES[a.dtype]
     op = dccl_amd.OP_NAMES[a.op]
     esz = dccl_amd.size_of_type(dt)
@@ -203,7 +210,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
     else:
@@ -214,7 +221,8 @@ def main():
     if world > 1:  # the one exchange step of C5: RCCL all-gather of the reduced shards (separate)
         width = max(b - a_ for a_, b in bounds) if strong else n
         src = recv if width == n else torch.cat([recv, recv.new_zeros(width - n)])
-        gathered = torch.empty(world * width, dtype=recv.dtype, device=dev)
+        src = src.to(coll_dev)
+        gathered = torch.empty(world * width, dtype=recv.dtype, device=coll_dev)
         dist.all_gather_into_tensor(gathered, src)
         torch.cuda.synchronize(dev)
         dist.barrier()
@@ -228,6 +236,7 @@ def main():
         extra["allgather"] = {"ms": round(tag * 1e3, 3),
                               "busbw_gb_s": round((world - 1) * width * esz / tag / 1e9, 1),
                               "combine_plus_allgather_ms": round(ms_per_step + tag * 1e3, 3),
+                              "backend": backend,
                               "note": "RCCL all_gather_into_tensor of the reduced shards over xGMI "
                                       "(every GPU ends with the full result); not in value"}
         del gathered, src

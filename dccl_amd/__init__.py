@@ -90,6 +90,7 @@ def _load():
         "dccl_version": (c_int, []),
         "dccl_tune_reduce_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_size_t, c_void_p]),
         "dccl_tune_num_variants": (c_int, []),
+        "dccl_tune_reduce_f32_sum_lds": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_size_t, c_size_t, c_void_p]),
         "dccl_tune_asm_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
         "dccl_tune_variant_info": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     }
@@ -107,7 +108,7 @@ EXPORTED_SYMBOLS = [
     "dccl_local_reduce", "dccl_local_reduce_multi", "dccl_local_reduce_host",
     "dccl_register_host_memory", "dccl_deregister_host_memory", "dccl_size_of_type",
     "dccl_result_string", "dccl_version", "dccl_tune_reduce_f32_sum", "dccl_tune_num_variants",
-    "dccl_tune_variant_info", "dccl_tune_asm_f32_sum",
+    "dccl_tune_variant_info", "dccl_tune_asm_f32_sum", "dccl_tune_reduce_f32_sum_lds",
 ]
 
 

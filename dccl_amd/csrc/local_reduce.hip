@@ -220,10 +220,12 @@ namespace {
 using DefaultCfg = VecCfg<64, 1, kNtSend | kNtRecv | kNtStore, false>;
 constexpr size_t kMaxGrid = size_t(1) << 24;  // grid-stride beyond this (2^24 x 64 threads)
 
-inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream, int block = kBlock) {
+inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream, int block = kBlock,
+                  size_t lds_bytes = 0) {
     if (grid == 0) return DCCL_SUCCESS;
     if (grid > kMaxGrid) grid = kMaxGrid;
-    const hipError_t e = hipLaunchKernel(fn, dim3(static_cast<unsigned>(grid)), dim3(block), args, 0, stream);
+    const hipError_t e =
+        hipLaunchKernel(fn, dim3(static_cast<unsigned>(grid)), dim3(block), args, lds_bytes, stream);
     return e == hipSuccess ? DCCL_SUCCESS : DCCL_UNHANDLED_DEVICE_ERROR;
 }
 
@@ -244,12 +246,14 @@ inline Split split_for_vectors(uintptr_t recv, size_t count) {
 }
 
 template <typename T, int OP, typename C>
-int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t stream, size_t grid_cap) {
+int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t stream, size_t grid_cap,
+               size_t lds_bytes = 0) {
     size_t grid = ceil_div(sp.nvec, C::TILE);
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     if (grid_cap && grid > grid_cap) grid = grid_cap;
     void* args[] = {&s, &r, &sp.head, &sp.nvec, &sp.tail};
-    return launch(reinterpret_cast<const void*>(&reduce_vec_kernel<T, OP, C>), grid, args, stream, C::BLOCK);
+    return launch(reinterpret_cast<const void*>(&reduce_vec_kernel<T, OP, C>), grid, args, stream, C::BLOCK,
+                  lds_bytes);
 }
 
 template <typename T, int OP>
@@ -356,10 +360,10 @@ extern "C" int dccl_local_reduce_multi(const void* const* sends, int nsend, void
 // Tuning entry: fp32 Sum with an explicit kernel variant (include/dccl/dccl_reduce_tuning.h).
 // ---------------------------------------------------------------------------------
 namespace {
-using TuneFn = int (*)(const unsigned char*, unsigned char*, Split, hipStream_t, size_t);
+using TuneFn = int (*)(const unsigned char*, unsigned char*, Split, hipStream_t, size_t, size_t);
 template <int B, int U, int P, bool X>
-int tune_one(const unsigned char* s, unsigned char* r, Split sp, hipStream_t st, size_t cap) {
-    return launch_vec<float, kSum, VecCfg<B, U, P, X>>(s, r, sp, st, cap);
+int tune_one(const unsigned char* s, unsigned char* r, Split sp, hipStream_t st, size_t cap, size_t lds) {
+    return launch_vec<float, kSum, VecCfg<B, U, P, X>>(s, r, sp, st, cap, lds);
 }
 struct TuneEntry { int block, unroll, policy, xcd; TuneFn fn; };
 #define DCCL_TV(B, U, P, X) TuneEntry{B, U, P, X, &tune_one<B, U, P, X>}
@@ -381,14 +385,20 @@ extern "C" int dccl_tune_variant_info(int v, int* block, int* unroll, int* polic
     return DCCL_SUCCESS;
 }
 
-extern "C" int dccl_tune_reduce_f32_sum(const void* send, void* recv, size_t count, int variant,
-                                        size_t grid_cap, void* stream) {
+extern "C" int dccl_tune_reduce_f32_sum_lds(const void* send, void* recv, size_t count, int variant,
+                                            size_t grid_cap, size_t lds_bytes, void* stream) {
     if (variant < 0 || variant >= dccl_tune_num_variants()) return DCCL_INVALID_ARGUMENT;
     if (count == 0) return DCCL_SUCCESS;
     const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
     if (((as | ar) & 3) || ((as ^ ar) & 15)) return DCCL_INVALID_ARGUMENT;
     return kTune[variant].fn(static_cast<const unsigned char*>(send), static_cast<unsigned char*>(recv),
-                             split_for_vectors<float>(ar, count), static_cast<hipStream_t>(stream), grid_cap);
+                             split_for_vectors<float>(ar, count), static_cast<hipStream_t>(stream), grid_cap,
+                             lds_bytes);
+}
+
+extern "C" int dccl_tune_reduce_f32_sum(const void* send, void* recv, size_t count, int variant, size_t grid_cap,
+                                        void* stream) {
+    return dccl_tune_reduce_f32_sum_lds(send, recv, count, variant, grid_cap, 0, stream);
 }
 
 // ---------------------------------------------------------------------------------

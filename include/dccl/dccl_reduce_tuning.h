@@ -20,6 +20,9 @@ int dccl_tune_variant_info(int variant, int* block, int* unroll, int* policy, in
 int dccl_tune_asm_f32_sum(const void* send, void* recv, size_t count, int flavor, void* stream);
 int dccl_tune_reduce_f32_sum(const void* send, void* recv, size_t count, int variant, size_t grid_cap,
                              void* stream);
+/* Same, with `lds_bytes` of (unused) dynamic LDS per block to cap waves per CU. */
+int dccl_tune_reduce_f32_sum_lds(const void* send, void* recv, size_t count, int variant, size_t grid_cap,
+                                 size_t lds_bytes, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -172,14 +172,32 @@ def host(results):
     results["host_staged"] = rows
 
 
+def c1(results):
+    """BASELINE C1 through the C++ API: dccl_cli all_reduce fp32 count 1024, 4 ranks (threads),
+    1000 repeats, host buffers and device buffers; plus a 64 MiB all_reduce on device buffers."""
+    import subprocess
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dccl_amd", "bin", "dccl_cli")
+    rows = []
+    for args in (["-c", "1024", "-r", "1000", "-g", "-1"], ["-c", "1024", "-r", "1000", "-g", "0"],
+                 ["-c", str(16 << 20), "-r", "20", "-w", "2", "-g", "0"]):
+        p = subprocess.run([cli, "-a", "all_reduce", "-t", "float32", "-n", "4", *args], capture_output=True,
+                           text=True, timeout=600)
+        ranks = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+        rows.append({"args": " ".join(args), "rc": p.returncode,
+                     "us_per_call_max": max(r["us_per_call"] for r in ranks) if ranks else None,
+                     "first": ranks[0]["first"] if ranks else None})
+        print("c1", rows[-1], flush=True)
+    results["c1"] = rows
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--parts", default="c3,c4,c2,kway,host")
+    p.add_argument("--parts", default="c3,c4,c2,kway,host,c1")
     p.add_argument("--out", default="")
     a = p.parse_args()
     results = {"device": torch.cuda.get_device_name(0), "peak_gb_s": PEAK}
     for part in a.parts.split(","):
-        {"c3": c3, "c4": c4, "c2": c2, "kway": kway, "host": host}[part](results)
+        {"c3": c3, "c4": c4, "c2": c2, "kway": kway, "host": host, "c1": c1}[part](results)
         if a.out:
             with open(a.out, "w") as f:
                 json.dump(results, f, indent=1)

@@ -52,6 +52,10 @@ def main():
                 cases[("tpl", v, cap)] = (
                     lambda v=v, cap=cap: lib.dccl_tune_reduce_f32_sum(s.data_ptr(), r.data_ptr(), n, v, cap, st),
                     {**inf, "kind": "template", "grid_cap": cap})
+    for lds in (5 << 10, 7 << 10, 10 << 10, 20 << 10, 40 << 10):  # cap waves/CU: 160 KiB / lds blocks
+        cases[("lds", lds)] = (
+            lambda lds=lds: lib.dccl_tune_reduce_f32_sum_lds(s.data_ptr(), r.data_ptr(), n, 0, 0, lds, st),
+            {"kind": "occupancy", "variant": info[0], "lds_bytes": lds, "max_waves_per_cu": (160 << 10) // lds})
     for fl in range(7):
         cases[("asm", fl)] = (lambda fl=fl: lib.dccl_tune_asm_f32_sum(s.data_ptr(), r.data_ptr(), n, fl, st),
                               {"kind": "asm", "flavor": fl})
