@@ -10,6 +10,9 @@
 //   * device steps are stream-ordered end to end: no host stream synchronisation per step
 //     (the reference syncs after every device combine, reduce_scatter_ring.cpp:88, and that
 //     sync overwrites the combine's return code — SURVEY.md A.3 #5);
+//   * by default the receive of a reduce-scatter step is fused with the combine: the combine reads
+//     the peer's chunk in place (scratch == nullptr); DCCL_RS_SCRATCH=1 keeps the reference's
+//     land-in-scratchpad-then-combine shape (same results, one extra write + read of the chunk);
 //   * the send of a step is posted before its receive (the in-process transport's receive
 //     blocks until the matching post exists; the reference posts recv first in the all-gather,
 //     all_gather_ring.cpp:46-49, which is equivalent for a non-blocking RDMA post).
@@ -34,10 +37,17 @@ ncclResult_t reduce_scatter_ring(dccl::dcclComm* c, void* buffer, void* scratch,
     const uint32_t to = to_old(mod(int64_t(r) + 1, W)), from = to_old(mod(int64_t(r) - 1, W));
     for (uint32_t s = 0; s + 1 < W; ++s) {
         ncclResult_t rc = xport_send(c, to, data(int64_t(r) - s), slot_bytes, device, st);
-        if (rc == dccl::ncclSuccess) rc = xport_recv(c, from, scratch, slot_bytes, device, st);
+        if (rc == dccl::ncclSuccess) {
+            if (scratch != nullptr) {  // reference shape: land in the scratchpad, then combine
+                rc = xport_recv(c, from, scratch, slot_bytes, device, st);
+                if (rc == dccl::ncclSuccess)
+                    rc = combine(scratch, data(int64_t(r) - s - 1), dtype, slot_elems, op, device, st);
+            } else {  // fused: combine straight from the peer's chunk
+                rc = xport_recv_combine(c, from, data(int64_t(r) - s - 1), slot_elems, dtype, op, device, st);
+            }
+        }
         const ncclResult_t rw = xport_wait_send(c, to, device, st);
         if (rc == dccl::ncclSuccess) rc = rw;
-        if (rc == dccl::ncclSuccess) rc = combine(scratch, data(int64_t(r) - s - 1), dtype, slot_elems, op, device, st);
         if (rc != dccl::ncclSuccess) return rc;
     }
     return dccl::ncclSuccess;

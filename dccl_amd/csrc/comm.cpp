@@ -7,12 +7,14 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "dccl/dccl_reduce.h"
+#include "dispatch.hpp"
 
 namespace dccl_amd {
 
-Group::Group(uint32_t world) : taken(world, false), world_(world) {
+Group::Group(uint32_t world) : taken(world, false), devices(world, -1), world_(world) {
     chan_.reserve(size_t(world) * world);
     for (size_t i = 0; i < size_t(world) * world; ++i) chan_.push_back(std::make_unique<Channel>());
 }
@@ -32,6 +34,18 @@ void Group::barrier() {
 namespace {
 inline ncclResult_t hip_ok(hipError_t e) {
     return e == hipSuccess ? dccl::ncclSuccess : dccl::ncclUnhandledCudaError;
+}
+
+// Wait for `ready()` on channel `ch`: spin briefly (ring steps hand off every few microseconds;
+// a futex sleep/wake costs as much), then block on the condition variable.
+template <typename Pred>
+void channel_wait(Channel& ch, std::unique_lock<std::mutex>& lk, Pred ready) {
+    for (int i = 0; i < 2000 && !ready(); ++i) {
+        lk.unlock();
+        std::this_thread::yield();
+        lk.lock();
+    }
+    ch.cv.wait(lk, ready);
 }
 }  // namespace
 
@@ -57,7 +71,7 @@ ncclResult_t xport_recv(dccl::dcclComm* c, uint32_t peer, void* dst, size_t byte
     Message m;
     {
         std::unique_lock<std::mutex> lk(ch.mu);
-        ch.cv.wait(lk, [&] { return !ch.msgs.empty(); });
+        channel_wait(ch, lk, [&] { return !ch.msgs.empty(); });
         m = ch.msgs.front();
         ch.msgs.pop_front();
     }
@@ -81,12 +95,44 @@ ncclResult_t xport_recv(dccl::dcclComm* c, uint32_t peer, void* dst, size_t byte
     return rc;
 }
 
+ncclResult_t xport_recv_combine(dccl::dcclComm* c, uint32_t peer, void* dst, size_t count, int dtype, int op,
+                                bool device, hipStream_t stream) {
+    Channel& ch = c->group->channel(peer, c->rank);
+    Message m;
+    {
+        std::unique_lock<std::mutex> lk(ch.mu);
+        channel_wait(ch, lk, [&] { return !ch.msgs.empty(); });
+        m = ch.msgs.front();
+        ch.msgs.pop_front();
+    }
+    ncclResult_t rc = dccl::ncclSuccess;
+    Ack a;
+    if (m.bytes != count * size_of_dtype(dtype) || m.device != device) {
+        rc = dccl::ncclInvalidUsage;
+    } else if (device) {
+        a.done = c->done_events[peer];
+        rc = hip_ok(hipStreamWaitEvent(stream, m.ready, 0));
+        if (rc == dccl::ncclSuccess) rc = combine(m.ptr, dst, dtype, count, op, true, stream);
+        // the done event must exist in the stream even after a failed combine: the sender waits on it
+        const ncclResult_t re = hip_ok(hipEventRecord(a.done, stream));
+        if (rc == dccl::ncclSuccess) rc = re;
+    } else {
+        rc = combine(m.ptr, dst, dtype, count, op, false, stream);
+    }
+    {
+        std::lock_guard<std::mutex> lk(ch.mu);
+        ch.acks.push_back(a);
+    }
+    ch.cv.notify_all();
+    return rc;
+}
+
 ncclResult_t xport_wait_send(dccl::dcclComm* c, uint32_t peer, bool device, hipStream_t stream) {
     Channel& ch = c->group->channel(c->rank, peer);
     Ack a;
     {
         std::unique_lock<std::mutex> lk(ch.mu);
-        ch.cv.wait(lk, [&] { return !ch.acks.empty(); });
+        channel_wait(ch, lk, [&] { return !ch.acks.empty(); });
         a = ch.acks.front();
         ch.acks.pop_front();
     }

@@ -56,6 +56,8 @@ public:
     Channel& channel(uint32_t src, uint32_t dst) { return *chan_[src * world_ + dst]; }
     // Rendezvous: blocks until every rank arrived (used by init / finalize).
     void barrier();
+    // HIP device of each rank (-1: none), filled at join; used to enable peer access.
+    std::vector<int> devices;
 
     // join bookkeeping (guarded by the registry mutex)
     std::vector<bool> taken;
@@ -104,6 +106,13 @@ ncclResult_t xport_send(dccl::dcclComm* c, uint32_t peer, const void* buf, size_
 ncclResult_t xport_recv(dccl::dcclComm* c, uint32_t peer, void* dst, size_t bytes, bool device,
                         hipStream_t stream);
 ncclResult_t xport_wait_send(dccl::dcclComm* c, uint32_t peer, bool device, hipStream_t stream);
+// Fused receive + combine: instead of landing the peer's chunk in a scratchpad and combining
+// from there (reduce_scatter_ring.cpp:77-94), the combine reads the peer's buffer directly
+// (same process; an xGMI peer read when the peer is another GPU):
+//     dst[i] = op(dst[i], peer_chunk[i]),  i < count
+// One HBM/xGMI read of the peer chunk instead of read + write + read.
+ncclResult_t xport_recv_combine(dccl::dcclComm* c, uint32_t peer, void* dst, size_t count, int dtype, int op,
+                                bool device, hipStream_t stream);
 
 // Scratch management (grown on demand, page/line rounded; never shrinks until finalize).
 ncclResult_t ensure_scratch(dccl::dcclComm* c, size_t bytes, bool device);

@@ -81,6 +81,20 @@ ncclResult_t placement(const void* send, const void* recv, bool* device) {
     return dccl::ncclSuccess;
 }
 
+// nullptr selects the fused receive+combine ring step; DCCL_RS_SCRATCH=1 the reference's scratchpad
+bool use_scratch() {
+    const char* e = std::getenv("DCCL_RS_SCRATCH");
+    return e != nullptr && e[0] == '1';
+}
+
+ncclResult_t ring_scratch(dcclComm* c, size_t bytes, bool dev, void** out) {
+    *out = nullptr;
+    if (!use_scratch()) return dccl::ncclSuccess;
+    const ncclResult_t rc = ensure_scratch(c, bytes, dev);
+    if (rc == dccl::ncclSuccess) *out = dev ? c->dev_scratch : c->host_scratch;
+    return rc;
+}
+
 ncclResult_t join(dcclComm** out, uint32_t world, int64_t want_rank) {
     if (world == 0) return dccl::ncclInvalidArgument;
     if (want_rank >= int64_t(world)) return dccl::ncclInvalidArgument;
@@ -106,6 +120,7 @@ ncclResult_t join(dcclComm** out, uint32_t world, int64_t want_rank) {
             while (rank < world && g->taken[rank]) ++rank;
         }
         g->taken[rank] = true;
+        g->devices[rank] = dev;
         c->rank = rank;
         if (++g->joined == world) R.forming.reset();  // group complete: the next init starts a new one
     }
@@ -121,6 +136,19 @@ ncclResult_t join(dcclComm** out, uint32_t world, int64_t want_rank) {
         }
     }
     g->barrier();  // like Derecho's group formation: returns once every member joined
+    // Ranks on other GPUs: let this device's kernels and copies read their memory over xGMI.
+    if (dev >= 0) {
+        for (uint32_t p = 0; p < world; ++p) {
+            const int pd = g->devices[p];
+            if (pd < 0 || pd == dev) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, dev, pd) == hipSuccess && can) {
+                const hipError_t e = hipDeviceEnablePeerAccess(pd, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return dccl::ncclUnhandledCudaError;
+                (void)hipGetLastError();
+            }
+        }
+    }
     *out = c.release();
     return dccl::ncclSuccess;
 }
@@ -205,8 +233,8 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
     if (W > 1 && (count < W || count % W)) return ncclInvalidArgument;
     if ((rc = copy_bytes(recvbuff, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:393-408
     if (W == 1) return ncclSuccess;
-    if ((rc = ensure_scratch(comm, total / W, dev)) != ncclSuccess) return rc;
-    void* scratch = dev ? comm->dev_scratch : comm->host_scratch;
+    void* scratch = nullptr;
+    if ((rc = ring_scratch(comm, total / W, dev, &scratch)) != ncclSuccess) return rc;
     return all_reduce_ring(comm, recvbuff, scratch, count, datatype, op, dev, stream);
 }
 
@@ -225,8 +253,8 @@ ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recv
     void* work = dev ? comm->dev_work : comm->host_work;
     if ((rc = copy_bytes(work, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:585-609
     if (W > 1) {
-        if ((rc = ensure_scratch(comm, slot, dev)) != ncclSuccess) return rc;
-        void* scratch = dev ? comm->dev_scratch : comm->host_scratch;
+        void* scratch = nullptr;
+        if ((rc = ring_scratch(comm, slot, dev, &scratch)) != ncclSuccess) return rc;
         rc = reduce_scatter_ring(comm, work, scratch, recvcount * W, datatype, op, dev, stream,
                                  [W](uint32_t o) { return (o + W - 1) % W; },
                                  [W](uint32_t n) { return (n + 1) % W; });
@@ -256,8 +284,8 @@ ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, nccl
     }
     if ((rc = copy_bytes(rbuf, sendbuff, total, dev, stream)) != ncclSuccess) return rc;
     if (W == 1) return ncclSuccess;
-    if ((rc = ensure_scratch(comm, slot, dev)) != ncclSuccess) return rc;
-    void* scratch = dev ? comm->dev_scratch : comm->host_scratch;
+    void* scratch = nullptr;
+    if ((rc = ring_scratch(comm, slot, dev, &scratch)) != ncclSuccess) return rc;
     rc = reduce_scatter_ring(comm, rbuf, scratch, count, datatype, op, dev, stream,
                              [W](uint32_t o) { return (o + W - 1) % W; }, [W](uint32_t n) { return (n + 1) % W; });
     if (rc != ncclSuccess) return rc;

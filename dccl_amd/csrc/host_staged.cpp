@@ -13,11 +13,15 @@
 // analogue of dcclRegisterCacheMemory, dccl.cpp:503-549) are DMA'd directly; pageable ones
 // are bounced through per-thread pinned staging buffers by the calling thread.
 //
+// Small operands (<= DCCL_HOST_ZEROCOPY_MAX, default 256 KiB) skip the DMA pipeline: one kernel
+// loads and stores the page-locked host memory directly over PCIe (latency of one launch + sync).
+//
 // Per-thread state (like the reference's thread_local scratchpads, dccl.cpp:67-83): no
 // locks, no global mutable state; each thread owns its streams and slots per device.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -64,6 +68,8 @@ public:
     }
 
     int run(const unsigned char* send, unsigned char* recv, int dtype, size_t count, int op);
+    int run_zero_copy(const unsigned char* send, unsigned char* recv, void* dsend, void* drecv, int dtype,
+                      size_t count, int op);
 
 private:
     int fail() { release(); return DCCL_UNHANDLED_DEVICE_ERROR; }
@@ -97,19 +103,58 @@ private:
     Slot slots_[kSlots];
 };
 
-bool is_pinned(const void* p) {
+// Page-locked host memory: returns the device-side alias the GPU can load/store through
+// (nullptr for pageable memory).
+void* pinned_device_alias(const void* p) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
         (void)hipGetLastError();  // unregistered pageable memory reports an error: clear it
-        return false;
+        return nullptr;
     }
-    return attr.type == hipMemoryTypeHost;
+    if (attr.type != hipMemoryTypeHost) return nullptr;
+    // attributes describe the allocation: offset the alias to `p`
+    const auto host_base = static_cast<const unsigned char*>(attr.hostPointer);
+    auto dev_base = static_cast<unsigned char*>(attr.devicePointer);
+    if (host_base == nullptr || dev_base == nullptr) return nullptr;
+    return dev_base + (static_cast<const unsigned char*>(p) - host_base);
+}
+
+// Operands up to this many bytes take the zero-copy path (one kernel reading and writing host
+// memory over PCIe, no DMA staging); DCCL_HOST_ZEROCOPY_MAX overrides (0 disables).
+size_t zero_copy_max() {
+    static const size_t v = [] {
+        const char* e = std::getenv("DCCL_HOST_ZEROCOPY_MAX");
+        return e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : size_t(256) << 10;
+    }();
+    return v;
+}
+
+int Stager::run_zero_copy(const unsigned char* send, unsigned char* recv, void* dsend, void* drecv, int dtype,
+                          size_t count, int op) {
+    const size_t bytes = count * size_of_dtype(dtype);
+    Slot& sl = slots_[0];
+    if (dsend == nullptr) {  // pageable: bounce through the slot's pinned buffer
+        std::memcpy(sl.h_send, send, bytes);
+        if (hipHostGetDevicePointer(&dsend, sl.h_send, 0) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
+    }
+    const bool bounce_recv = drecv == nullptr;
+    if (bounce_recv) {
+        std::memcpy(sl.h_recv, recv, bytes);
+        if (hipHostGetDevicePointer(&drecv, sl.h_recv, 0) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
+    }
+    int rc = dccl_local_reduce(dsend, drecv, dtype, count, op, comp_);
+    if (hipStreamSynchronize(comp_) != hipSuccess && rc == DCCL_SUCCESS) rc = DCCL_UNHANDLED_DEVICE_ERROR;
+    if (rc == DCCL_SUCCESS && bounce_recv) std::memcpy(recv, sl.h_recv, bytes);
+    return rc;
 }
 
 int Stager::run(const unsigned char* send, unsigned char* recv, int dtype, size_t count, int op) {
     const size_t esz = size_of_dtype(dtype);
     const size_t per_chunk = kChunkBytes / esz;
-    const bool send_pinned = is_pinned(send), recv_pinned = is_pinned(recv);
+    void* const dsend = pinned_device_alias(send);
+    void* const drecv = pinned_device_alias(recv);
+    if (count * esz <= zero_copy_max()) return run_zero_copy(send, recv, dsend, drecv, dtype, count, op);
+    const bool send_pinned = dsend != nullptr, recv_pinned = drecv != nullptr;
     int rc = DCCL_SUCCESS;
     size_t k = 0;
     for (size_t off = 0; off < count && rc == DCCL_SUCCESS; off += per_chunk, ++k) {

@@ -29,10 +29,11 @@ def fnv1a(b: bytes) -> int:
     return h
 
 
-def run_cli(*args, timeout=300):
+def run_cli(*args, timeout=300, env=None):
     if not os.path.exists(CLI):
         pytest.skip("dccl_cli not built")
-    p = subprocess.run([CLI, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+    p = subprocess.run([CLI, *map(str, args)], capture_output=True, text=True, timeout=timeout,
+                       env={**os.environ, **(env or {})})
     rows = [json.loads(line) for line in p.stdout.splitlines() if line.startswith("{")]
     return p.returncode, rows, p.stderr
 
@@ -94,9 +95,10 @@ def expected(api, W, n, dtype, op, device, repeat=1, faithful=False):
     return recvs if api == "broadcast" else sends
 
 
-def check_api(api, W, n, dtype, op, gpu_flag, device):
+def check_api(api, W, n, dtype, op, gpu_flag, device, env=None):
     opname = ["sum", "prod", "max", "min"][op]
-    rc, rows, err = run_cli("-a", api, "-t", dtype, "-o", opname, "-c", n, "-n", W, "-r", 1, "-g", gpu_flag)
+    rc, rows, err = run_cli("-a", api, "-t", dtype, "-o", opname, "-c", n, "-n", W, "-r", 1, "-g", gpu_flag,
+                            env=env)
     assert rc == 0, err
     assert len(rows) == W
     want = expected(api, W, n, dtype, op, device)
@@ -166,9 +168,12 @@ def test_c1_known_answers(gpu_flag, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("scratch", ["0", "1"])  # fused recv+combine (default) / reference scratchpad shape
 @pytest.mark.parametrize("gpu_flag,device", [(-1, False), (0, True)])
 @pytest.mark.parametrize("api", ["all_reduce", "reduce_scatter", "reduce", "all_gather", "broadcast"])
-def test_cli_apis_against_oracle(api, gpu_flag, device):
+def test_cli_apis_against_oracle(api, gpu_flag, device, scratch):
+    if api in ("all_gather", "broadcast") and scratch == "1":
+        pytest.skip("no combine in this api")
     for W, n, dtype, op in [(4, 1024, "float32", 0), (3, 3 * 1001, "float64", 1), (2, 4096, "int8", 2),
-                            (8, 8 * 513, "bfloat16", 3), (5, 5 * 77, "uint64", 0)]:
-        check_api(api, W, n, dtype, op, gpu_flag, device)
+                            (8, 8 * 513, "bfloat16", 3), (5, 5 * 77, "uint64", 0), (4, 4 * (1 << 18), "float32", 0)]:
+        check_api(api, W, n, dtype, op, gpu_flag, device, env={"DCCL_RS_SCRATCH": scratch})

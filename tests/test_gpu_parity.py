@@ -205,7 +205,9 @@ def test_multi_matches_sequential(dccl, k):
 def test_host_staged(dccl, pinned):
     rng = np.random.default_rng(400)
     for dt in [0, 6, 7, 8, 9, 4]:
-        for n in [1, 1000, 3 * (16 << 20) // 4 + 12345]:  # > 3 staging slots for 4-B types
+        # 1 / 1000 / 256 KiB of fp32: zero-copy kernel on host memory; 65537: just above it;
+        # the last: > 3 DMA staging slots of 16 MiB for 4-B types
+        for n in [1, 1000, 65536, 65537, 3 * (16 << 20) // 4 + 12345]:
             s, r = rand_inputs(rng, dt, n)
             op = int(rng.integers(0, 4))
             want = expected(s, r, dt, op)

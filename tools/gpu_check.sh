@@ -16,15 +16,22 @@ cat "$out/smoke.log"
 echo "== bench"
 timeout -k 10 600 python bench.py > "$out/bench.json" 2> "$out/bench.err"
 cat "$out/bench.json"
-echo "== rocprof kernel trace"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench --output-format csv -- python3 bench.py --steps 20 --no-cpu --no-host-staged > "$out/prof.log" 2>&1
-echo "== pmc FETCH_SIZE"
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc_fetch" -o fetch -- python3 tools/pmc_probe.py > "$out/pmc_fetch.log" 2>&1
-echo "== pmc WRITE_SIZE"
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/pmc_write" -o write -- python3 tools/pmc_probe.py > "$out/pmc_write.log" 2>&1
-if [[ -n "${SUITE:-1}" && "${SUITE:-1}" != 0 ]]; then
-  echo "== suite"
-  timeout -k 10 900 python tools/bench_suite.py --out "$out/suite.json" > "$out/suite.log" 2>&1
-  tail -5 "$out/suite.log"
+if [[ "${PROF:-1}" != 0 ]]; then
+  echo "== rocprof kernel trace"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench --output-format csv -- python3 bench.py --steps 20 --no-cpu --no-host-staged > "$out/prof.log" 2>&1
+  echo "== pmc FETCH_SIZE"
+  timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc_fetch" -o fetch -- python3 tools/pmc_probe.py > "$out/pmc_fetch.log" 2>&1
+  echo "== pmc WRITE_SIZE"
+  timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/pmc_write" -o write -- python3 tools/pmc_probe.py > "$out/pmc_write.log" 2>&1
+fi
+if [[ -n "${SUITE:-}" ]]; then
+  echo "== suite ($SUITE)"
+  timeout -k 10 900 python tools/bench_suite.py --parts "$SUITE" --out "$out/suite.json" > "$out/suite.log" 2>&1
+  tail -30 "$out/suite.log"
+fi
+if [[ -n "${SUITE_STAGED:-}" ]]; then
+  echo "== host path with zero-copy disabled"
+  DCCL_HOST_ZEROCOPY_MAX=0 timeout -k 10 600 python tools/bench_suite.py --parts host,c1 --out "$out/suite_nozc.json" > "$out/suite_nozc.log" 2>&1
+  tail -20 "$out/suite_nozc.log"
 fi
 echo "== done"

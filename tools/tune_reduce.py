@@ -29,6 +29,8 @@ def main():
     p.add_argument("--rounds", type=int, default=7)
     p.add_argument("--iters", type=int, default=10)
     p.add_argument("--out", default="")
+    p.add_argument("--lds-kib", type=float, default=0.0)
+    p.add_argument("--only", default="", help="comma list of kinds to run: template,occupancy,asm,placement")
     a = p.parse_args()
     n = (a.mib << 20) // 4
     s = torch.rand(n, device="cuda")
@@ -52,7 +54,7 @@ def main():
                 cases[("tpl", v, cap)] = (
                     lambda v=v, cap=cap: lib.dccl_tune_reduce_f32_sum(s.data_ptr(), r.data_ptr(), n, v, cap, st),
                     {**inf, "kind": "template", "grid_cap": cap})
-    for lds in (5 << 10, 7 << 10, 10 << 10, 20 << 10, 40 << 10):  # cap waves/CU: 160 KiB / lds blocks
+    for lds in [int(a.lds_kib * 1024)] if a.lds_kib else (5 << 10, 6 << 10, 7 << 10, 8 << 10, 9 << 10, 10 << 10, 20 << 10):
         cases[("lds", lds)] = (
             lambda lds=lds: lib.dccl_tune_reduce_f32_sum_lds(s.data_ptr(), r.data_ptr(), n, 0, 0, lds, st),
             {"kind": "occupancy", "variant": info[0], "lds_bytes": lds, "max_waves_per_cu": (160 << 10) // lds})
@@ -64,6 +66,9 @@ def main():
         sp = rp + n * 4 + d
         cases[("place", d)] = (lambda sp=sp, rp=rp: lib.dccl_tune_reduce_f32_sum(sp, rp, n, 0, 0, st),
                                {"kind": "placement", "variant": info[0], "send_minus_recv_end": d})
+    if a.only:
+        keep = set(a.only.split(","))
+        cases = {k: v for k, v in cases.items() if v[1]["kind"] in keep or (k[0] == "tpl" and k[1] == 0)}
     for k, (fn, _) in cases.items():
         assert fn() == 0, k
     torch.cuda.synchronize()
