@@ -12,7 +12,8 @@ Rank 0 prints ONE JSON line:
   value            whole-job HBM traffic rate, GiB/s = N * 3 * bytes_per_operand / t_step
                    (3 = read send + read recv + write recv; BASELINE.md §2 roofline basis)
   roofline         dominant kernel (the combine): algorithmic bytes per launch / average
-                   launch duration from HIP events on the launch stream, vs 8.0 TB/s HBM peak;
+                   launch duration (HIP events around the timed region on the launch stream,
+                   divided by the steps), vs 8.0 TB/s HBM peak;
                    `traffic` = PMC HBM bytes per launch from profiles/pmc_traffic.json when present
   cpu_baseline     the reference's own CPU loop (oracle/_ref, Release flags) or the oracle
                    restatement, single thread, timed on this host on a bounded sample (rank 0, N=1)
@@ -44,7 +45,7 @@ GIB = float(1 << 30)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--mib", type=int, default=1024, help="MiB per operand per GPU (weak scaling)")
     p.add_argument("--total-gib", type=float, default=0.0,
@@ -193,22 +194,24 @@ def main():
 
     for _ in range(a.warmup):
         step()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    # HIP events over the timed region, on the stream the kernel is launched on: the average
+    # launch duration of the dominant kernel (back-to-back launches, as rocprofv3 sees them)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        ev[i][0].record(stream)
+    ev0.record(stream)
+    for _ in range(a.steps):
         step()
-        ev[i][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / a.steps
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
