@@ -13,8 +13,8 @@
 // analogue of dcclRegisterCacheMemory, dccl.cpp:503-549) are DMA'd directly; pageable ones
 // are bounced through per-thread pinned staging buffers by the calling thread.
 //
-// Small operands (<= DCCL_HOST_ZEROCOPY_MAX, default 256 KiB) skip the DMA pipeline: one kernel
-// loads and stores the page-locked host memory directly over PCIe (latency of one launch + sync).
+// Page-locked operands (and pageable ones up to 16 MiB, bounced) skip the DMA pipeline: one kernel
+// loads and stores the host memory directly over PCIe; the pipeline serves large pageable operands.
 //
 // Per-thread state (like the reference's thread_local scratchpads, dccl.cpp:67-83): no
 // locks, no global mutable state; each thread owns its streams and slots per device.
@@ -119,20 +119,21 @@ void* pinned_device_alias(const void* p) {
     return dev_base + (static_cast<const unsigned char*>(p) - host_base);
 }
 
-// Operands up to this many bytes take the zero-copy path (one kernel reading and writing host
-// memory over PCIe, no DMA staging); DCCL_HOST_ZEROCOPY_MAX overrides (0 disables).
+// Operands up to this many bytes take the zero-copy path (one kernel loading and storing the
+// page-locked host memory over PCIe, no DMA staging).  Measured on MI355X it beats the 3-stream
+// DMA pipeline at every size for page-locked operands (1 MiB: 13.4 vs 7.9 GiB/s; 256 MiB: 24.8
+// vs 24.0 GiB/s), so the default is unlimited; DCCL_HOST_ZEROCOPY_MAX overrides (0 disables).
+// Pageable operands are bounced through a 16 MiB pinned slot, so they qualify only up to that.
 size_t zero_copy_max() {
-    static const size_t v = [] {
-        const char* e = std::getenv("DCCL_HOST_ZEROCOPY_MAX");
-        return e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : size_t(256) << 10;
-    }();
-    return v;
+    const char* e = std::getenv("DCCL_HOST_ZEROCOPY_MAX");
+    return e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : ~size_t(0);
 }
 
 int Stager::run_zero_copy(const unsigned char* send, unsigned char* recv, void* dsend, void* drecv, int dtype,
                           size_t count, int op) {
     const size_t bytes = count * size_of_dtype(dtype);
     Slot& sl = slots_[0];
+    if ((dsend == nullptr || drecv == nullptr) && bytes > kChunkBytes) return DCCL_INTERNAL_ERROR;  // bounce size
     if (dsend == nullptr) {  // pageable: bounce through the slot's pinned buffer
         std::memcpy(sl.h_send, send, bytes);
         if (hipHostGetDevicePointer(&dsend, sl.h_send, 0) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
@@ -153,7 +154,9 @@ int Stager::run(const unsigned char* send, unsigned char* recv, int dtype, size_
     const size_t per_chunk = kChunkBytes / esz;
     void* const dsend = pinned_device_alias(send);
     void* const drecv = pinned_device_alias(recv);
-    if (count * esz <= zero_copy_max()) return run_zero_copy(send, recv, dsend, drecv, dtype, count, op);
+    const size_t bytes = count * esz;
+    if (bytes <= zero_copy_max() && ((dsend != nullptr && drecv != nullptr) || bytes <= kChunkBytes))
+        return run_zero_copy(send, recv, dsend, drecv, dtype, count, op);
     const bool send_pinned = dsend != nullptr, recv_pinned = drecv != nullptr;
     int rc = DCCL_SUCCESS;
     size_t k = 0;

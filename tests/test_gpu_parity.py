@@ -201,13 +201,17 @@ def test_multi_matches_sequential(dccl, k):
 
 
 # ----------------------------------------------------------------------------- host path
+@pytest.mark.parametrize("zero_copy", ["default", "0"])
 @pytest.mark.parametrize("pinned", [False, True])
-def test_host_staged(dccl, pinned):
+def test_host_staged(dccl, pinned, zero_copy, monkeypatch):
+    """Host operands: zero-copy kernel (page-locked, or pageable <= 16 MiB bounced) and the
+    3-stream DMA pipeline (large pageable, or DCCL_HOST_ZEROCOPY_MAX=0)."""
+    if zero_copy == "0":
+        monkeypatch.setenv("DCCL_HOST_ZEROCOPY_MAX", "0")
     rng = np.random.default_rng(400)
     for dt in [0, 6, 7, 8, 9, 4]:
-        # 1 / 1000 / 256 KiB of fp32: zero-copy kernel on host memory; 65537: just above it;
-        # the last: > 3 DMA staging slots of 16 MiB for 4-B types
-        for n in [1, 1000, 65536, 65537, 3 * (16 << 20) // 4 + 12345]:
+        # the last size spans > 3 DMA staging slots of 16 MiB for 4-B types
+        for n in [1, 1000, 65537, (16 << 20) // 4 + 1, 3 * (16 << 20) // 4 + 12345]:
             s, r = rand_inputs(rng, dt, n)
             op = int(rng.integers(0, 4))
             want = expected(s, r, dt, op)
