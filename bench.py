@@ -18,7 +18,9 @@ Rank 0 prints ONE JSON line:
   cpu_baseline     the reference's own CPU loop (oracle/_ref, Release flags) or the oracle
                    restatement, single thread, timed on this host on a bounded sample (rank 0, N=1)
 Extra keys: payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
-rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately).
+rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately),
+dccl_allreduce_rccl (N>1: the namespace-dccl ncclAllReduce — ring with the gfx950 combine — over
+the RCCL p2p transport, checked against and timed beside RCCL's own all_reduce; under a watchdog).
 """
 from __future__ import annotations
 
@@ -26,6 +28,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 
@@ -150,6 +153,75 @@ def host_staged_rate(nbytes: int, dt: int, op: int) -> dict:
             "bytes_per_operand": nbytes, "note": "pinned host operands; PCIe H2D 2N + D2H N bytes"}
 
 
+def run_with_watchdog(fn, seconds: float):
+    """Run fn() in a daemon thread; (result, finished).  A collective that hangs must not take the
+    bench line with it: the caller reports the timeout and exits without joining the thread."""
+    box = {}
+    done = threading.Event()
+
+    def target():
+        try:
+            box["value"] = fn()
+        except Exception as e:  # reported in the JSON line
+            box["value"] = {"error": repr(e)}
+        finally:
+            done.set()
+
+    threading.Thread(target=target, daemon=True).start()
+    if not done.wait(seconds):
+        return {"error": f"timed out after {seconds:.0f}s"}, False
+    return box["value"], True
+
+
+def dccl_allreduce_rccl(world: int, rank: int, dev, count: int, iters: int = 5) -> dict:
+    """the namespace-dccl ncclAllReduce (ring RS with the gfx950 combine + ring AG)
+    over the RCCL p2p transport, one process per GPU; checked against RCCL's own all_reduce
+    (int32: bit-exact; fp32: |d| <= (W-1) eps sum|x|, a different association order) and timed."""
+    obj = [dccl_amd.Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    comm = dccl_amd.Comm.rccl(world, rank, obj[0])
+    out = {"count": count, "world": world}
+    try:
+        st = torch.cuda.current_stream(dev)
+        g = torch.Generator(device=dev).manual_seed(1234 + rank)
+        xi = torch.randint(-2**20, 2**20, (count,), device=dev, generator=g, dtype=torch.int32)
+        yi = xi.clone()
+        dccl_amd.check(comm.all_reduce(yi.data_ptr(), yi.data_ptr(), count, 2, 0, st.cuda_stream), "all_reduce i32")
+        ri = xi.clone()
+        dist.all_reduce(ri)
+        torch.cuda.synchronize(dev)
+        out["int32_sum_bit_exact_vs_rccl"] = bool(torch.equal(yi, ri))
+        xf = torch.rand(count, device=dev, generator=g).mul_(2).sub_(1)
+        yf = xf.clone()
+        dccl_amd.check(comm.all_reduce(yf.data_ptr(), yf.data_ptr(), count, 7, 0, st.cuda_stream), "all_reduce f32")
+        rf = xf.clone()
+        dist.all_reduce(rf)
+        torch.cuda.synchronize(dev)
+        bound = (world - 1) * 1.2e-7 * world  # |x| < 1
+        out["fp32_max_abs_diff_vs_rccl"] = float((yf - rf).abs().max())
+        out["fp32_within_bound"] = out["fp32_max_abs_diff_vs_rccl"] <= bound
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dccl_amd.check(comm.all_reduce(yf.data_ptr(), yf.data_ptr(), count, 7, 0, st.cuda_stream), "all_reduce")
+        torch.cuda.synchronize(dev)
+        t_dccl = (time.perf_counter() - t0) / iters
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(rf)
+        torch.cuda.synchronize(dev)
+        t_rccl = (time.perf_counter() - t0) / iters
+        nbytes = count * 4
+        out.update({"dccl_ms": round(t_dccl * 1e3, 3), "rccl_allreduce_ms": round(t_rccl * 1e3, 3),
+                    "dccl_busbw_gb_s": round(2 * (world - 1) / world * nbytes / t_dccl / 1e9, 1),
+                    "rccl_busbw_gb_s": round(2 * (world - 1) / world * nbytes / t_rccl / 1e9, 1),
+                    "note": "RCCL's own all_reduce is an informational comparison: its combine is RCCL's"})
+    finally:
+        comm.finalize()
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -243,6 +315,12 @@ def main():
                               "note": "RCCL all_gather_into_tensor of the reduced shards over xGMI "
                                       "(every GPU ends with the full result); not in value"}
         del gathered, src
+        if backend == "nccl" and os.environ.get("DCCL_BENCH_NO_COLLECTIVE", "0") != "1":
+            count = (256 << 20) // 4 // world * world
+            ar_res, finished = run_with_watchdog(lambda: dccl_allreduce_rccl(world, rank, dev, count), 180.0)
+            extra["dccl_allreduce_rccl"] = ar_res
+            if not finished:
+                extra["dccl_allreduce_rccl"]["abandoned"] = True
 
     if rank == 0:
         traffic = None
@@ -282,6 +360,8 @@ def main():
         if world == 1 and not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(res), flush=True)
+    if extra.get("dccl_allreduce_rccl", {}).get("abandoned"):
+        os._exit(0)  # a rank is stuck inside RCCL: do not wait for it at teardown
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

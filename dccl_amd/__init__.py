@@ -94,6 +94,16 @@ def _load():
         "dccl_tune_asm_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
         "dccl_tune_variant_info": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     }
+    sig.update({
+        "dccl_comm_init_rank": (c_int, [ctypes.POINTER(c_void_p), ctypes.c_uint32, ctypes.c_uint32]),
+        "dccl_get_unique_id": (c_int, [c_void_p]),
+        "dccl_comm_init_rccl": (c_int, [ctypes.POINTER(c_void_p), ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
+        "dccl_comm_finalize": (c_int, [c_void_p]),
+        "dccl_all_reduce": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
+        "dccl_reduce_scatter": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
+        "dccl_all_gather": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_void_p]),
+        "dccl_rccl_available": (c_int, []),
+    })
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
         f.restype = res
@@ -109,6 +119,8 @@ EXPORTED_SYMBOLS = [
     "dccl_register_host_memory", "dccl_deregister_host_memory", "dccl_size_of_type",
     "dccl_result_string", "dccl_version", "dccl_tune_reduce_f32_sum", "dccl_tune_num_variants",
     "dccl_tune_variant_info", "dccl_tune_asm_f32_sum", "dccl_tune_reduce_f32_sum_lds",
+    "dccl_comm_init_rank", "dccl_get_unique_id", "dccl_comm_init_rccl", "dccl_comm_finalize", "dccl_all_reduce",
+    "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available",
 ]
 
 
@@ -155,6 +167,47 @@ def register_host_memory(ptr: int, size: int) -> int:
 
 def deregister_host_memory(ptr: int) -> int:
     return int(lib.dccl_deregister_host_memory(ptr))
+
+
+class Comm:
+    """A DCCL communicator (include/dccl/dccl_comm.h) — the namespace-dccl collectives over the
+    in-process transport (``Comm.in_process(world, rank)``, one per thread) or the cross-process
+    RCCL transport (``Comm.rccl(world, rank, unique_id)``, one process per GPU)."""
+
+    def __init__(self, handle: int):
+        self.handle = handle
+
+    @classmethod
+    def in_process(cls, world: int, rank: int) -> "Comm":
+        h = ctypes.c_void_p()
+        check(lib.dccl_comm_init_rank(ctypes.byref(h), world, rank), "dccl_comm_init_rank")
+        return cls(h.value)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        check(lib.dccl_get_unique_id(buf), "dccl_get_unique_id")
+        return buf.raw
+
+    @classmethod
+    def rccl(cls, world: int, rank: int, unique_id: bytes) -> "Comm":
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(unique_id, 128)
+        check(lib.dccl_comm_init_rccl(ctypes.byref(h), world, rank, buf), "dccl_comm_init_rccl")
+        return cls(h.value)
+
+    def all_reduce(self, send: int, recv: int, count: int, dtype: int, op: int, stream: int = 0) -> int:
+        return int(lib.dccl_all_reduce(send, recv, count, dtype, op, self.handle, stream or None))
+
+    def reduce_scatter(self, send: int, recv: int, recvcount: int, dtype: int, op: int, stream: int = 0) -> int:
+        return int(lib.dccl_reduce_scatter(send, recv, recvcount, dtype, op, self.handle, stream or None))
+
+    def all_gather(self, send: int, recv: int, sendcount: int, dtype: int, stream: int = 0) -> int:
+        return int(lib.dccl_all_gather(send, recv, sendcount, dtype, self.handle, stream or None))
+
+    def finalize(self) -> int:
+        h, self.handle = self.handle, None
+        return int(lib.dccl_comm_finalize(h)) if h else 0
 
 
 def check(code: int, what: str = "dccl") -> None:

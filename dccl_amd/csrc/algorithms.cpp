@@ -19,6 +19,7 @@
 #include <functional>
 
 #include "algorithms.hpp"
+#include "rccl_transport.hpp"
 
 namespace dccl_amd {
 
@@ -35,6 +36,16 @@ ncclResult_t reduce_scatter_ring(dccl::dcclComm* c, void* buffer, void* scratch,
     const uint32_t r = to_new(c->rank);
     auto data = [&](int64_t i) { return static_cast<unsigned char*>(buffer) + slot_bytes * mod(i, W); };
     const uint32_t to = to_old(mod(int64_t(r) + 1, W)), from = to_old(mod(int64_t(r) - 1, W));
+    if (c->rccl != nullptr) {  // cross-process: RCCL p2p into the scratchpad, then the combine
+        ncclResult_t rc = ensure_scratch(c, slot_bytes, true);
+        for (uint32_t s = 0; s + 1 < W && rc == dccl::ncclSuccess; ++s) {
+            rc = static_cast<ncclResult_t>(rccl_exchange(c->rccl, data(int64_t(r) - s), slot_bytes, to,
+                                                         c->dev_scratch, slot_bytes, from, st));
+            if (rc == dccl::ncclSuccess)
+                rc = combine(c->dev_scratch, data(int64_t(r) - s - 1), dtype, slot_elems, op, true, st);
+        }
+        return rc;
+    }
     for (uint32_t s = 0; s + 1 < W; ++s) {
         ncclResult_t rc = xport_send(c, to, data(int64_t(r) - s), slot_bytes, device, st);
         if (rc == dccl::ncclSuccess) {
@@ -60,6 +71,14 @@ ncclResult_t all_gather_ring(dccl::dcclComm* c, void* buffer, size_t slot_elems,
     const uint32_t r = to_new(c->rank);
     auto data = [&](int64_t i) { return static_cast<unsigned char*>(buffer) + slot_bytes * mod(i, W); };
     const uint32_t to = to_old(mod(int64_t(r) + 1, W)), from = to_old(mod(int64_t(r) - 1, W));
+    if (c->rccl != nullptr) {
+        for (uint32_t s = 0; s + 1 < W; ++s) {
+            const int rc = rccl_exchange(c->rccl, data(int64_t(r) - s), slot_bytes, to, data(int64_t(r) - s - 1),
+                                         slot_bytes, from, st);
+            if (rc != 0) return static_cast<ncclResult_t>(rc);
+        }
+        return dccl::ncclSuccess;
+    }
     for (uint32_t s = 0; s + 1 < W; ++s) {
         ncclResult_t rc = xport_send(c, to, data(int64_t(r) - s), slot_bytes, device, st);
         if (rc == dccl::ncclSuccess) rc = xport_recv(c, from, data(int64_t(r) - s - 1), slot_bytes, device, st);

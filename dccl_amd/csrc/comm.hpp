@@ -81,6 +81,7 @@ struct dccl::dcclComm {
     uint32_t rank = 0;
     uint32_t world = 1;
     int device = -1;  // HIP device current at init
+    void* rccl = nullptr;  // non-null: cross-process RCCL transport (rccl_transport.hpp), device buffers only
     // Per-peer event pairs for the stream-ordered device transport (reused every step:
     // a stream wait captures the event's state at the time of the wait).
     std::vector<hipEvent_t> ready_events;  // indexed by destination rank

@@ -24,8 +24,13 @@
 #include <stdexcept>
 #include <string>
 
+#include <chrono>
+#include <fstream>
+#include <thread>
+
 #include "algorithms.hpp"
 #include "comm.hpp"
+#include "rccl_transport.hpp"
 #include "dccl/dccl.hpp"
 #include "dccl/dccl_reduce.h"
 
@@ -153,16 +158,86 @@ ncclResult_t join(dcclComm** out, uint32_t world, int64_t want_rank) {
     return dccl::ncclSuccess;
 }
 
+// Cross-process communicator on the RCCL transport; the current HIP device is this rank's GPU.
+ncclResult_t join_rccl(dcclComm** out, uint32_t world, uint32_t rank, const void* id128) {
+    if (world == 0 || rank >= world || id128 == nullptr) return dccl::ncclInvalidArgument;
+    auto c = std::make_unique<dcclComm>();
+    if (hipGetDevice(&c->device) != hipSuccess) return dccl::ncclUnhandledCudaError;
+    c->rank = rank;
+    c->world = world;
+    const int rc = rccl_comm_init(&c->rccl, world, rank, id128);
+    if (rc != 0) return static_cast<ncclResult_t>(rc);
+    *out = c.release();
+    return dccl::ncclSuccess;
+}
+
+// Single-node bootstrap of the RCCL unique id through a file: rank 0 writes it (atomically, by
+// rename), the others poll for it.  Directory: DCCL_BOOTSTRAP_DIR (default /tmp); name tag:
+// DCCL_BOOTSTRAP_TAG, else MASTER_PORT (set by torchrun).
+ncclResult_t bootstrap_unique_id(uint32_t rank, unsigned char* id) {
+    const char* dir = std::getenv("DCCL_BOOTSTRAP_DIR");
+    const char* tag = std::getenv("DCCL_BOOTSTRAP_TAG");
+    if (!tag) tag = std::getenv("MASTER_PORT");
+    const std::string path = std::string(dir ? dir : "/tmp") + "/dccl_rccl_uid_" + (tag ? tag : "default");
+    if (rank == 0) {
+        const int rc = rccl_get_unique_id(id);
+        if (rc != 0) return static_cast<ncclResult_t>(rc);
+        const std::string tmp = path + ".tmp";
+        {
+            std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+            f.write(reinterpret_cast<const char*>(id), kRcclUniqueIdBytes);
+            if (!f) return dccl::ncclSystemError;
+        }
+        if (std::rename(tmp.c_str(), path.c_str()) != 0) return dccl::ncclSystemError;
+        return dccl::ncclSuccess;
+    }
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+    while (std::chrono::steady_clock::now() < deadline) {
+        std::ifstream f(path, std::ios::binary);
+        if (f.read(reinterpret_cast<char*>(id), kRcclUniqueIdBytes)) return dccl::ncclSuccess;
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+    return dccl::ncclSystemError;
+}
+
+long env_long(const char* a, const char* b, long dflt) {
+    const char* v = std::getenv(a);
+    if (!v && b) v = std::getenv(b);
+    return v ? std::strtol(v, nullptr, 10) : dflt;
+}
+
+bool rccl_requested() {
+    const char* t = std::getenv("DCCL_TRANSPORT");
+    return t != nullptr && std::string(t) == "rccl";
+}
+
 }  // namespace
 
 namespace dccl {
 
 ncclResult_t ncclCommInit(ncclComm_t* comm) {
     if (comm == nullptr) return ncclInvalidArgument;
-    const char* ws = std::getenv("DCCL_WORLD_SIZE");
-    const long w = ws ? std::strtol(ws, nullptr, 10) : 1;
+    const long w = env_long("DCCL_WORLD_SIZE", rccl_requested() ? "WORLD_SIZE" : nullptr, 1);
     if (w <= 0) return ncclInvalidArgument;
+    if (rccl_requested()) {  // one process per GPU: rank / world from the launcher's environment
+        const long r = env_long("DCCL_RANK", "RANK", 0);
+        if (r < 0 || r >= w) return ncclInvalidArgument;
+        unsigned char id[kRcclUniqueIdBytes];
+        const ncclResult_t rc = bootstrap_unique_id(static_cast<uint32_t>(r), id);
+        if (rc != ncclSuccess) return rc;
+        return join_rccl(comm, static_cast<uint32_t>(w), static_cast<uint32_t>(r), id);
+    }
     return join(comm, static_cast<uint32_t>(w), -1);
+}
+
+ncclResult_t dcclGetUniqueId(void* id128) {
+    if (id128 == nullptr) return ncclInvalidArgument;
+    return static_cast<ncclResult_t>(rccl_get_unique_id(id128));
+}
+
+ncclResult_t dcclCommInitRccl(ncclComm_t* comm, uint32_t world_size, uint32_t rank, const void* id128) {
+    if (comm == nullptr) return ncclInvalidArgument;
+    return join_rccl(comm, world_size, rank, id128);
 }
 
 ncclResult_t dcclCommInitRank(ncclComm_t* comm, uint32_t world_size, uint32_t rank) {
@@ -174,7 +249,12 @@ ncclResult_t ncclCommFinalize(ncclComm_t comm) {
     validate_comm(comm, __func__);
     ncclResult_t rc = ncclSuccess;
     if (comm->device >= 0 && hipDeviceSynchronize() != hipSuccess) rc = ncclUnhandledCudaError;
-    comm->group->barrier();  // no peer may still be reading our buffers
+    if (comm->rccl != nullptr) {
+        const int r = rccl_comm_destroy(comm->rccl);
+        if (rc == ncclSuccess) rc = static_cast<ncclResult_t>(r);
+    } else {
+        comm->group->barrier();  // no peer may still be reading our buffers
+    }
     for (hipEvent_t e : comm->ready_events)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : comm->done_events)
@@ -228,6 +308,7 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
     if (sendbuff == nullptr || recvbuff == nullptr) return ncclInvalidArgument;
     bool dev = false;
     if ((rc = placement(sendbuff, recvbuff, &dev)) != ncclSuccess) return rc;
+    if (comm->rccl != nullptr && !dev) return ncclInvalidUsage;  // the RCCL transport moves device memory
     const size_t total = count * size_of_dtype(datatype);
     const uint32_t W = comm->world;
     if (W > 1 && (count < W || count % W)) return ncclInvalidArgument;
@@ -247,6 +328,7 @@ ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recv
     if (sendbuff == nullptr || recvbuff == nullptr) return ncclInvalidArgument;
     bool dev = false;
     if ((rc = placement(sendbuff, recvbuff, &dev)) != ncclSuccess) return rc;
+    if (comm->rccl != nullptr && !dev) return ncclInvalidUsage;
     const uint32_t W = comm->world, r = comm->rank;
     const size_t slot = recvcount * size_of_dtype(datatype), total = slot * W;
     if ((rc = ensure_work(comm, total, dev)) != ncclSuccess) return rc;
@@ -276,6 +358,7 @@ ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, nccl
     if (sendbuff == nullptr || (iamroot && recvbuff == nullptr)) return ncclInvalidArgument;
     bool dev = false;
     if ((rc = placement(sendbuff, iamroot ? recvbuff : sendbuff, &dev)) != ncclSuccess) return rc;
+    if (comm->rccl != nullptr && !dev) return ncclInvalidUsage;
     const size_t total = count * size_of_dtype(datatype), slot = total / W;
     void* rbuf = recvbuff;
     if (!iamroot) {
@@ -290,6 +373,8 @@ ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, nccl
                              [W](uint32_t o) { return (o + W - 1) % W; }, [W](uint32_t n) { return (n + 1) % W; });
     if (rc != ncclSuccess) return rc;
     auto at = [&](uint32_t i) { return static_cast<unsigned char*>(rbuf) + size_t(i) * slot; };
+    if (comm->rccl != nullptr)
+        return static_cast<ncclResult_t>(rccl_gather_p2p(comm->rccl, rbuf, slot, uint32_t(root), r, W, stream));
     if (iamroot) {
         for (uint32_t p = 0; p < W; ++p)
             if (p != r && (rc = xport_recv(comm, p, at(p), slot, dev, stream)) != ncclSuccess) return rc;
@@ -309,6 +394,7 @@ ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcoun
     bool dev = false;
     ncclResult_t rc = placement(sendbuff, recvbuff, &dev);
     if (rc != ncclSuccess) return rc;
+    if (comm->rccl != nullptr && !dev) return ncclInvalidUsage;
     void* slot = static_cast<unsigned char*>(recvbuff) + sendcount * comm->rank * esz;
     if ((rc = copy_bytes(slot, sendbuff, sendcount * esz, dev, stream)) != ncclSuccess) return rc;
     const RankMap id = [](uint32_t x) { return x; };
@@ -326,6 +412,13 @@ ncclResult_t ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, n
     bool dev = false;
     ncclResult_t rc = placement(r == uint32_t(root) ? sendbuff : recvbuff, recvbuff, &dev);
     if (rc != ncclSuccess) return rc;
+    if (comm->rccl != nullptr) {
+        if (!dev) return ncclInvalidUsage;
+        rc = static_cast<ncclResult_t>(rccl_bcast_p2p(comm->rccl, sendbuff, recvbuff, bytes, uint32_t(root), r, W,
+                                                      stream));
+        if (rc == ncclSuccess && r == uint32_t(root)) rc = copy_bytes(recvbuff, sendbuff, bytes, true, stream);
+        return rc;
+    }
     if (r == uint32_t(root)) {
         for (uint32_t p = 0; p < W; ++p)
             if (p != r && (rc = xport_send(comm, p, sendbuff, bytes, dev, stream)) != ncclSuccess) return rc;
@@ -349,6 +442,10 @@ ncclResult_t ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatyp
     if (esz == 0 || peer < 0 || uint32_t(peer) >= comm->world || uint32_t(peer) == comm->rank)
         return ncclInvalidArgument;  // dccl.cpp:869-872
     const bool dev = is_device_ptr(sendbuff);
+    if (comm->rccl != nullptr)
+        return dev ? static_cast<ncclResult_t>(rccl_exchange(comm->rccl, sendbuff, count * esz, uint32_t(peer),
+                                                             nullptr, 0, 0, stream))
+                   : ncclInvalidUsage;
     ncclResult_t rc = xport_send(comm, uint32_t(peer), sendbuff, count * esz, dev, stream);
     if (rc != ncclSuccess) return rc;
     return xport_wait_send(comm, uint32_t(peer), dev, stream);
@@ -360,7 +457,74 @@ ncclResult_t ncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int
     const size_t esz = size_of_dtype(datatype);
     if (esz == 0 || peer < 0 || uint32_t(peer) >= comm->world || uint32_t(peer) == comm->rank)
         return ncclInvalidArgument;  // dccl.cpp:893-896
-    return xport_recv(comm, uint32_t(peer), recvbuff, count * esz, is_device_ptr(recvbuff), stream);
+    const bool dev = is_device_ptr(recvbuff);
+    if (comm->rccl != nullptr)
+        return dev ? static_cast<ncclResult_t>(rccl_exchange(comm->rccl, nullptr, 0, 0, recvbuff, count * esz,
+                                                             uint32_t(peer), stream))
+                   : ncclInvalidUsage;
+    return xport_recv(comm, uint32_t(peer), recvbuff, count * esz, dev, stream);
 }
 
 }  // namespace dccl
+
+// ------------------------------------------------------------------------------------------
+// C-ABI of the collectives (include/dccl/dccl_comm.h): plain pointers for FFI callers.
+// ------------------------------------------------------------------------------------------
+namespace {
+template <typename F>
+int guarded(F&& f) {
+    try {
+        return static_cast<int>(f());
+    } catch (const std::exception&) {
+        return DCCL_INVALID_ARGUMENT;  // null / invalid communicator (VALIDATE_COMM)
+    }
+}
+}  // namespace
+
+extern "C" int dccl_comm_init_rank(void** comm, uint32_t world, uint32_t rank) {
+    if (comm == nullptr) return DCCL_INVALID_ARGUMENT;
+    return guarded([&] { return dccl::dcclCommInitRank(reinterpret_cast<dccl::ncclComm_t*>(comm), world, rank); });
+}
+
+extern "C" int dccl_get_unique_id(void* id128) {
+    return guarded([&] { return dccl::dcclGetUniqueId(id128); });
+}
+
+extern "C" int dccl_comm_init_rccl(void** comm, uint32_t world, uint32_t rank, const void* id128) {
+    if (comm == nullptr) return DCCL_INVALID_ARGUMENT;
+    return guarded([&] {
+        return dccl::dcclCommInitRccl(reinterpret_cast<dccl::ncclComm_t*>(comm), world, rank, id128);
+    });
+}
+
+extern "C" int dccl_comm_finalize(void* comm) {
+    return guarded([&] { return dccl::ncclCommFinalize(static_cast<dccl::ncclComm_t>(comm)); });
+}
+
+extern "C" int dccl_all_reduce(const void* send, void* recv, size_t count, int dtype, int op, void* comm,
+                               void* stream) {
+    return guarded([&] {
+        return dccl::ncclAllReduce(send, recv, count, static_cast<dccl::ncclDataType_t>(dtype),
+                                   static_cast<dccl::ncclRedOp_t>(op), static_cast<dccl::ncclComm_t>(comm),
+                                   static_cast<hipStream_t>(stream));
+    });
+}
+
+extern "C" int dccl_reduce_scatter(const void* send, void* recv, size_t recvcount, int dtype, int op, void* comm,
+                                   void* stream) {
+    return guarded([&] {
+        return dccl::ncclReduceScatter(send, recv, recvcount, static_cast<dccl::ncclDataType_t>(dtype),
+                                       static_cast<dccl::ncclRedOp_t>(op), static_cast<dccl::ncclComm_t>(comm),
+                                       static_cast<hipStream_t>(stream));
+    });
+}
+
+extern "C" int dccl_all_gather(const void* send, void* recv, size_t sendcount, int dtype, void* comm,
+                               void* stream) {
+    return guarded([&] {
+        return dccl::ncclAllGather(send, recv, sendcount, static_cast<dccl::ncclDataType_t>(dtype),
+                                   static_cast<dccl::ncclComm_t>(comm), static_cast<hipStream_t>(stream));
+    });
+}
+
+extern "C" int dccl_rccl_available(void) { return rccl_available(); }

@@ -72,6 +72,12 @@ typedef struct dcclComm* ncclComm_t;
 ncclResult_t ncclCommInit(ncclComm_t* comm);
 /** MI355X-build extension: join the process's group at an explicit rank. */
 ncclResult_t dcclCommInitRank(ncclComm_t* comm, uint32_t world_size, uint32_t rank);
+/** MI355X-build extension: cross-process communicator on the RCCL (xGMI) transport, one process
+ *  per GPU (the current HIP device).  `unique_id` is 128 bytes from dcclGetUniqueId on one rank.
+ *  ncclCommInit selects this transport itself when DCCL_TRANSPORT=rccl (rank/world from
+ *  RANK/WORLD_SIZE, id exchanged through a file in DCCL_BOOTSTRAP_DIR). Device buffers only. */
+ncclResult_t dcclGetUniqueId(void* unique_id);
+ncclResult_t dcclCommInitRccl(ncclComm_t* comm, uint32_t world_size, uint32_t rank, const void* unique_id);
 ncclResult_t ncclCommFinalize(ncclComm_t comm);
 
 /** Page-lock host memory for direct DMA (device memory: accepted, nothing to do). */

@@ -1,0 +1,34 @@
+/*
+ * include/dccl/dccl_comm.h — C-ABI of the collectives built around the combine, for FFI callers
+ * (the C++ surface is include/dccl/dccl.hpp).  Communicators are opaque `void*`; integer enums
+ * and results are the ncclDataType_t / ncclRedOp_t / ncclResult_t values.
+ *
+ *   dccl_comm_init_rank   in-process group: one communicator per thread, blocks until all
+ *                         `world` ranks joined (dcclCommInitRank)
+ *   dccl_get_unique_id /  cross-process group over the RCCL (xGMI) transport, one process per
+ *   dccl_comm_init_rccl   GPU; the 128-byte id travels out of band (dcclCommInitRccl)
+ *   dccl_all_reduce       ncclAllReduce       (/root/reference/include/dccl/dccl.hpp:206-207)
+ *   dccl_reduce_scatter   ncclReduceScatter   (/root/reference/include/dccl/dccl.hpp:243-244)
+ *   dccl_all_gather       ncclAllGather       (/root/reference/include/dccl/dccl.hpp:392-393)
+ * A null / finalized communicator returns ncclInvalidArgument (4) instead of throwing.
+ */
+#ifndef DCCL_COMM_H_
+#define DCCL_COMM_H_
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+int dccl_comm_init_rank(void** comm, uint32_t world, uint32_t rank);
+int dccl_get_unique_id(void* unique_id_128);
+int dccl_comm_init_rccl(void** comm, uint32_t world, uint32_t rank, const void* unique_id_128);
+int dccl_comm_finalize(void* comm);
+int dccl_all_reduce(const void* send, void* recv, size_t count, int dtype, int op, void* comm, void* stream);
+int dccl_reduce_scatter(const void* send, void* recv, size_t recvcount, int dtype, int op, void* comm,
+                        void* stream);
+int dccl_all_gather(const void* send, void* recv, size_t sendcount, int dtype, void* comm, void* stream);
+int dccl_rccl_available(void);
+#ifdef __cplusplus
+}
+#endif
+#endif
