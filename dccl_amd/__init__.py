@@ -103,6 +103,7 @@ def _load():
         "dccl_reduce_scatter": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
         "dccl_all_gather": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_void_p]),
         "dccl_rccl_available": (c_int, []),
+        "dccl_tune_skew_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),
     })
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -120,7 +121,7 @@ EXPORTED_SYMBOLS = [
     "dccl_result_string", "dccl_version", "dccl_tune_reduce_f32_sum", "dccl_tune_num_variants",
     "dccl_tune_variant_info", "dccl_tune_asm_f32_sum", "dccl_tune_reduce_f32_sum_lds",
     "dccl_comm_init_rank", "dccl_get_unique_id", "dccl_comm_init_rccl", "dccl_comm_finalize", "dccl_all_reduce",
-    "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available",
+    "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available", "dccl_tune_skew_f32_sum",
 ]
 
 

@@ -460,3 +460,42 @@ extern "C" int dccl_tune_asm_f32_sum(const void* send, void* recv, size_t count,
     void* args[] = {&send, &recv, const_cast<size_t*>(&nvec)};
     return launch(fns[flavor], nvec / 64, args, static_cast<hipStream_t>(stream), 64);
 }
+
+// ---------------------------------------------------------------------------------
+// Tuning only: decorrelate the send/recv addresses each wave issues together.  A block of
+// WAVES one-wave tiles loads recv tile w and send tile (w + SKEW) % WAVES, so the two loads a
+// wave has in flight are SKEW KiB apart; send vectors are exchanged through LDS behind one
+// barrier.  SKEW = 0 is the control (same pairing as the shipped kernel, plus the LDS hop).
+// fp32 Sum; count must be a multiple of WAVES * 256 elements.
+// ---------------------------------------------------------------------------------
+namespace {
+template <int WAVES, int SKEW>
+__global__ __launch_bounds__(WAVES * 64) void tune_skew_kernel(const u32x4* __restrict__ s, u32x4* __restrict__ r) {
+    __shared__ u32x4 lds[WAVES * 64];
+    const size_t base = size_t(blockIdx.x) * WAVES * 64;
+    const int w = threadIdx.x / 64, l = threadIdx.x % 64;
+    const int ws = (w + SKEW) % WAVES;
+    const u32x4 sv = __builtin_nontemporal_load(s + base + ws * 64 + l);
+    const u32x4 rv = __builtin_nontemporal_load(r + base + w * 64 + l);
+    lds[ws * 64 + l] = sv;
+    __syncthreads();
+    __builtin_nontemporal_store(combine16<float, kSum>(rv, lds[w * 64 + l]), r + base + w * 64 + l);
+}
+}  // namespace
+
+extern "C" int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count, int waves, int skew,
+                                      void* stream) {
+    if (((reinterpret_cast<uintptr_t>(send) | reinterpret_cast<uintptr_t>(recv)) & 15)) return DCCL_INVALID_ARGUMENT;
+    const void* fn = nullptr;
+    if (waves == 8 && skew == 0) fn = reinterpret_cast<const void*>(&tune_skew_kernel<8, 0>);
+    if (waves == 8 && skew == 1) fn = reinterpret_cast<const void*>(&tune_skew_kernel<8, 1>);
+    if (waves == 8 && skew == 2) fn = reinterpret_cast<const void*>(&tune_skew_kernel<8, 2>);
+    if (waves == 8 && skew == 4) fn = reinterpret_cast<const void*>(&tune_skew_kernel<8, 4>);
+    if (waves == 4 && skew == 0) fn = reinterpret_cast<const void*>(&tune_skew_kernel<4, 0>);
+    if (waves == 4 && skew == 2) fn = reinterpret_cast<const void*>(&tune_skew_kernel<4, 2>);
+    if (waves == 16 && skew == 8) fn = reinterpret_cast<const void*>(&tune_skew_kernel<16, 8>);
+    if (waves == 16 && skew == 4) fn = reinterpret_cast<const void*>(&tune_skew_kernel<16, 4>);
+    if (fn == nullptr || count % (size_t(waves) * 256)) return DCCL_INVALID_ARGUMENT;
+    void* args[] = {&send, &recv};
+    return launch(fn, count / (size_t(waves) * 256), args, static_cast<hipStream_t>(stream), waves * 64);
+}

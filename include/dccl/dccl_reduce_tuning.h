@@ -23,6 +23,9 @@ int dccl_tune_reduce_f32_sum(const void* send, void* recv, size_t count, int var
 /* Same, with `lds_bytes` of (unused) dynamic LDS per block to cap waves per CU. */
 int dccl_tune_reduce_f32_sum_lds(const void* send, void* recv, size_t count, int variant, size_t grid_cap,
                                  size_t lds_bytes, void* stream);
+/* Block of `waves` one-wave tiles; each wave pairs recv tile w with send tile (w+skew)%waves,
+ * exchanging send through LDS (tests address-pair decorrelation). */
+int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count, int waves, int skew, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -58,6 +58,10 @@ def main():
         cases[("lds", lds)] = (
             lambda lds=lds: lib.dccl_tune_reduce_f32_sum_lds(s.data_ptr(), r.data_ptr(), n, 0, 0, lds, st),
             {"kind": "occupancy", "variant": info[0], "lds_bytes": lds, "max_waves_per_cu": (160 << 10) // lds})
+    for waves, skew in ((8, 0), (8, 1), (8, 2), (8, 4), (4, 0), (4, 2), (16, 8), (16, 4)):
+        cases[("skew", waves, skew)] = (
+            lambda waves=waves, skew=skew: lib.dccl_tune_skew_f32_sum(s.data_ptr(), r.data_ptr(), n, waves, skew, st),
+            {"kind": "skew", "waves": waves, "skew_kib": skew})
     for fl in range(7):
         cases[("asm", fl)] = (lambda fl=fl: lib.dccl_tune_asm_f32_sum(s.data_ptr(), r.data_ptr(), n, fl, st),
                               {"kind": "asm", "flavor": fl})
@@ -94,7 +98,10 @@ def main():
         with open(a.out, "w") as f:
             f.write(txt)
     for row in rows:
-        print(json.dumps(row))
+        try:
+            print(json.dumps(row))
+        except BrokenPipeError:
+            break
 
 
 if __name__ == "__main__":
