@@ -177,8 +177,16 @@ def dccl_allreduce_rccl(world: int, rank: int, dev, count: int, iters: int = 5) 
     """the namespace-dccl ncclAllReduce (ring RS with the gfx950 combine + ring AG)
     over the RCCL p2p transport, one process per GPU; checked against RCCL's own all_reduce
     (int32: bit-exact; fp32: |d| <= (W-1) eps sum|x|, a different association order) and timed."""
-    obj = [dccl_amd.Comm.unique_id() if rank == 0 else None]
+    uid = None
+    if rank == 0:
+        try:
+            uid = dccl_amd.Comm.unique_id()
+        except Exception:  # every rank must still reach the broadcast below
+            uid = None
+    obj = [uid]
     dist.broadcast_object_list(obj, src=0)
+    if obj[0] is None:
+        raise RuntimeError("rank 0 could not create an RCCL unique id (librccl not loadable?)")
     comm = dccl_amd.Comm.rccl(world, rank, obj[0])
     out = {"count": count, "world": world}
     try:
@@ -360,11 +368,15 @@ def main():
         if world == 1 and not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(res), flush=True)
-    if extra.get("dccl_allreduce_rccl", {}).get("abandoned"):
-        os._exit(0)  # a rank is stuck inside RCCL: do not wait for it at teardown
+    ar = extra.get("dccl_allreduce_rccl", {})
+    if ar.get("abandoned") or "error" in ar:
+        os._exit(0)  # a rank may be stuck inside RCCL: never wait for it at teardown
     if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        try:
+            dist.barrier()
+            dist.destroy_process_group()
+        except Exception:  # a peer left early after printing its part; the line is out
+            os._exit(0)
 
 
 if __name__ == "__main__":
