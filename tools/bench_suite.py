@@ -190,14 +190,35 @@ def c1(results):
     results["c1"] = rows
 
 
+def misaligned(results, mib=1024):
+    """Operands off the 16-B phase of each other (scalar element kernel) or off element alignment
+    (byte-gather kernel): the fallback paths, fp32 Sum, 1 GiB."""
+    st = torch.cuda.current_stream().cuda_stream
+    nbytes = mib << 20
+    n = nbytes // 4 - 4
+    s = fill(nbytes, 7, 0, 1)
+    r = fill(nbytes, 7, 0, 2)
+    rows = []
+    for soff, roff, what in ((0, 0, "aligned (vector path)"), (16, 0, "same 16-B phase, offset 16 B (vector)"),
+                             (4, 0, "4-B phase mismatch (scalar element path)"), (8, 4, "8/4-B offsets (scalar)"),
+                             (1, 1, "byte offsets, same phase (element-misaligned byte path)")):
+        fn = lambda soff=soff, roff=roff: dccl_amd.local_reduce(s.data_ptr() + soff, r.data_ptr() + roff, 7, n, 0, st)
+        med, _ = time_launches([fn], rounds=5)
+        gbs = 3 * n * 4 / (med * 1e-3) / 1e9
+        rows.append({"send_offset": soff, "recv_offset": roff, "path": what, "ms": round(med, 4),
+                     "gb_s": round(gbs, 1), "frac": round(gbs / PEAK, 4)})
+        print("misaligned", rows[-1], flush=True)
+    results["misaligned"] = rows
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--parts", default="c3,c4,c2,kway,host,c1")
+    p.add_argument("--parts", default="c3,c4,c2,kway,host,c1,misaligned")
     p.add_argument("--out", default="")
     a = p.parse_args()
     results = {"device": torch.cuda.get_device_name(0), "peak_gb_s": PEAK}
     for part in a.parts.split(","):
-        {"c3": c3, "c4": c4, "c2": c2, "kway": kway, "host": host, "c1": c1}[part](results)
+        {"c3": c3, "c4": c4, "c2": c2, "kway": kway, "host": host, "c1": c1, "misaligned": misaligned}[part](results)
         if a.out:
             with open(a.out, "w") as f:
                 json.dump(results, f, indent=1)
