@@ -15,6 +15,8 @@ Outputs (data only: inputs and expected outputs):
 * ``host_reduce_half.npz`` — float16 / bfloat16 (no reference host path: SURVEY.md
   A.2/A.3 #6): outputs of numpy float16 arithmetic and torch CPU bfloat16 arithmetic
   — independent of both the oracle and the HIP kernel.
+* ``misaligned_ref.npz`` — SURVEY.md A.4 cases (recv off a 64-B line): the reference's output
+  (it re-combines the tail and writes past `count`) next to the correct result the build gives.
 * ``rc_cases.json`` — return codes of the reference for Avg / bad op / count 0.
 
 The C1 ring goldens (dccl_cli all_reduce) live in ``c1_ring.json``,
@@ -130,6 +132,38 @@ def gen_half():
     np.savez_compressed(os.path.join(HERE, "host_reduce_half.npz"), **out)
 
 
+def gen_misaligned():
+    """SURVEY.md A.4 'reference-wrong, build-correct' expectations: recv off a 64-B line with
+    count % P < head.  The reference loop (run on padded buffers) re-combines the tail and writes
+    past `count`; the build must produce the plain element-wise result."""
+    rng = np.random.default_rng(SEED + 2)
+    out = {}
+    cases = [(7, 32, 100), (7, 4, 33), (2, 48, 70), (8, 8, 13), (0, 1, 130), (4, 16, 21)]
+    for i, (dt, off, n) in enumerate(cases):
+        npd = oracle.NP_DTYPES[dt]
+        pad = 64
+        if np.issubdtype(npd, np.integer):
+            info = np.iinfo(npd)
+            s = rng.integers(info.min // 2, info.max // 2, n + pad, dtype=npd)
+            r = rng.integers(info.min // 2, info.max // 2, n + pad, dtype=npd)
+        else:
+            s = rng.uniform(-1, 1, n + pad).astype(npd)
+            r = rng.uniform(-1, 1, n + pad).astype(npd)
+        ss = oracle.aligned_empty(n + pad, npd, offset_bytes=off)
+        rr = oracle.aligned_empty(n + pad, npd, offset_bytes=off)
+        ss[:] = s
+        rr[:] = r
+        assert oracle.ref_reduce(ss, rr, dt, 0, count=n) == 0  # Sum over the first n only
+        correct = r.copy()
+        correct[:n] = oracle.combine(s[:n], r[:n], dt, 0)
+        out[f"c{i}_meta"] = np.array([dt, off, n], dtype=np.int64)
+        out[f"c{i}_send"] = s
+        out[f"c{i}_recv"] = r
+        out[f"c{i}_ref"] = np.array(rr)        # reference result incl. the overrun into the padding
+        out[f"c{i}_correct"] = correct         # build contract: only [0, n) changes
+    np.savez_compressed(os.path.join(HERE, "misaligned_ref.npz"), **out)
+
+
 def gen_rc():
     cases = []
     for dt in HOST_DTYPES:
@@ -149,5 +183,6 @@ if __name__ == "__main__":
         sys.exit("oracle/_ref missing: run `make -C oracle` in the container that has /root/reference")
     gen_ref()
     gen_half()
+    gen_misaligned()
     gen_rc()
     print("golden fixtures written to", HERE)

@@ -309,3 +309,16 @@ def test_one_gib_inverse_roundtrip(dccl):
     s.neg_()
     assert dccl.local_reduce(s.data_ptr(), r.data_ptr(), 2, n, 0, 0) == 0
     assert torch.equal(r, r0)
+
+
+def test_misaligned_reference_wrong_build_correct(dccl):
+    """SURVEY.md A.4 fixtures: at the reference's own misaligned recv offsets the HIP combine gives the
+    element-wise result and touches nothing past `count`; the reference's output differs."""
+    from tests.test_oracle import _misaligned_cases
+    for i, dt, off, n, s, r, ref, correct in _misaligned_cases():
+        ts, ps = dev_bytes(s, off)
+        tr, pr = dev_bytes(r, off)
+        assert dccl.local_reduce(ps, pr, dt, n, 0, 0) == 0
+        torch.cuda.synchronize()
+        got = host_of(tr, off, r)
+        assert got.tobytes() == correct.tobytes(), i

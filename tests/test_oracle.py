@@ -195,3 +195,26 @@ def test_c1_ring_goldens_with_oracle(kind):
         want = int(g[kind][str(target)], 16)
         for b in bufs:
             assert np.all(b.view(np.uint32) == want), (kind, target, hex(int(b.view(np.uint32)[0])))
+
+
+def _misaligned_cases():
+    z = np.load(os.path.join(GOLDEN, "misaligned_ref.npz"))
+    for i in range(len([k for k in z.files if k.endswith("_meta")])):
+        dt, off, n = (int(x) for x in z[f"c{i}_meta"])
+        yield i, dt, off, n, z[f"c{i}_send"], z[f"c{i}_recv"], z[f"c{i}_ref"], z[f"c{i}_correct"]
+
+
+def test_misaligned_fixture_reference_vs_restatement():
+    """The faithful restatement reproduces the reference's A.4 output (overrun included) on the same
+    layout; the fixture's `correct` is what the build must produce and differs where A.4 bites."""
+    diverging = 0
+    for i, dt, off, n, s, r, ref, correct in _misaligned_cases():
+        npd = oracle.NP_DTYPES[dt]
+        ss = oracle.aligned_empty(s.size, npd, offset_bytes=off)
+        rr = oracle.aligned_empty(r.size, npd, offset_bytes=off)
+        ss[:] = s
+        rr[:] = r
+        assert oracle.host_reduce(ss, rr, dt, 0, count=n) == 0
+        assert rr.tobytes() == ref.tobytes(), i
+        diverging += ref.tobytes() != correct.tobytes()
+    assert diverging >= 4
