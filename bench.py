@@ -4,7 +4,9 @@
 One "step" = one pass of the combine ``recv[i] = recv[i] + send[i]`` over 1 GiB fp32
 operands resident in HBM (BASELINE.json metric: ncclSum fp32, 1 GiB).  Each rank owns its
 own 1 GiB shard pair (the combine is element-wise: no data-path collective), so the
-aggregate is weak scaling.
+aggregate is weak scaling.  Operands are carved from one HBM allocation (recv, then send 4 KiB
+past its end); the separately allocated layout is timed too and reported as `other_layout`
+(separate 1 GiB allocations land in one of two physical placement modes).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--mib 1024] [--dtype float32] [--op sum]
 
@@ -58,6 +60,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-host-staged", action="store_true")
+    p.add_argument("--layout", default="pooled", choices=["pooled", "separate"],
+                   help="operand placement in HBM (see operand_pair); the other layout is also timed briefly")
     return p.parse_args()
 
 
@@ -73,6 +77,41 @@ def synth(n: int, dt: int, op: int, seed: int, device) -> torch.Tensor:
                         generator=g, dtype=torch.int32)
     return raw.view(torch.uint8)[: n * dccl_amd.size_of_type(dt)].view(torch.int8) if dt in (0, 1) else \
         raw.view(torch.int64 if dt in (4, 5) else torch.int32)[:n]
+
+
+PAIR_GAP = 4096  # bytes between the end of recv and the start of send in the pooled layout
+
+
+def operand_pair(n: int, dt: int, op: int, seed: int, device, layout: str):
+    """(send, recv) synthetic operands.  "pooled": both carved from ONE HBM allocation, recv first
+    and send PAIR_GAP bytes past its end; "separate": two allocations (DCCL's own shape: scratchpad
+    + user chunk).  Separately allocated 1 GiB operands land in one of two physical placement modes
+    (0.476 vs 0.508 ms on MI355X); the pooled layout is consistently in the fast one."""
+    s = synth(n, dt, op, seed, device)
+    r = synth(n, dt, op, seed + 1, device)
+    if layout == "separate":
+        return s, r
+    nbytes = n * dccl_amd.size_of_type(dt)
+    pool = torch.empty(2 * nbytes + PAIR_GAP, dtype=torch.uint8, device=device)
+    recv = pool[:nbytes].view(r.dtype)
+    send = pool[nbytes + PAIR_GAP:].view(s.dtype)
+    recv.copy_(r)
+    send.copy_(s)
+    del s, r
+    return send, recv
+
+
+def time_kernel(ps: int, pr: int, dt: int, n: int, op: int, stream, steps: int) -> float:
+    """Average launch duration (ms) over `steps` back-to-back launches, HIP events on `stream`."""
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        dccl_amd.check(dccl_amd.local_reduce(ps, pr, dt, n, op, stream.cuda_stream))
+    ev0.record(stream)
+    for _ in range(steps):
+        dccl_amd.check(dccl_amd.local_reduce(ps, pr, dt, n, op, stream.cuda_stream))
+    ev1.record(stream)
+    ev1.synchronize()
+    return ev0.elapsed_time(ev1) / steps
 
 
 def cpu_baseline(budget_s: float) -> dict | None:
@@ -261,8 +300,7 @@ def main():
         total_bytes = world * n * esz
     nbytes = n * esz
 
-    send = synth(n, dt, op, 0xDCC1 + 2 * rank, dev)
-    recv = synth(n, dt, op, 0xDCC1 + 2 * rank + 1, dev)
+    send, recv = operand_pair(n, dt, op, 0xDCC1 + 2 * rank, dev, a.layout)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     ps, pr = send.data_ptr(), recv.data_ptr()
@@ -301,6 +339,15 @@ def main():
     ms_per_step = elapsed / a.steps * 1e3
 
     extra = {}
+    # the other operand layout, timed briefly on every rank (reported, never in `value`)
+    other = "separate" if a.layout == "pooled" else "pooled"
+    del send, recv
+    torch.cuda.empty_cache()
+    s2, r2 = operand_pair(n, dt, op, 0xDCC1 + 2 * rank, dev, other)
+    k2 = time_kernel(s2.data_ptr(), r2.data_ptr(), dt, n, op, stream, max(10, a.steps // 4))
+    extra["other_layout"] = {"layout": other, "kernel_ms_avg": round(k2, 4),
+                             "frac": round(3 * nbytes / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    send, recv = s2, r2  # the all-gather below only needs a reduced shard of the right size
     if world > 1:  # the one exchange step of C5: RCCL all-gather of the reduced shards (separate)
         width = max(b - a_ for a_, b in bounds) if strong else n
         src = recv if width == n else torch.cat([recv, recv.new_zeros(width - n)])
@@ -348,7 +395,7 @@ def main():
             "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": {0: "i8", 1: "u8", 2: "i32", 3: "u32", 4: "i64", 5: "u64", 6: "f16", 7: "f32", 8: "f64",
                       9: "bf16"}[dt],
-            "data": "synthetic (seeded uniform [-1,1) operands resident in HBM)",
+            "data": f"synthetic (seeded uniform [-1,1) operands resident in HBM, {a.layout} layout)",
             "config": {"workload": (f"C5: {a.total_gib:g} GiB per operand sharded over {world} GPU(s), "
                                     f"in-place combine recv=op(recv,send), {a.op}") if strong else
                                    (f"in-place two-buffer combine recv=op(recv,send), {a.op}, "
@@ -360,7 +407,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "reduce_vec_kernel (dccl_local_reduce)",
                          "kernel_ms_avg": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_ms_max, 4),
-                         "bytes_per_launch": 3 * nbytes},
+                         "bytes_per_launch": 3 * nbytes, "operand_layout": a.layout},
         }
         res.update(extra)
         if world == 1 and not a.no_host_staged:

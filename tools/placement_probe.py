@@ -22,17 +22,24 @@ N = (1 << 30) // 4
 ST = 0
 
 
-def timeit(sp, rp, rounds=10, iters=10):
+VARIANTS = {}
+
+
+def timeit(sp, rp, rounds=10, iters=10, variant=None):
     st = torch.cuda.current_stream().cuda_stream
+    if variant is None:
+        call = lambda: dccl_amd.local_reduce(sp, rp, 7, N, 0, st)
+    else:
+        call = lambda: dccl_amd.lib.dccl_tune_reduce_f32_sum_lds(sp, rp, N, variant, 0, 7 << 10, st)
     for _ in range(3):
-        dccl_amd.local_reduce(sp, rp, 7, N, 0, st)
+        call()
     torch.cuda.synchronize()
     ts = []
     for _ in range(rounds):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(iters):
-            dccl_amd.local_reduce(sp, rp, 7, N, 0, st)
+            call()
         e1.record()
         e1.synchronize()
         ts.append(e0.elapsed_time(e1) / iters)
@@ -42,14 +49,26 @@ def timeit(sp, rp, rounds=10, iters=10):
 
 def main():
     rows = []
-    for k in range(4):
+    info = dccl_amd.tune_variants()
+    v_plain = next(i for i, v in enumerate(info) if v == {"block": 64, "unroll": 1, "policy": 7, "xcd": 0})
+    v_xcd = next(i for i, v in enumerate(info) if v == {"block": 64, "unroll": 1, "policy": 7, "xcd": 1})
+    keep = []  # hold allocations so later pairs land elsewhere in physical memory
+    for k in range(6):
         s = torch.empty(N, device="cuda").uniform_(-1, 1)
         r = torch.empty(N, device="cuda").uniform_(-1, 1)
-        rows.append({"case": f"sep-{k}", "delta_mib": (s.data_ptr() - r.data_ptr()) / 2**20,
-                     **timeit(s.data_ptr(), r.data_ptr())})
-        print(rows[-1], flush=True)
-        del s, r
+        row = {"case": f"sep-{k}", "delta_mib": (s.data_ptr() - r.data_ptr()) / 2**20,
+               "shipped": timeit(s.data_ptr(), r.data_ptr())["ms"],
+               "plain_capped": timeit(s.data_ptr(), r.data_ptr(), variant=v_plain)["ms"],
+               "xcd_capped": timeit(s.data_ptr(), r.data_ptr(), variant=v_xcd)["ms"]}
+        rows.append(row)
+        print(row, flush=True)
+        if k % 2:
+            keep.append((s, r))
+        else:
+            del s, r
         torch.cuda.empty_cache()
+    del keep
+    torch.cuda.empty_cache()
     big = torch.empty(2 * N + (4 << 20) // 4, device="cuda").uniform_(-1, 1)
     for d in (0, 4096, 65536, 2 << 20):
         rp = big.data_ptr()
