@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 
 #include "combine.hpp"
@@ -218,10 +219,19 @@ namespace {
 // One-wave blocks, one 16-B vector per lane and operand, every access non-temporal: the
 // fastest shape measured on MI355X at 1 GiB (tools/tune_reduce.py, profiles/r1_tune.json).
 using DefaultCfg = VecCfg<64, 1, kNtSend | kNtRecv | kNtStore, false>;
-// Occupancy cap: 7 KiB of (unused) dynamic LDS per one-wave block admits 22 blocks per CU
-// (160 KiB / 7 KiB) instead of 32.  Fewer concurrent streams per CU measured +1.0-1.4 % at 1 GiB
-// over the uncapped launch in two interleaved sweeps (profiles/r1_tune_occupancy*.json).
-constexpr size_t kOccupancyLds = size_t(7) << 10;
+// Optional occupancy cap: DCCL_REDUCE_LDS_CAP bytes of (unused) dynamic LDS per one-wave block
+// (e.g. 7168 admits 22 blocks per CU instead of 32).  Off by default: with operands in a friendly
+// physical placement the uncapped launch is 0.8 % faster (profiles/r1_occupancy_pooled_*.json);
+// with separately allocated operands in the slow placement mode a 22-wave cap gained 1.0-1.4 %
+// (profiles/r1_tune_occupancy*.json).  Read once per process.
+size_t occupancy_lds() {
+    static const size_t v = [] {
+        const char* e = std::getenv("DCCL_REDUCE_LDS_CAP");
+        const unsigned long long x = e ? std::strtoull(e, nullptr, 10) : 0ull;
+        return static_cast<size_t>(x > (64ull << 10) ? (64ull << 10) : x);
+    }();
+    return v;
+}
 constexpr size_t kMaxGrid = size_t(1) << 24;  // grid-stride beyond this (2^24 x 64 threads)
 
 inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream, int block = kBlock,
@@ -276,7 +286,7 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
     const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
     if ((as | ar) % sizeof(T)) return launch_scalar<T, OP>(s, r, count, false, stream);
     if ((as ^ ar) & 15) return launch_scalar<T, OP>(s, r, count, true, stream);
-    return launch_vec<T, OP, DefaultCfg>(s, r, split_for_vectors<T>(ar, count), stream, 0, kOccupancyLds);
+    return launch_vec<T, OP, DefaultCfg>(s, r, split_for_vectors<T>(ar, count), stream, 0, occupancy_lds());
 }
 
 template <typename T, int OP, int K>
