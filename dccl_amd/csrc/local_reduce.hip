@@ -6,12 +6,13 @@
 // do_device_reduce (/root/reference/src/core/reduce.cu:9-100).  That kernel moves one
 // scalar element per thread per iteration through a runtime op switch on a grid of
 // num_SMs x 256 threads; this one is an HBM stream:
-//   * 16-byte (global_load_dwordx4 / global_store_dwordx4) accesses of both operands,
-//     UNROLL vectors per thread in flight before the first use, 256-thread blocks,
-//     one 16 KiB (x UNROLL/4) tile of each operand per block, >> 256 blocks per launch;
+//   * 16-byte (global_load_dwordx4 / global_store_dwordx4) accesses of both operands;
+//   * the shipped shape (DefaultCfg, chosen by tools/tune_reduce.py on MI355X): one-wave
+//     (64-thread) blocks, one 16-B vector per lane and operand, i.e. one 1 KiB tile of each
+//     operand per block and ~1M blocks for 1 GiB; every load and the store non-temporal;
 //   * dtype and op are template parameters (no per-element switch);
-//   * the single-use `send` stream is read with non-temporal loads;
-//   * unaligned head / tail elements are folded into block 0 of the same launch.
+//   * unaligned head / tail elements are folded into block 0 of the same launch;
+//   * operands with different 16-B phases / element misalignment take scalar kernels.
 // No LDS and no MFMA: each element is touched once (BASELINE.json north_star).
 //
 // Roofline: HBM, 3 * count * sizeof(T) algorithmic bytes (read send, read recv, write recv).
@@ -28,7 +29,7 @@
 
 namespace dccl_amd {
 
-constexpr int kBlock = 256;
+constexpr int kBlock = 256;  // block size of the scalar fallback kernels
 
 // Cache policy bits of the vector kernel.
 enum : int {
