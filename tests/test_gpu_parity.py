@@ -268,7 +268,7 @@ def _torch_expected(r, s, op):
 
 @pytest.mark.slow
 @pytest.mark.parametrize("dt,tdt", [(7, "float32"), (6, "float16"), (9, "bfloat16"), (2, "int32"),
-                                    (4, "int64")])
+                                    (4, "int64"), (0, "int8"), (1, "uint8"), (8, "float64")])
 def test_one_gib_against_torch(dccl, dt, tdt):
     """BASELINE config C3 sizes (1 GiB per operand): every op, bit-exact vs torch's device ops."""
     tdtype = getattr(torch, tdt)
@@ -289,8 +289,8 @@ def test_one_gib_against_torch(dccl, dt, tdt):
         if tdtype.is_floating_point:
             nan_r, nan_w = torch.isnan(r), torch.isnan(want)
             assert torch.equal(nan_r, nan_w)
-            assert torch.equal(r.view(torch.int16 if esz == 2 else torch.int32)[~nan_r],
-                               want.view(torch.int16 if esz == 2 else torch.int32)[~nan_w]), op
+            bits = {2: torch.int16, 4: torch.int32, 8: torch.int64}[esz]
+            assert torch.equal(r.view(bits)[~nan_r], want.view(bits)[~nan_w]), op
         else:
             assert torch.equal(r, want), op
         del r, want
