@@ -1,0 +1,241 @@
+// dccl_amd/csrc/reduce_kernels.hpp — device code of the combine and its launch helpers, shared by
+// the production entry points (local_reduce.hip) and the tuning variants (tune_kernels.hip).
+// See local_reduce.hip for the design; SURVEY.md §7 / DESIGN.md §3 for the rooflines.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "combine.hpp"
+#include "dccl/dccl_reduce.h"
+
+namespace dccl_amd {
+
+constexpr int kBlock = 256;  // block size of the scalar fallback kernels
+
+// Cache policy bits of the vector kernel.
+enum : int {
+    kNtSend = 1,   // non-temporal load of send (read once)
+    kNtRecv = 2,   // non-temporal load of recv
+    kNtStore = 4,  // non-temporal store of recv
+};
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+// Scalar element access that is correct for any alignment of the operand bases.
+template <typename T, bool ALIGNED>
+__device__ __forceinline__ T ld_elem(const unsigned char* base, size_t i) {
+    if constexpr (ALIGNED) return reinterpret_cast<const T*>(base)[i];
+    T v;
+    __builtin_memcpy(&v, base + i * sizeof(T), sizeof(T));
+    return v;
+}
+template <typename T, bool ALIGNED>
+__device__ __forceinline__ void st_elem(unsigned char* base, size_t i, T v) {
+    if constexpr (ALIGNED) { reinterpret_cast<T*>(base)[i] = v; return; }
+    __builtin_memcpy(base + i * sizeof(T), &v, sizeof(T));
+}
+
+// ---------------------------------------------------------------------------------
+// Vector kernel.  Operands are split as [head scalars | nvec 16-B vectors | tail
+// scalars]; head aligns recv (and, by construction, send) to 16 B.
+// ---------------------------------------------------------------------------------
+// Kernel shape: BLOCK threads, UNROLL 16-B vectors per thread per operand, cache POLICY
+// bits, XCD: remap block ids so that each XCD's blocks walk one contiguous range.
+// TAG keeps instantiations of different translation units distinct (production: 0, tuning: 1),
+// so no kernel symbol is registered from two code objects.
+template <int BLOCK_, int UNROLL_, int POLICY_, bool XCD_, int TAG = 0>
+struct VecCfg {
+    static constexpr int BLOCK = BLOCK_, UNROLL = UNROLL_, POLICY = POLICY_;
+    static constexpr bool XCD = XCD_;
+    static constexpr size_t TILE = size_t(BLOCK_) * UNROLL_;
+};
+
+template <typename T, int OP, typename C>
+__device__ __forceinline__ void full_tile(const u32x4* __restrict__ vs, u32x4* __restrict__ vr, size_t base) {
+    u32x4 s[C::UNROLL], r[C::UNROLL];
+#pragma unroll
+    for (int u = 0; u < C::UNROLL; ++u) s[u] = ld16<(C::POLICY & kNtSend) != 0>(vs + base + u * C::BLOCK);
+#pragma unroll
+    for (int u = 0; u < C::UNROLL; ++u) r[u] = ld16<(C::POLICY & kNtRecv) != 0>(vr + base + u * C::BLOCK);
+#pragma unroll
+    for (int u = 0; u < C::UNROLL; ++u) {
+        const u32x4 o = combine16<T, OP>(r[u], s[u]);
+        if constexpr ((C::POLICY & kNtStore) != 0) __builtin_nontemporal_store(o, vr + base + u * C::BLOCK);
+        else vr[base + u * C::BLOCK] = o;
+    }
+}
+
+template <typename T, int OP, typename C>
+__device__ __noinline__ void partial_tile(const u32x4* __restrict__ vs, u32x4* __restrict__ vr, size_t base,
+                                          size_t nvec) {
+#pragma unroll
+    for (int u = 0; u < C::UNROLL; ++u) {
+        const size_t i = base + u * C::BLOCK;
+        if (i < nvec) vr[i] = combine16<T, OP>(vr[i], vs[i]);
+    }
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md, "XCD swizzle must be bijective"):
+// blocks b and b+8 share an XCD, so give each group {b : b % 8 == x} one contiguous range.
+__device__ __forceinline__ size_t xcd_remap(size_t b, size_t nb) {
+    const size_t q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+template <typename T, int OP, typename C>
+__global__ __launch_bounds__(C::BLOCK) void reduce_vec_kernel(const unsigned char* __restrict__ send,
+                                                              unsigned char* __restrict__ recv,
+                                                              size_t head, size_t nvec, size_t tail) {
+    const u32x4* __restrict__ vs = reinterpret_cast<const u32x4*>(send + head * sizeof(T));
+    u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
+    const size_t nfull = nvec / C::TILE;
+    const size_t bid = C::XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+
+    // Full tiles: no bounds checks, all 2*UNROLL loads in flight before the first use.
+    for (size_t t = bid; t < nfull; t += gridDim.x)
+        full_tile<T, OP, C>(vs, vr, t * C::TILE + threadIdx.x);
+
+    // The partial last tile goes to the block after the last full one (mod grid).
+    if (nfull * C::TILE < nvec && bid == nfull % gridDim.x)
+        partial_tile<T, OP, C>(vs, vr, nfull * C::TILE + threadIdx.x, nvec);
+
+    // Scalar head [0, head) and tail [head + nvec*V, count): < 16 elements each.
+    if (blockIdx.x == 0 && threadIdx.x < head + tail) {
+        const size_t i = threadIdx.x < head ? threadIdx.x
+                                            : head + nvec * Pack<T>::N + (threadIdx.x - head);
+        const T a = ld_elem<T, true>(recv, i), b = ld_elem<T, true>(send, i);
+        st_elem<T, true>(recv, i, Combine<T, OP>::apply(a, b));
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Scalar fallback for operands whose 16-B phases differ (ALIGNED) or that are not
+// even element-aligned (!ALIGNED).  Grid-stride, 4 independent elements per thread.
+// ---------------------------------------------------------------------------------
+template <typename T, int OP, bool ALIGNED>
+__global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(const unsigned char* __restrict__ send,
+                                                               unsigned char* __restrict__ recv,
+                                                               size_t count) {
+    const size_t stride = size_t(gridDim.x) * kBlock;
+    for (size_t i0 = size_t(blockIdx.x) * kBlock * 4 + threadIdx.x; i0 < count; i0 += stride * 4) {
+        T a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t i = i0 + u * kBlock;
+            if (i < count) { a[u] = ld_elem<T, ALIGNED>(recv, i); b[u] = ld_elem<T, ALIGNED>(send, i); }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t i = i0 + u * kBlock;
+            if (i < count) st_elem<T, ALIGNED>(recv, i, Combine<T, OP>::apply(a[u], b[u]));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// k-way vector kernel: recv = op(...op(op(recv, s0), s1)..., s{K-1}), one pass.
+// ---------------------------------------------------------------------------------
+struct SendList { const unsigned char* p[8]; };
+
+template <typename T, int OP, int K, typename C>
+__global__ __launch_bounds__(C::BLOCK) void reduce_multi_vec_kernel(SendList sends, unsigned char* __restrict__ recv,
+                                                                    size_t head, size_t nvec, size_t tail) {
+    u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
+    const size_t ntiles = (nvec + C::TILE - 1) / C::TILE;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t base = t * C::TILE + threadIdx.x;
+        u32x4 r[C::UNROLL], s[K][C::UNROLL];
+#pragma unroll
+        for (int u = 0; u < C::UNROLL; ++u) {
+            const size_t i = base + u * C::BLOCK;
+            if (i < nvec) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    s[k][u] = ld16<(C::POLICY & kNtSend) != 0>(
+                        reinterpret_cast<const u32x4*>(sends.p[k] + head * sizeof(T)) + i);
+                r[u] = ld16<(C::POLICY & kNtRecv) != 0>(vr + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < C::UNROLL; ++u) {
+            const size_t i = base + u * C::BLOCK;
+            if (i < nvec) {
+                u32x4 acc = r[u];
+#pragma unroll
+                for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, s[k][u]);
+                if constexpr ((C::POLICY & kNtStore) != 0) __builtin_nontemporal_store(acc, vr + i);
+                else vr[i] = acc;
+            }
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < head + tail) {
+        const size_t i = threadIdx.x < head ? threadIdx.x
+                                            : head + nvec * Pack<T>::N + (threadIdx.x - head);
+        T acc = ld_elem<T, true>(recv, i);
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, true>(sends.p[k], i));
+        st_elem<T, true>(recv, i, acc);
+    }
+}
+
+template <typename T, int OP, bool ALIGNED>
+__global__ __launch_bounds__(kBlock) void reduce_multi_scalar_kernel(SendList sends, int nsend,
+                                                                     unsigned char* __restrict__ recv,
+                                                                     size_t count) {
+    const size_t stride = size_t(gridDim.x) * kBlock;
+    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < count; i += stride) {
+        T acc = ld_elem<T, ALIGNED>(recv, i);
+        for (int k = 0; k < nsend; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, ALIGNED>(sends.p[k], i));
+        st_elem<T, ALIGNED>(recv, i, acc);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Host-side launch helpers
+// ---------------------------------------------------------------------------------
+constexpr size_t kMaxGrid = size_t(1) << 24;  // grid-stride beyond this (2^24 x 64 threads)
+
+inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream, int block = kBlock,
+                  size_t lds_bytes = 0) {
+    if (grid == 0) return DCCL_SUCCESS;
+    if (grid > kMaxGrid) grid = kMaxGrid;
+    const hipError_t e =
+        hipLaunchKernel(fn, dim3(static_cast<unsigned>(grid)), dim3(block), args, lds_bytes, stream);
+    return e == hipSuccess ? DCCL_SUCCESS : DCCL_UNHANDLED_DEVICE_ERROR;
+}
+
+inline size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }
+
+struct Split {
+    size_t head, nvec, tail;
+};
+
+template <typename T>
+inline Split split_for_vectors(uintptr_t recv, size_t count) {
+    constexpr size_t V = Pack<T>::N;
+    size_t head = ((16 - (recv & 15)) & 15) / sizeof(T);
+    if (head > count) head = count;
+    const size_t rest = count - head;
+    const size_t nvec = rest / V;
+    return Split{head, nvec, rest - nvec * V};
+}
+
+template <typename T, int OP, typename C>
+int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t stream, size_t grid_cap,
+               size_t lds_bytes = 0) {
+    size_t grid = ceil_div(sp.nvec, C::TILE);
+    if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    if (grid_cap && grid > grid_cap) grid = grid_cap;
+    void* args[] = {&s, &r, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&reduce_vec_kernel<T, OP, C>), grid, args, stream, C::BLOCK,
+                  lds_bytes);
+}
+
+}  // namespace dccl_amd

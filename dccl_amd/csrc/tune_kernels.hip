@@ -1,0 +1,153 @@
+// dccl_amd/csrc/tune_kernels.hip — tuning-only variants of the fp32 Sum combine (not part of the
+// drop-in boundary; include/dccl/dccl_reduce_tuning.h).  Kept in their own translation unit so their
+// instantiations cannot perturb the production kernel's code generation.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dccl/dccl_reduce.h"
+#include "dccl/dccl_reduce_tuning.h"
+#include "reduce_kernels.hpp"
+
+using namespace dccl_amd;
+
+// ---------------------------------------------------------------------------------
+// Tuning entry: fp32 Sum with an explicit kernel variant (include/dccl/dccl_reduce_tuning.h).
+// ---------------------------------------------------------------------------------
+namespace {
+using TuneFn = int (*)(const unsigned char*, unsigned char*, Split, hipStream_t, size_t, size_t);
+template <int B, int U, int P, bool X>
+int tune_one(const unsigned char* s, unsigned char* r, Split sp, hipStream_t st, size_t cap, size_t lds) {
+    return launch_vec<float, kSum, VecCfg<B, U, P, X, 1>>(s, r, sp, st, cap, lds);
+}
+struct TuneEntry { int block, unroll, policy, xcd; TuneFn fn; };
+#define DCCL_TV(B, U, P, X) TuneEntry{B, U, P, X, &tune_one<B, U, P, X>}
+const TuneEntry kTune[] = {
+    DCCL_TV(64, 1, 7, 0),  DCCL_TV(64, 1, 5, 0),  DCCL_TV(64, 1, 6, 0),  DCCL_TV(64, 1, 3, 0),
+    DCCL_TV(64, 1, 1, 0),  DCCL_TV(64, 1, 7, 1),  DCCL_TV(64, 2, 7, 0),  DCCL_TV(64, 4, 7, 0),
+    DCCL_TV(128, 1, 7, 0), DCCL_TV(128, 1, 5, 0), DCCL_TV(128, 1, 6, 0), DCCL_TV(128, 1, 7, 1),
+    DCCL_TV(256, 1, 7, 0), DCCL_TV(256, 1, 7, 1), DCCL_TV(256, 4, 7, 0), DCCL_TV(1024, 1, 7, 0),
+    DCCL_TV(256, 4, 1, 0),
+};
+#undef DCCL_TV
+}  // namespace
+
+extern "C" int dccl_tune_num_variants(void) { return int(sizeof(kTune) / sizeof(kTune[0])); }
+
+extern "C" int dccl_tune_variant_info(int v, int* block, int* unroll, int* policy, int* xcd) {
+    if (v < 0 || v >= dccl_tune_num_variants()) return DCCL_INVALID_ARGUMENT;
+    *block = kTune[v].block; *unroll = kTune[v].unroll; *policy = kTune[v].policy; *xcd = kTune[v].xcd;
+    return DCCL_SUCCESS;
+}
+
+extern "C" int dccl_tune_reduce_f32_sum_lds(const void* send, void* recv, size_t count, int variant,
+                                            size_t grid_cap, size_t lds_bytes, void* stream) {
+    if (variant < 0 || variant >= dccl_tune_num_variants()) return DCCL_INVALID_ARGUMENT;
+    if (count == 0) return DCCL_SUCCESS;
+    const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
+    if (((as | ar) & 3) || ((as ^ ar) & 15)) return DCCL_INVALID_ARGUMENT;
+    return kTune[variant].fn(static_cast<const unsigned char*>(send), static_cast<unsigned char*>(recv),
+                             split_for_vectors<float>(ar, count), static_cast<hipStream_t>(stream), grid_cap,
+                             lds_bytes);
+}
+
+extern "C" int dccl_tune_reduce_f32_sum(const void* send, void* recv, size_t count, int variant, size_t grid_cap,
+                                        void* stream) {
+    return dccl_tune_reduce_f32_sum_lds(send, recv, count, variant, grid_cap, 0, stream);
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning only: one-wave blocks, one 16-B vector per lane and operand, cache-policy bits
+// chosen in inline asm (the builtins only expose `nt`).  Requires count % 256 == 0 and
+// 16-B aligned operands; fp32 Sum.
+// ---------------------------------------------------------------------------------
+namespace {
+#define DCCL_ASM_LS(BITS_S, BITS_R)                                                              \
+    asm volatile("global_load_dwordx4 %0, %2, off " BITS_S "\n\t"                                \
+                 "global_load_dwordx4 %1, %3, off " BITS_R "\n\t"                                \
+                 "s_waitcnt vmcnt(0)"                                                            \
+                 : "=&v"(a), "=&v"(b)                                                            \
+                 : "v"(ps), "v"(pr)                                                              \
+                 : "memory")
+#define DCCL_ASM_ST(BITS) asm volatile("global_store_dwordx4 %0, %1, off " BITS :: "v"(pr), "v"(o) : "memory")
+
+template <int FLAVOR>
+__global__ __launch_bounds__(64) void tune_asm_kernel(const u32x4* __restrict__ s, u32x4* __restrict__ r,
+                                                      size_t nvec) {
+    const size_t i = size_t(blockIdx.x) * 64 + threadIdx.x;
+    if (i >= nvec) return;
+    const u32x4* ps = s + i;
+    u32x4* pr = r + i;
+    u32x4 a, b;
+    if constexpr (FLAVOR == 0) DCCL_ASM_LS("nt", "nt");
+    if constexpr (FLAVOR == 1) DCCL_ASM_LS("sc1 nt", "sc1 nt");
+    if constexpr (FLAVOR == 2) DCCL_ASM_LS("sc0 sc1 nt", "sc0 sc1 nt");
+    if constexpr (FLAVOR == 3) DCCL_ASM_LS("nt", "nt");
+    if constexpr (FLAVOR == 4) DCCL_ASM_LS("sc1", "sc1");
+    if constexpr (FLAVOR == 5) DCCL_ASM_LS("nt", "nt");
+    if constexpr (FLAVOR == 6) DCCL_ASM_LS("sc0 sc1", "nt");
+    const u32x4 o = combine16<float, kSum>(b, a);
+    if constexpr (FLAVOR == 0) DCCL_ASM_ST("nt");
+    if constexpr (FLAVOR == 1) DCCL_ASM_ST("sc1 nt");
+    if constexpr (FLAVOR == 2) DCCL_ASM_ST("sc0 sc1 nt");
+    if constexpr (FLAVOR == 3) DCCL_ASM_ST("sc0 sc1 nt");
+    if constexpr (FLAVOR == 4) DCCL_ASM_ST("nt");
+    if constexpr (FLAVOR == 5) DCCL_ASM_ST("sc1");
+    if constexpr (FLAVOR == 6) DCCL_ASM_ST("nt");
+}
+#undef DCCL_ASM_LS
+#undef DCCL_ASM_ST
+}  // namespace
+
+extern "C" int dccl_tune_asm_f32_sum(const void* send, void* recv, size_t count, int flavor, void* stream) {
+    if (count % 256 || ((reinterpret_cast<uintptr_t>(send) | reinterpret_cast<uintptr_t>(recv)) & 15))
+        return DCCL_INVALID_ARGUMENT;
+    const size_t nvec = count / 4;
+    const void* fns[] = {reinterpret_cast<const void*>(&tune_asm_kernel<0>), reinterpret_cast<const void*>(&tune_asm_kernel<1>),
+                         reinterpret_cast<const void*>(&tune_asm_kernel<2>), reinterpret_cast<const void*>(&tune_asm_kernel<3>),
+                         reinterpret_cast<const void*>(&tune_asm_kernel<4>), reinterpret_cast<const void*>(&tune_asm_kernel<5>),
+                         reinterpret_cast<const void*>(&tune_asm_kernel<6>)};
+    if (flavor < 0 || flavor >= int(sizeof(fns) / sizeof(fns[0]))) return DCCL_INVALID_ARGUMENT;
+    void* args[] = {&send, &recv, const_cast<size_t*>(&nvec)};
+    return launch(fns[flavor], nvec / 64, args, static_cast<hipStream_t>(stream), 64);
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning only: decorrelate the send/recv addresses each wave issues together.  A block of
+// WAVES one-wave tiles loads recv tile w and send tile (w + SKEW) % WAVES, so the two loads a
+// wave has in flight are SKEW KiB apart; send vectors are exchanged through LDS behind one
+// barrier.  SKEW = 0 is the control (same pairing as the shipped kernel, plus the LDS hop).
+// fp32 Sum; count must be a multiple of WAVES * 256 elements.
+// ---------------------------------------------------------------------------------
+namespace {
+template <int WAVES, int SKEW>
+__global__ __launch_bounds__(WAVES * 64) void tune_skew_kernel(const u32x4* __restrict__ s, u32x4* __restrict__ r) {
+    __shared__ u32x4 lds[WAVES * 64];
+    const size_t base = size_t(blockIdx.x) * WAVES * 64;
+    const int w = threadIdx.x / 64, l = threadIdx.x % 64;
+    const int ws = (w + SKEW) % WAVES;
+    const u32x4 sv = __builtin_nontemporal_load(s + base + ws * 64 + l);
+    const u32x4 rv = __builtin_nontemporal_load(r + base + w * 64 + l);
+    lds[ws * 64 + l] = sv;
+    __syncthreads();
+    __builtin_nontemporal_store(combine16<float, kSum>(rv, lds[w * 64 + l]), r + base + w * 64 + l);
+}
+}  // namespace
+
+extern "C" int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count, int waves, int skew,
+                                      void* stream) {
+    if (((reinterpret_cast<uintptr_t>(send) | reinterpret_cast<uintptr_t>(recv)) & 15)) return DCCL_INVALID_ARGUMENT;
+    const void* fn = nullptr;
+    if (waves == 8 && skew == 0) fn = reinterpret_cast<const void*>(&tune_skew_kernel<8, 0>);
+    if (waves == 8 && skew == 1) fn = reinterpret_cast<const void*>(&tune_skew_kernel<8, 1>);
+    if (waves == 8 && skew == 2) fn = reinterpret_cast<const void*>(&tune_skew_kernel<8, 2>);
+    if (waves == 8 && skew == 4) fn = reinterpret_cast<const void*>(&tune_skew_kernel<8, 4>);
+    if (waves == 4 && skew == 0) fn = reinterpret_cast<const void*>(&tune_skew_kernel<4, 0>);
+    if (waves == 4 && skew == 2) fn = reinterpret_cast<const void*>(&tune_skew_kernel<4, 2>);
+    if (waves == 16 && skew == 8) fn = reinterpret_cast<const void*>(&tune_skew_kernel<16, 8>);
+    if (waves == 16 && skew == 4) fn = reinterpret_cast<const void*>(&tune_skew_kernel<16, 4>);
+    if (fn == nullptr || count % (size_t(waves) * 256)) return DCCL_INVALID_ARGUMENT;
+    void* args[] = {&send, &recv};
+    return launch(fn, count / (size_t(waves) * 256), args, static_cast<hipStream_t>(stream), waves * 64);
+}
+
