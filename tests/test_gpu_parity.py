@@ -322,3 +322,24 @@ def test_misaligned_reference_wrong_build_correct(dccl):
         torch.cuda.synchronize()
         got = host_of(tr, off, r)
         assert got.tobytes() == correct.tobytes(), i
+
+
+def test_graph_capture_replay(dccl):
+    """dccl_local_reduce only enqueues a kernel on the given stream, so it can be captured in a HIP
+    graph (torch.cuda.graph) and replayed; each replay applies the combine once more."""
+    n = (1 << 20) + 3
+    s = torch.full((n,), 1.0, device="cuda")
+    r = torch.zeros(n, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=st):
+            for _ in range(4):
+                assert dccl.local_reduce(s.data_ptr(), r.data_ptr(), 7, n, 0, st.cuda_stream) == 0
+    torch.cuda.synchronize()
+    r.zero_()
+    for _ in range(5):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.all(r == 20.0)

@@ -118,6 +118,37 @@ def c4(results):
     results["c4"] = rows
 
 
+def c4_graph(results):
+    """The small end of the sweep with launch overhead removed: 50 back-to-back combines captured in
+    one HIP graph and replayed (torch.cuda.graph), so the per-combine time is the kernel's own."""
+    rows = []
+    for lg in range(12, 25):
+        nbytes = 1 << lg
+        n = nbytes // 4
+        s, r = fill(nbytes, 7, 0, 1), fill(nbytes, 7, 0, 2)
+        st = torch.cuda.Stream()
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=st):
+            for _ in range(50):
+                dccl_amd.local_reduce(s.data_ptr(), r.data_ptr(), 7, n, 0, st.cuda_stream)
+        g.replay()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) / 50)
+        med = statistics.median(ts)
+        rows.append({"bytes_per_operand": nbytes, "us_per_combine": round(med * 1e3, 3),
+                     "gb_s": round(3 * nbytes / (med * 1e-3) / 1e9, 1), "regime": "mall (L2/MALL-resident)"})
+        print("c4_graph", rows[-1], flush=True)
+    results["c4_graph"] = rows
+
+
 def c2(results):
     st = torch.cuda.current_stream().cuda_stream
     nbytes = 256 << 20
@@ -226,7 +257,8 @@ def main():
     a = p.parse_args()
     results = {"device": torch.cuda.get_device_name(0), "peak_gb_s": PEAK}
     for part in a.parts.split(","):
-        {"c3": c3, "c4": c4, "c2": c2, "kway": kway, "host": host, "c1": c1, "misaligned": misaligned}[part](results)
+        {"c3": c3, "c4": c4, "c2": c2, "kway": kway, "host": host, "c1": c1, "misaligned": misaligned,
+         "c4_graph": c4_graph}[part](results)
         if a.out:
             with open(a.out, "w") as f:
                 json.dump(results, f, indent=1)
