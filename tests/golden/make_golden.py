@@ -8,7 +8,7 @@ Outputs (data only: inputs and expected outputs):
 
 * ``host_reduce_ref.npz`` — for every host dtype the reference supports
   (int8, uint8, int32, uint32, int64, uint64, float32, float64) x sizes
-  {1, 15, 16, 17, 255, 256, 1000}: seeded ``send`` / ``recv`` inputs (special values
+  {1, 15, 16, 17, 255, 256, 1000, 4099}: seeded ``send`` / ``recv`` inputs (special values
   spliced in) and, per op {Sum, Prod, Max, Min}, the output of the REFERENCE's own
   ``do_host_reduce<DT>`` (/root/reference/src/core/internal_common.hpp:496-586,
   compiled by oracle/build_ref.sh), run on 64-B aligned buffers.
@@ -37,7 +37,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 import oracle  # noqa: E402  (test infrastructure)
 
-SIZES = [1, 15, 16, 17, 255, 256, 1000]
+SIZES = [1, 15, 16, 17, 255, 256, 1000, 4099]
 HOST_DTYPES = [0, 1, 2, 3, 4, 5, 7, 8]
 OPS = [0, 1, 2, 3]
 SEED = 0xDCC1

@@ -55,7 +55,7 @@ def test_restatement_matches_golden_fixtures():
         assert oracle.host_reduce(np.ascontiguousarray(send), recv, dt, op) == 0
         assert recv.tobytes() == z[key].tobytes(), key
         checked += 1
-    assert checked == 8 * 7 * 4
+    assert checked == 8 * 8 * 4  # dtypes x sizes {1,...,1000,4099} x ops
 
 
 def test_restatement_matches_half_fixtures():
