@@ -65,39 +65,33 @@ def parse():
     return p.parse_args()
 
 
-def synth(n: int, dt: int, op: int, seed: int, device) -> torch.Tensor:
-    """Synthetic operand: uniform [-1,1) for Sum/Max/Min, [0.5,2) for Prod; ints full range."""
-    g = torch.Generator(device=device).manual_seed(seed)
-    tdt = dccl_amd.TORCH_DTYPES[dt]
-    if dt in (6, 7, 8, 9):
-        x = torch.rand(n, device=device, generator=g, dtype=torch.float32 if dt != 8 else torch.float64)
-        x = x.mul_(1.5).add_(0.5) if op == 1 else x.mul_(2).sub_(1)
-        return x.to(tdt)
-    raw = torch.randint(-2**31, 2**31 - 1, ((n * dccl_amd.size_of_type(dt) + 3) // 4,), device=device,
-                        generator=g, dtype=torch.int32)
-    return raw.view(torch.uint8)[: n * dccl_amd.size_of_type(dt)].view(torch.int8) if dt in (0, 1) else \
-        raw.view(torch.int64 if dt in (4, 5) else torch.int32)[:n]
+def synth_into(t: torch.Tensor, n: int, dt: int, op: int, buffer_id: int) -> None:
+    """Counter-based synthetic operand written on the device (include/dccl/dccl_synth.h):
+    uniform [-1,1) for Sum/Max/Min, [0.5,2) for Prod, integers full range; seed 0xDCC1."""
+    dccl_amd.check(dccl_amd.synth_fill(t.data_ptr(), dt, n, op, SEED, buffer_id,
+                                       torch.cuda.current_stream().cuda_stream), "synth_fill")
 
 
+SEED = 0xDCC1
 PAIR_GAP = 4096  # bytes between the end of recv and the start of send in the pooled layout
 
 
-def operand_pair(n: int, dt: int, op: int, seed: int, device, layout: str):
+def operand_pair(n: int, dt: int, op: int, buffer_id: int, device, layout: str):
     """(send, recv) synthetic operands.  "pooled": both carved from ONE HBM allocation, recv first
     and send PAIR_GAP bytes past its end; "separate": two allocations (DCCL's own shape: scratchpad
     + user chunk).  Separately allocated 1 GiB operands land in one of two physical placement modes
     (0.476 vs 0.508 ms on MI355X); the pooled layout is consistently in the fast one."""
-    s = synth(n, dt, op, seed, device)
-    r = synth(n, dt, op, seed + 1, device)
-    if layout == "separate":
-        return s, r
     nbytes = n * dccl_amd.size_of_type(dt)
-    pool = torch.empty(2 * nbytes + PAIR_GAP, dtype=torch.uint8, device=device)
-    recv = pool[:nbytes].view(r.dtype)
-    send = pool[nbytes + PAIR_GAP:].view(s.dtype)
-    recv.copy_(r)
-    send.copy_(s)
-    del s, r
+    tdt = dccl_amd.TORCH_DTYPES[dt]
+    if layout == "separate":
+        send = torch.empty(nbytes, dtype=torch.uint8, device=device).view(tdt)
+        recv = torch.empty(nbytes, dtype=torch.uint8, device=device).view(tdt)
+    else:
+        pool = torch.empty(2 * nbytes + PAIR_GAP, dtype=torch.uint8, device=device)
+        recv = pool[:nbytes].view(tdt)
+        send = pool[nbytes + PAIR_GAP:].view(tdt)
+    synth_into(send, n, dt, op, buffer_id)
+    synth_into(recv, n, dt, op, buffer_id + 1)
     return send, recv
 
 
@@ -300,7 +294,7 @@ def main():
         total_bytes = world * n * esz
     nbytes = n * esz
 
-    send, recv = operand_pair(n, dt, op, 0xDCC1 + 2 * rank, dev, a.layout)
+    send, recv = operand_pair(n, dt, op, 2 * rank, dev, a.layout)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     ps, pr = send.data_ptr(), recv.data_ptr()
@@ -343,7 +337,7 @@ def main():
     other = "separate" if a.layout == "pooled" else "pooled"
     del send, recv
     torch.cuda.empty_cache()
-    s2, r2 = operand_pair(n, dt, op, 0xDCC1 + 2 * rank, dev, other)
+    s2, r2 = operand_pair(n, dt, op, 2 * rank, dev, other)
     k2 = time_kernel(s2.data_ptr(), r2.data_ptr(), dt, n, op, stream, max(10, a.steps // 4))
     extra["other_layout"] = {"layout": other, "kernel_ms_avg": round(k2, 4),
                              "frac": round(3 * nbytes / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
@@ -395,7 +389,7 @@ def main():
             "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
             "dtype": {0: "i8", 1: "u8", 2: "i32", 3: "u32", 4: "i64", 5: "u64", 6: "f16", 7: "f32", 8: "f64",
                       9: "bf16"}[dt],
-            "data": f"synthetic (seeded uniform [-1,1) operands resident in HBM, {a.layout} layout)",
+            "data": f"synthetic (device splitmix64 counter generator, seed 0xDCC1, uniform [-1,1) operands resident in HBM, {a.layout} layout)",
             "config": {"workload": (f"C5: {a.total_gib:g} GiB per operand sharded over {world} GPU(s), "
                                     f"in-place combine recv=op(recv,send), {a.op}") if strong else
                                    (f"in-place two-buffer combine recv=op(recv,send), {a.op}, "

@@ -104,6 +104,8 @@ def _load():
         "dccl_all_gather": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_void_p]),
         "dccl_rccl_available": (c_int, []),
         "dccl_tune_skew_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),
+        "dccl_tune_multi_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_void_p]),
+        "dccl_synth_fill": (c_int, [c_void_p, c_int, c_size_t, c_int, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),
     })
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -122,6 +124,7 @@ EXPORTED_SYMBOLS = [
     "dccl_tune_variant_info", "dccl_tune_asm_f32_sum", "dccl_tune_reduce_f32_sum_lds",
     "dccl_comm_init_rank", "dccl_get_unique_id", "dccl_comm_init_rccl", "dccl_comm_finalize", "dccl_all_reduce",
     "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available", "dccl_tune_skew_f32_sum",
+    "dccl_synth_fill", "dccl_tune_multi_f32_sum",
 ]
 
 
@@ -160,6 +163,11 @@ def local_reduce_multi(send_ptrs, recv_ptr: int, dtype: int, count: int, op: int
 def local_reduce_host(send_ptr: int, recv_ptr: int, dtype: int, count: int, op: int) -> int:
     """Host-pointer combine (staged through the current GPU); synchronous."""
     return int(lib.dccl_local_reduce_host(send_ptr, recv_ptr, int(dtype), int(count), int(op)))
+
+
+def synth_fill(ptr: int, dtype: int, count: int, op: int, seed: int, buffer_id: int, stream: int = 0) -> int:
+    """Counter-based synthetic operand in device memory (include/dccl/dccl_synth.h)."""
+    return int(lib.dccl_synth_fill(ptr, int(dtype), int(count), int(op), int(seed), int(buffer_id), stream or None))
 
 
 def register_host_memory(ptr: int, size: int) -> int:

@@ -16,7 +16,7 @@ extern "C" {
 #endif
 int dccl_tune_num_variants(void);
 int dccl_tune_variant_info(int variant, int* block, int* unroll, int* policy, int* xcd);
-/* One-wave blocks, one vector per lane, cache bits in inline asm; flavor 0-6 (see local_reduce.hip). */
+/* One-wave blocks, one vector per lane, cache bits in inline asm; flavor 0-6 (see tune_kernels.hip). */
 int dccl_tune_asm_f32_sum(const void* send, void* recv, size_t count, int flavor, void* stream);
 int dccl_tune_reduce_f32_sum(const void* send, void* recv, size_t count, int variant, size_t grid_cap,
                              void* stream);
@@ -26,6 +26,9 @@ int dccl_tune_reduce_f32_sum_lds(const void* send, void* recv, size_t count, int
 /* Block of `waves` one-wave tiles; each wave pairs recv tile w with send tile (w+skew)%waves,
  * exchanging send through LDS (tests address-pair decorrelation). */
 int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count, int waves, int skew, void* stream);
+/* k-way fp32 Sum (the dccl_local_reduce_multi kernel) in shape `variant` 0-4 (see tune_kernels.hip). */
+int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
+                            void* stream);
 #ifdef __cplusplus
 }
 #endif

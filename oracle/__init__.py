@@ -59,6 +59,9 @@ def restatement():
         lib.oracle_float_to_bf16.argtypes = [ctypes.c_float]
         lib.oracle_bf16_to_float.restype = ctypes.c_float
         lib.oracle_bf16_to_float.argtypes = [ctypes.c_uint16]
+        lib.oracle_synth_fill.restype = ctypes.c_int
+        lib.oracle_synth_fill.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t]
         _cache["rs"] = lib
     return _cache["rs"]
 
@@ -92,6 +95,15 @@ def ref_reduce(send: np.ndarray, recv: np.ndarray, dtype: int, op: int, count: i
         raise RuntimeError("reference oracle not built (oracle/_ref missing)")
     n = recv.size if count is None else count
     return lib.ref_host_reduce(_ptr(send), _ptr(recv), n, dtype, op)
+
+
+def synth(n: int, dtype: int, op: int, seed: int, buffer_id: int, first: int = 0) -> np.ndarray:
+    """Elements [first, first+n) of the counter-based synthetic operand (include/dccl/dccl_synth.h)."""
+    out = aligned_empty(n, NP_DTYPES[dtype])
+    rc = restatement().oracle_synth_fill(_ptr(out), dtype, n, op, seed, buffer_id, first)
+    if rc != 0:
+        raise ValueError(f"oracle synth failed rc={rc}")
+    return out
 
 
 def combine(send: np.ndarray, recv: np.ndarray, dtype: int, op: int) -> np.ndarray:

@@ -222,3 +222,46 @@ float oracle_half_to_float(uint16_t h) { return half_to_float(h); }
 uint16_t oracle_float_to_half(float f) { return float_to_half(f); }
 float oracle_bf16_to_float(uint16_t b) { return bf16_to_float(b); }
 uint16_t oracle_float_to_bf16(float f) { return float_to_bf16(f); }
+
+/* ---------------- synthetic operands ----------------
+ * Host restatement of the generator documented in include/dccl/dccl_synth.h; the tests use it
+ * to regenerate full-size operands and check the device combine bit for bit.  Written from the
+ * published splitmix64 finaliser (Steele, Lea, Flood 2014), independently of the HIP kernel. */
+static uint64_t splitmix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+int oracle_synth_fill(void* dst, int dtype, size_t count, int op, uint64_t seed, uint64_t buffer_id,
+                      size_t first) {
+    const uint64_t key = seed ^ (buffer_id << 40);
+    const int prod = op == OP_PROD;
+    for (size_t j = 0; j < count; j++) {
+        const uint64_t x = splitmix64(key ^ (uint64_t)(first + j));
+        switch (dtype) {
+        case DT_I8: case DT_U8: ((uint8_t*)dst)[j] = (uint8_t)x; break;
+        case DT_I32: case DT_U32: ((uint32_t*)dst)[j] = (uint32_t)x; break;
+        case DT_I64: case DT_U64: ((uint64_t*)dst)[j] = x; break;
+        case DT_F32:
+            if (prod) ((uint32_t*)dst)[j] = (uint32_t)(((126u + (x >> 63)) << 23) | (x & 0x7fffffu));
+            else ((float*)dst)[j] = (float)((int32_t)(x >> 40) - (1 << 23)) / 8388608.0f;
+            break;
+        case DT_F64:
+            if (prod) ((uint64_t*)dst)[j] = ((1022ull + (x >> 63)) << 52) | (x & 0xfffffffffffffull);
+            else ((double*)dst)[j] = (double)((int64_t)(x >> 11) - (1ll << 52)) / 4503599627370496.0;
+            break;
+        case DT_F16:
+            if (prod) ((uint16_t*)dst)[j] = (uint16_t)(((14u + (x >> 63)) << 10) | (x & 0x3ffu));
+            else ((uint16_t*)dst)[j] = float_to_half((float)((int32_t)(x >> 53) - (1 << 10)) / 1024.0f);
+            break;
+        case DT_BF16:
+            if (prod) ((uint16_t*)dst)[j] = (uint16_t)(((126u + (x >> 63)) << 7) | (x & 0x7fu));
+            else ((uint16_t*)dst)[j] = float_to_bf16((float)((int32_t)(x >> 56) - (1 << 7)) / 128.0f);
+            break;
+        default: return R_INVALID_ARGUMENT;
+        }
+    }
+    return R_SUCCESS;
+}

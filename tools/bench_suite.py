@@ -33,16 +33,12 @@ NAMES = {0: "int8", 1: "uint8", 2: "int32", 3: "uint32", 4: "int64", 5: "uint64"
 OPS = {0: "sum", 1: "prod", 2: "max", 3: "min"}
 
 
-def fill(nbytes, dt, op, seed):
-    g = torch.Generator(device="cuda").manual_seed(seed)
+def fill(nbytes, dt, op, buffer_id):
+    """Device-generated synthetic operand (include/dccl/dccl_synth.h)."""
     t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    if dt in (6, 7, 8, 9):
-        f = {6: torch.float16, 7: torch.float32, 8: torch.float64, 9: torch.bfloat16}[dt]
-        x = torch.rand(nbytes // t.new_empty(0, dtype=f).element_size(), device="cuda", generator=g)
-        x = x.mul_(1.5).add_(0.5) if op == 1 else x.mul_(2).sub_(1)
-        t.view(f).copy_(x.to(f))
-    else:
-        t.view(torch.int32)[: nbytes // 4].random_(generator=g)
+    n = nbytes // dccl_amd.size_of_type(dt)
+    dccl_amd.check(dccl_amd.synth_fill(t.data_ptr(), dt, n, op, 0xDCC1, buffer_id,
+                                       torch.cuda.current_stream().cuda_stream), "synth_fill")
     return t
 
 
