@@ -104,7 +104,8 @@ def _load():
         "dccl_all_gather": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_void_p]),
         "dccl_rccl_available": (c_int, []),
         "dccl_tune_skew_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),
-        "dccl_tune_multi_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_void_p]),
+        "dccl_tune_multi_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_size_t,
+                                            c_void_p]),
         "dccl_synth_fill": (c_int, [c_void_p, c_int, c_size_t, c_int, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),
     })
     for name, (res, args) in sig.items():

@@ -64,13 +64,24 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
     return launch_vec<T, OP, DefaultCfg>(s, r, split_for_vectors<T>(ar, count), stream, 0, occupancy_lds());
 }
 
+// k-way combine: every resident wave keeps k+1 16-B loads per lane in flight, so the resident waves
+// per CU are capped (through unused dynamic LDS, 160 KiB per CU) to keep roughly 50-80 KiB of reads
+// outstanding per CU.  Measured optimum per k at 1 GiB per operand on MI355X, fp32 Sum
+// (tools/tune_multi.py, profiles/r1_tune_multi_waves.json): 4-7 % faster than 32 waves for k >= 2.
+constexpr int kMultiWaves[9] = {32, 32, 18, 13, 13, 11, 11, 10, 9};
+constexpr size_t kLdsPerCu = 160u << 10;
+constexpr size_t multi_lds(int k) {
+    return kMultiWaves[k] >= 32 ? 0 : (kLdsPerCu / kMultiWaves[k] + 255) / 256 * 256;
+}
+
 template <typename T, int OP, int K>
 int launch_multi_vec(SendList sl, unsigned char* r, Split sp, hipStream_t stream) {
     using C = DefaultCfg;
     size_t grid = ceil_div(sp.nvec, C::TILE);
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
-    return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, C>), grid, args, stream, C::BLOCK);
+    return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, C>), grid, args, stream, C::BLOCK,
+                  multi_lds(K));
 }
 
 template <typename T, int OP>

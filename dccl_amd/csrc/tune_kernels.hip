@@ -155,32 +155,34 @@ extern "C" int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count
 // ---------------------------------------------------------------------------------
 // Tuning only: k-way fp32 Sum (dccl_local_reduce_multi's kernel) with an explicit shape.
 // Variant v: 0 = shipped (64 threads, 1 vector, all nt), 1 = 64 threads x 2 vectors,
-// 2 = 256 threads x 1 vector, 3 = only send loads nt, 4 = 64 threads x 4 vectors.
+// 2 = 256 threads x 1 vector, 3 = only send loads nt, 4 = 64 threads x 4 vectors; `lds_bytes` of
+// unused dynamic LDS per block caps the resident blocks per CU (160 KiB / lds_bytes).
 // ---------------------------------------------------------------------------------
 namespace {
 template <int K, typename C>
-int tune_multi_launch(SendList sl, unsigned char* r, Split sp, hipStream_t stream) {
+int tune_multi_launch(SendList sl, unsigned char* r, Split sp, hipStream_t stream, size_t lds = 0) {
     size_t grid = ceil_div(sp.nvec, C::TILE);
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<float, kSum, K, C>), grid, args, stream,
-                  C::BLOCK);
+                  C::BLOCK, lds);
 }
 template <int K>
-int tune_multi_k(int variant, SendList sl, unsigned char* r, Split sp, hipStream_t st) {
+int tune_multi_k(int variant, SendList sl, unsigned char* r, Split sp, hipStream_t st, size_t lds) {
     switch (variant) {
-    case 0: return tune_multi_launch<K, VecCfg<64, 1, 7, false, 1>>(sl, r, sp, st);
-    case 1: return tune_multi_launch<K, VecCfg<64, 2, 7, false, 1>>(sl, r, sp, st);
-    case 2: return tune_multi_launch<K, VecCfg<256, 1, 7, false, 1>>(sl, r, sp, st);
-    case 3: return tune_multi_launch<K, VecCfg<64, 1, 1, false, 1>>(sl, r, sp, st);
-    case 4: return tune_multi_launch<K, VecCfg<64, 4, 7, false, 1>>(sl, r, sp, st);
+    case 0: return tune_multi_launch<K, VecCfg<64, 1, 7, false, 1>>(sl, r, sp, st, lds);
+    case 1: return tune_multi_launch<K, VecCfg<64, 2, 7, false, 1>>(sl, r, sp, st, lds);
+    case 2: return tune_multi_launch<K, VecCfg<256, 1, 7, false, 1>>(sl, r, sp, st, lds);
+    case 3: return tune_multi_launch<K, VecCfg<64, 1, 1, false, 1>>(sl, r, sp, st, lds);
+    case 4: return tune_multi_launch<K, VecCfg<64, 4, 7, false, 1>>(sl, r, sp, st, lds);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
 }  // namespace
 
 extern "C" int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
-                                       void* stream) {
+                                       size_t lds_bytes, void* stream) {
+    if (lds_bytes > (64u << 10)) return DCCL_INVALID_ARGUMENT;
     if (nsend < 1 || nsend > 8 || sends == nullptr || recv == nullptr) return DCCL_INVALID_ARGUMENT;
     SendList sl{};
     const uintptr_t ar = reinterpret_cast<uintptr_t>(recv);
@@ -195,13 +197,13 @@ extern "C" int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void
     auto r = static_cast<unsigned char*>(recv);
     const auto st = static_cast<hipStream_t>(stream);
     switch (nsend) {
-    case 1: return tune_multi_k<1>(variant, sl, r, sp, st);
-    case 2: return tune_multi_k<2>(variant, sl, r, sp, st);
-    case 3: return tune_multi_k<3>(variant, sl, r, sp, st);
-    case 4: return tune_multi_k<4>(variant, sl, r, sp, st);
-    case 5: return tune_multi_k<5>(variant, sl, r, sp, st);
-    case 6: return tune_multi_k<6>(variant, sl, r, sp, st);
-    case 7: return tune_multi_k<7>(variant, sl, r, sp, st);
-    default: return tune_multi_k<8>(variant, sl, r, sp, st);
+    case 1: return tune_multi_k<1>(variant, sl, r, sp, st, lds_bytes);
+    case 2: return tune_multi_k<2>(variant, sl, r, sp, st, lds_bytes);
+    case 3: return tune_multi_k<3>(variant, sl, r, sp, st, lds_bytes);
+    case 4: return tune_multi_k<4>(variant, sl, r, sp, st, lds_bytes);
+    case 5: return tune_multi_k<5>(variant, sl, r, sp, st, lds_bytes);
+    case 6: return tune_multi_k<6>(variant, sl, r, sp, st, lds_bytes);
+    case 7: return tune_multi_k<7>(variant, sl, r, sp, st, lds_bytes);
+    default: return tune_multi_k<8>(variant, sl, r, sp, st, lds_bytes);
     }
 }

@@ -1,11 +1,13 @@
 """A/B the k-way combine (dccl_local_reduce_multi) shapes on MI355X.
 
-For k = 1..8 sends of 256 MiB fp32 and two operand placements (separate allocations; one pool
+For k = 1..8 sends of --mib MiB fp32 and two operand placements (separate allocations; one pool
 with a 4 KiB x (j+1) stagger between operand j and j+1), times each variant of
 dccl_tune_multi_f32_sum (include/dccl/dccl_reduce_tuning.h) and the shipped entry point.
-Algorithmic bytes per launch: (k + 2) * 256 MiB.
+Algorithmic bytes per launch: (k + 2) * operand bytes.  Use 1 GiB operands (--mib 1024) for decisions:
+at 256 MiB a recv buffer written with the default cache policy partly survives in the 256 MiB
+Infinity Cache between back-to-back launches, which flatters variants 3 (profiles/r1_tune_multi_*.json).
 
-    python tools/tune_multi.py [--mib 256] [--out gpurun_out/tune_multi.json]
+    python tools/tune_multi.py [--mib 1024] [--out gpurun_out/tune_multi.json]
 """
 import argparse
 import ctypes
@@ -21,6 +23,12 @@ import dccl_amd  # noqa: E402
 
 PEAK = 8.0e12
 VARIANTS = {0: "64x1 nt-all (shipped)", 1: "64x2 nt-all", 2: "256x1 nt-all", 3: "64x1 nt-send", 4: "64x4 nt-all"}
+LDS_PER_CU = 160 << 10
+WAVES = [32, 24, 20, 16, 13, 11, 9, 7, 5]  # one-wave blocks resident per CU, set through unused LDS
+
+
+def lds_for(waves: int) -> int:
+    return 0 if waves >= 32 else -(-LDS_PER_CU // waves // 256) * 256
 
 
 def operands(k, nbytes, layout):
@@ -53,7 +61,7 @@ def median_ms(fn, reps=30):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--mib", type=int, default=256)
+    p.add_argument("--mib", type=int, default=1024)
     p.add_argument("--out", default="gpurun_out/tune_multi.json")
     a = p.parse_args()
     nbytes = a.mib << 20
@@ -70,17 +78,22 @@ def main():
             row = {"layout": layout, "k": k, "bytes_per_launch": (k + 2) * nbytes}
             ms = median_ms(lambda: dccl_amd.local_reduce_multi(sends, recv, 7, n, 0, st))
             row["shipped_ms"] = round(ms, 4)
+            row["shipped_frac"] = round((k + 2) * nbytes / (ms * 1e-3) / PEAK, 4)
             for v in VARIANTS:
-                ms = median_ms(lambda: dccl_amd.lib.dccl_tune_multi_f32_sum(arr, k, recv, n, v, st))
+                ms = median_ms(lambda: dccl_amd.lib.dccl_tune_multi_f32_sum(arr, k, recv, n, v, 0, st))
                 row[f"v{v}_ms"] = round(ms, 4)
                 row[f"v{v}_frac"] = round((k + 2) * nbytes / (ms * 1e-3) / PEAK, 4)
+            for w in WAVES:
+                ms = median_ms(lambda: dccl_amd.lib.dccl_tune_multi_f32_sum(arr, k, recv, n, 0, lds_for(w), st))
+                row[f"w{w}_frac"] = round((k + 2) * nbytes / (ms * 1e-3) / PEAK, 4)
             rows.append(row)
             print(json.dumps(row), flush=True)
             del keep
             torch.cuda.empty_cache()
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
-        json.dump({"device": torch.cuda.get_device_name(), "variants": VARIANTS, "rows": rows}, f, indent=1)
+        json.dump({"device": torch.cuda.get_device_name(), "variants": VARIANTS,
+                   "waves": {w: lds_for(w) for w in WAVES}, "rows": rows}, f, indent=1)
 
 
 if __name__ == "__main__":
