@@ -83,6 +83,9 @@ def _load():
         "dccl_local_reduce_multi": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_int, c_size_t,
                                             c_int, c_void_p]),
         "dccl_local_reduce_host": (c_int, [c_void_p, c_void_p, c_int, c_size_t, c_int]),
+        "dccl_local_reduce_chain": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_void_p, c_int, c_size_t,
+                                            c_int, c_void_p]),
+        "dccl_copy_multi": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_size_t, c_void_p]),
         "dccl_register_host_memory": (c_int, [c_void_p, c_size_t]),
         "dccl_deregister_host_memory": (c_int, [c_void_p]),
         "dccl_size_of_type": (c_size_t, [c_int]),
@@ -99,6 +102,9 @@ def _load():
         "dccl_get_unique_id": (c_int, [c_void_p]),
         "dccl_comm_init_rccl": (c_int, [ctypes.POINTER(c_void_p), ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
         "dccl_comm_finalize": (c_int, [c_void_p]),
+        "dccl_comm_init_ipc": (c_int, [ctypes.POINTER(c_void_p), ctypes.c_uint32, ctypes.c_uint32]),
+        "dccl_reduce": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, c_void_p, c_void_p]),
+        "dccl_broadcast": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
         "dccl_all_reduce": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
         "dccl_reduce_scatter": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
         "dccl_all_gather": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_void_p]),
@@ -125,7 +131,8 @@ EXPORTED_SYMBOLS = [
     "dccl_tune_variant_info", "dccl_tune_asm_f32_sum", "dccl_tune_reduce_f32_sum_lds",
     "dccl_comm_init_rank", "dccl_get_unique_id", "dccl_comm_init_rccl", "dccl_comm_finalize", "dccl_all_reduce",
     "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available", "dccl_tune_skew_f32_sum",
-    "dccl_synth_fill", "dccl_tune_multi_f32_sum",
+    "dccl_synth_fill", "dccl_tune_multi_f32_sum", "dccl_local_reduce_chain", "dccl_copy_multi",
+    "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast",
 ]
 
 
@@ -161,6 +168,20 @@ def local_reduce_multi(send_ptrs, recv_ptr: int, dtype: int, count: int, op: int
                                            stream or None))
 
 
+def local_reduce_chain(send_ptrs, own_ptr: int, dst_ptr: int, dtype: int, count: int, op: int, stream: int = 0) -> int:
+    """dst = op(own, op(s[k-1], ... op(s[1], s[0]))): the ring reduce-scatter's order for one chunk."""
+    arr = (ctypes.c_void_p * max(1, len(send_ptrs)))(*send_ptrs)
+    return int(lib.dccl_local_reduce_chain(arr, len(send_ptrs), own_ptr, dst_ptr, int(dtype), int(count), int(op),
+                                           stream or None))
+
+
+def copy_multi(src_ptrs, dst_ptrs, nbytes: int, stream: int = 0) -> int:
+    n = len(src_ptrs)
+    s = (ctypes.c_void_p * max(1, n))(*src_ptrs)
+    d = (ctypes.c_void_p * max(1, n))(*dst_ptrs)
+    return int(lib.dccl_copy_multi(s, d, n, int(nbytes), stream or None))
+
+
 def local_reduce_host(send_ptr: int, recv_ptr: int, dtype: int, count: int, op: int) -> int:
     """Host-pointer combine (staged through the current GPU); synchronous."""
     return int(lib.dccl_local_reduce_host(send_ptr, recv_ptr, int(dtype), int(count), int(op)))
@@ -182,7 +203,8 @@ def deregister_host_memory(ptr: int) -> int:
 class Comm:
     """A DCCL communicator (include/dccl/dccl_comm.h) — the namespace-dccl collectives over the
     in-process transport (``Comm.in_process(world, rank)``, one per thread) or the cross-process
-    RCCL transport (``Comm.rccl(world, rank, unique_id)``, one process per GPU)."""
+    RCCL transport (``Comm.rccl(world, rank, unique_id)``) or IPC peer-read transport
+    (``Comm.ipc(world, rank)``), one process per GPU."""
 
     def __init__(self, handle: int):
         self.handle = handle
@@ -206,6 +228,14 @@ class Comm:
         check(lib.dccl_comm_init_rccl(ctypes.byref(h), world, rank, buf), "dccl_comm_init_rccl")
         return cls(h.value)
 
+    @classmethod
+    def ipc(cls, world: int, rank: int) -> "Comm":
+        """Cross-process IPC peer-read transport (one process per GPU); rendezvous through
+        DCCL_BOOTSTRAP_DIR / DCCL_BOOTSTRAP_TAG (or MASTER_PORT)."""
+        h = ctypes.c_void_p()
+        check(lib.dccl_comm_init_ipc(ctypes.byref(h), world, rank), "dccl_comm_init_ipc")
+        return cls(h.value)
+
     def all_reduce(self, send: int, recv: int, count: int, dtype: int, op: int, stream: int = 0) -> int:
         return int(lib.dccl_all_reduce(send, recv, count, dtype, op, self.handle, stream or None))
 
@@ -214,6 +244,12 @@ class Comm:
 
     def all_gather(self, send: int, recv: int, sendcount: int, dtype: int, stream: int = 0) -> int:
         return int(lib.dccl_all_gather(send, recv, sendcount, dtype, self.handle, stream or None))
+
+    def reduce(self, send: int, recv: int, count: int, dtype: int, op: int, root: int, stream: int = 0) -> int:
+        return int(lib.dccl_reduce(send, recv, count, dtype, op, root, self.handle, stream or None))
+
+    def broadcast(self, send: int, recv: int, count: int, dtype: int, root: int, stream: int = 0) -> int:
+        return int(lib.dccl_broadcast(send, recv, count, dtype, root, self.handle, stream or None))
 
     def finalize(self) -> int:
         h, self.handle = self.handle, None

@@ -14,7 +14,8 @@
 
 namespace dccl_amd {
 
-Group::Group(uint32_t world) : devices(world, -1), taken(world, false), world_(world) {
+Group::Group(uint32_t world)
+    : devices(world, -1), pub_in(world, nullptr), pub_out(world, nullptr), taken(world, false), world_(world) {
     chan_.reserve(size_t(world) * world);
     for (size_t i = 0; i < size_t(world) * world; ++i) chan_.push_back(std::make_unique<Channel>());
 }

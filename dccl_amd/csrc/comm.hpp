@@ -58,6 +58,9 @@ public:
     void barrier();
     // HIP device of each rank (-1: none), filled at join; used to enable peer access.
     std::vector<int> devices;
+    // Buffer addresses each rank publishes for the direct (peer-read) collectives, direct.cpp.
+    std::vector<const void*> pub_in;
+    std::vector<void*> pub_out;
 
     // join bookkeeping (guarded by the registry mutex)
     std::vector<bool> taken;
@@ -82,6 +85,7 @@ struct dccl::dcclComm {
     uint32_t world = 1;
     int device = -1;  // HIP device current at init
     void* rccl = nullptr;  // non-null: cross-process RCCL transport (rccl_transport.hpp), device buffers only
+    void* ipc = nullptr;   // non-null: cross-process IPC peer-read transport (direct.hpp), device buffers only
     // Per-peer event pairs for the stream-ordered device transport (reused every step:
     // a stream wait captures the event's state at the time of the wait).
     std::vector<hipEvent_t> ready_events;  // indexed by destination rank

@@ -30,6 +30,7 @@
 
 #include "algorithms.hpp"
 #include "comm.hpp"
+#include "direct.hpp"
 #include "rccl_transport.hpp"
 #include "dccl/dccl.hpp"
 #include "dccl/dccl_reduce.h"
@@ -211,14 +212,27 @@ bool rccl_requested() {
     return t != nullptr && std::string(t) == "rccl";
 }
 
+bool ipc_requested() {
+    const char* t = std::getenv("DCCL_TRANSPORT");
+    return t != nullptr && std::string(t) == "ipc";
+}
+
+// Cross-process transports move device memory only.
+bool cross_process(const dcclComm* c) { return c->rccl != nullptr || c->ipc != nullptr; }
+
 }  // namespace
 
 namespace dccl {
 
 ncclResult_t ncclCommInit(ncclComm_t* comm) {
     if (comm == nullptr) return ncclInvalidArgument;
-    const long w = env_long("DCCL_WORLD_SIZE", rccl_requested() ? "WORLD_SIZE" : nullptr, 1);
+    const long w = env_long("DCCL_WORLD_SIZE", (rccl_requested() || ipc_requested()) ? "WORLD_SIZE" : nullptr, 1);
     if (w <= 0) return ncclInvalidArgument;
+    if (ipc_requested()) {
+        const long r = env_long("DCCL_RANK", "RANK", 0);
+        if (r < 0 || r >= w) return ncclInvalidArgument;
+        return dcclCommInitIpc(comm, static_cast<uint32_t>(w), static_cast<uint32_t>(r));
+    }
     if (rccl_requested()) {  // one process per GPU: rank / world from the launcher's environment
         const long r = env_long("DCCL_RANK", "RANK", 0);
         if (r < 0 || r >= w) return ncclInvalidArgument;
@@ -240,6 +254,18 @@ ncclResult_t dcclCommInitRccl(ncclComm_t* comm, uint32_t world_size, uint32_t ra
     return join_rccl(comm, world_size, rank, id128);
 }
 
+ncclResult_t dcclCommInitIpc(ncclComm_t* comm, uint32_t world_size, uint32_t rank) {
+    if (comm == nullptr) return ncclInvalidArgument;
+    auto c = std::make_unique<dcclComm>();
+    const ncclResult_t rc = ipc_join(c.get(), world_size, rank);
+    if (rc != ncclSuccess) {
+        if (c->ipc) (void)ipc_leave(c.get());
+        return rc;
+    }
+    *comm = c.release();
+    return ncclSuccess;
+}
+
 ncclResult_t dcclCommInitRank(ncclComm_t* comm, uint32_t world_size, uint32_t rank) {
     if (comm == nullptr) return ncclInvalidArgument;
     return join(comm, world_size, rank);
@@ -252,6 +278,9 @@ ncclResult_t ncclCommFinalize(ncclComm_t comm) {
     if (comm->rccl != nullptr) {
         const int r = rccl_comm_destroy(comm->rccl);
         if (rc == ncclSuccess) rc = static_cast<ncclResult_t>(r);
+    } else if (comm->ipc != nullptr) {
+        const ncclResult_t r = ipc_leave(comm);
+        if (rc == ncclSuccess) rc = r;
     } else {
         comm->group->barrier();  // no peer may still be reading our buffers
     }
@@ -308,10 +337,12 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
     if (sendbuff == nullptr || recvbuff == nullptr) return ncclInvalidArgument;
     bool dev = false;
     if ((rc = placement(sendbuff, recvbuff, &dev)) != ncclSuccess) return rc;
-    if (comm->rccl != nullptr && !dev) return ncclInvalidUsage;  // the RCCL transport moves device memory
+    if (cross_process(comm) && !dev) return ncclInvalidUsage;  // the cross-process transports move device memory
     const size_t total = count * size_of_dtype(datatype);
     const uint32_t W = comm->world;
     if (W > 1 && (count < W || count % W)) return ncclInvalidArgument;
+    if (W > 1 && dev && direct_selected(comm))
+        return direct_all_reduce(comm, sendbuff, recvbuff, count, datatype, op, stream);
     if ((rc = copy_bytes(recvbuff, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:393-408
     if (W == 1) return ncclSuccess;
     void* scratch = nullptr;
@@ -328,9 +359,11 @@ ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recv
     if (sendbuff == nullptr || recvbuff == nullptr) return ncclInvalidArgument;
     bool dev = false;
     if ((rc = placement(sendbuff, recvbuff, &dev)) != ncclSuccess) return rc;
-    if (comm->rccl != nullptr && !dev) return ncclInvalidUsage;
+    if (cross_process(comm) && !dev) return ncclInvalidUsage;
     const uint32_t W = comm->world, r = comm->rank;
     const size_t slot = recvcount * size_of_dtype(datatype), total = slot * W;
+    if (W > 1 && dev && direct_selected(comm))
+        return direct_reduce_scatter(comm, sendbuff, recvbuff, recvcount, datatype, op, stream);
     if ((rc = ensure_work(comm, total, dev)) != ncclSuccess) return rc;
     void* work = dev ? comm->dev_work : comm->host_work;
     if ((rc = copy_bytes(work, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:585-609
@@ -358,7 +391,9 @@ ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, nccl
     if (sendbuff == nullptr || (iamroot && recvbuff == nullptr)) return ncclInvalidArgument;
     bool dev = false;
     if ((rc = placement(sendbuff, iamroot ? recvbuff : sendbuff, &dev)) != ncclSuccess) return rc;
-    if (comm->rccl != nullptr && !dev) return ncclInvalidUsage;
+    if (cross_process(comm) && !dev) return ncclInvalidUsage;
+    if (W > 1 && dev && direct_selected(comm))
+        return direct_reduce(comm, sendbuff, recvbuff, count, datatype, op, uint32_t(root), stream);
     const size_t total = count * size_of_dtype(datatype), slot = total / W;
     void* rbuf = recvbuff;
     if (!iamroot) {
@@ -394,7 +429,9 @@ ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcoun
     bool dev = false;
     ncclResult_t rc = placement(sendbuff, recvbuff, &dev);
     if (rc != ncclSuccess) return rc;
-    if (comm->rccl != nullptr && !dev) return ncclInvalidUsage;
+    if (cross_process(comm) && !dev) return ncclInvalidUsage;
+    if (comm->world > 1 && dev && direct_selected(comm))
+        return direct_all_gather(comm, sendbuff, recvbuff, sendcount, datatype, stream);
     void* slot = static_cast<unsigned char*>(recvbuff) + sendcount * comm->rank * esz;
     if ((rc = copy_bytes(slot, sendbuff, sendcount * esz, dev, stream)) != ncclSuccess) return rc;
     const RankMap id = [](uint32_t x) { return x; };
@@ -412,6 +449,9 @@ ncclResult_t ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, n
     bool dev = false;
     ncclResult_t rc = placement(r == uint32_t(root) ? sendbuff : recvbuff, recvbuff, &dev);
     if (rc != ncclSuccess) return rc;
+    if (comm->ipc != nullptr && !dev) return ncclInvalidUsage;
+    if (W > 1 && dev && direct_selected(comm))
+        return direct_broadcast(comm, sendbuff, recvbuff, count, datatype, uint32_t(root), stream);
     if (comm->rccl != nullptr) {
         if (!dev) return ncclInvalidUsage;
         rc = static_cast<ncclResult_t>(rccl_bcast_p2p(comm->rccl, sendbuff, recvbuff, bytes, uint32_t(root), r, W,
@@ -442,6 +482,7 @@ ncclResult_t ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatyp
     if (esz == 0 || peer < 0 || uint32_t(peer) >= comm->world || uint32_t(peer) == comm->rank)
         return ncclInvalidArgument;  // dccl.cpp:869-872
     const bool dev = is_device_ptr(sendbuff);
+    if (comm->ipc != nullptr) return ncclInvalidUsage;  // the IPC transport has no point-to-point verbs
     if (comm->rccl != nullptr)
         return dev ? static_cast<ncclResult_t>(rccl_exchange(comm->rccl, sendbuff, count * esz, uint32_t(peer),
                                                              nullptr, 0, 0, stream))
@@ -458,6 +499,7 @@ ncclResult_t ncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int
     if (esz == 0 || peer < 0 || uint32_t(peer) >= comm->world || uint32_t(peer) == comm->rank)
         return ncclInvalidArgument;  // dccl.cpp:893-896
     const bool dev = is_device_ptr(recvbuff);
+    if (comm->ipc != nullptr) return ncclInvalidUsage;
     if (comm->rccl != nullptr)
         return dev ? static_cast<ncclResult_t>(rccl_exchange(comm->rccl, nullptr, 0, 0, recvbuff, count * esz,
                                                              uint32_t(peer), stream))
@@ -497,6 +539,11 @@ extern "C" int dccl_comm_init_rccl(void** comm, uint32_t world, uint32_t rank, c
     });
 }
 
+extern "C" int dccl_comm_init_ipc(void** comm, uint32_t world, uint32_t rank) {
+    if (comm == nullptr) return DCCL_INVALID_ARGUMENT;
+    return guarded([&] { return dccl::dcclCommInitIpc(reinterpret_cast<dccl::ncclComm_t*>(comm), world, rank); });
+}
+
 extern "C" int dccl_comm_finalize(void* comm) {
     return guarded([&] { return dccl::ncclCommFinalize(static_cast<dccl::ncclComm_t>(comm)); });
 }
@@ -523,6 +570,23 @@ extern "C" int dccl_all_gather(const void* send, void* recv, size_t sendcount, i
                                void* stream) {
     return guarded([&] {
         return dccl::ncclAllGather(send, recv, sendcount, static_cast<dccl::ncclDataType_t>(dtype),
+                                   static_cast<dccl::ncclComm_t>(comm), static_cast<hipStream_t>(stream));
+    });
+}
+
+extern "C" int dccl_reduce(const void* send, void* recv, size_t count, int dtype, int op, int root, void* comm,
+                           void* stream) {
+    return guarded([&] {
+        return dccl::ncclReduce(send, recv, count, static_cast<dccl::ncclDataType_t>(dtype),
+                                static_cast<dccl::ncclRedOp_t>(op), root, static_cast<dccl::ncclComm_t>(comm),
+                                static_cast<hipStream_t>(stream));
+    });
+}
+
+extern "C" int dccl_broadcast(const void* send, void* recv, size_t count, int dtype, int root, void* comm,
+                              void* stream) {
+    return guarded([&] {
+        return dccl::ncclBroadcast(send, recv, count, static_cast<dccl::ncclDataType_t>(dtype), root,
                                    static_cast<dccl::ncclComm_t>(comm), static_cast<hipStream_t>(stream));
     });
 }

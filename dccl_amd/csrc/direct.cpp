@@ -1,0 +1,408 @@
+// dccl_amd/csrc/direct.cpp — see direct.hpp.
+#include "direct.hpp"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <map>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "dccl/dccl_reduce.h"
+#include "dispatch.hpp"
+
+namespace dccl_amd {
+namespace {
+
+using dccl::dcclComm;
+
+constexpr uint64_t kMagic = 0x3143504943434344ull;  // "DCCIPC1"
+constexpr uint32_t kMaxRanks = 64;
+constexpr size_t kHandleBytes = sizeof(hipIpcMemHandle_t);
+constexpr size_t kMaxOpenPerXport = 256;  // mappings kept open; the oldest is closed beyond this
+
+struct ShmSlot {
+    unsigned char h_in[kHandleBytes];
+    unsigned char h_out[kHandleBytes];
+    uint64_t off_in, off_out;
+};
+
+struct ShmCtl {
+    std::atomic<uint64_t> magic;
+    uint32_t world;
+    std::atomic<uint32_t> joined;
+    std::atomic<uint32_t> count;
+    std::atomic<uint32_t> gen;
+    std::atomic<int32_t> abort;
+    ShmSlot slot[kMaxRanks];
+};
+
+struct Export {
+    size_t size;
+    uint64_t buffer_id;
+    hipIpcMemHandle_t handle;
+};
+
+struct IpcXport {
+    ShmCtl* ctl = nullptr;
+    std::map<uintptr_t, Export> exported;   // allocation base -> its handle (one export per allocation)
+    std::map<std::string, void*> opened;    // peer handle bytes -> mapped base
+    std::deque<std::string> open_order;
+    double timeout_s = 300.0;
+};
+
+IpcXport* xport(const dcclComm* c) { return static_cast<IpcXport*>(c->ipc); }
+
+std::string bootstrap_path() {
+    const char* dir = std::getenv("DCCL_BOOTSTRAP_DIR");
+    const char* tag = std::getenv("DCCL_BOOTSTRAP_TAG");
+    if (!tag) tag = std::getenv("MASTER_PORT");
+    return std::string(dir ? dir : "/tmp") + "/dccl_ipc_name_" + (tag ? tag : "default");
+}
+
+// Sense-reversing barrier on the shared counters; every waiter gives up (and tells the others)
+// after timeout_s, so a dead peer turns into an error instead of a hang.
+ncclResult_t shm_barrier(IpcXport* x) {
+    ShmCtl* s = x->ctl;
+    const uint32_t g = s->gen.load(std::memory_order_acquire);
+    if (s->count.fetch_add(1, std::memory_order_acq_rel) + 1 == s->world) {
+        s->count.store(0, std::memory_order_relaxed);
+        s->gen.store(g + 1, std::memory_order_release);
+        return dccl::ncclSuccess;
+    }
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(x->timeout_s);
+    for (uint64_t i = 0; s->gen.load(std::memory_order_acquire) == g; ++i) {
+        if (s->abort.load(std::memory_order_relaxed)) return dccl::ncclRemoteError;
+        if (i > 4096) {
+            if ((i & 255) == 0 && std::chrono::steady_clock::now() > deadline) {
+                s->abort.store(1, std::memory_order_relaxed);
+                return dccl::ncclSystemError;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+    }
+    return dccl::ncclSuccess;
+}
+
+ncclResult_t export_ptr(IpcXport* x, const void* p, unsigned char* handle_out, uint64_t* off_out) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess) {
+        (void)hipGetLastError();
+        return dccl::ncclInvalidArgument;  // not a device allocation of this process
+    }
+    uint64_t id = 0;
+    if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, reinterpret_cast<hipDeviceptr_t>(base)) !=
+        hipSuccess)
+        (void)hipGetLastError();
+    const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+    auto it = x->exported.find(b);
+    if (it == x->exported.end() || it->second.size != size || it->second.buffer_id != id) {
+        Export e{size, id, {}};
+        if (hipIpcGetMemHandle(&e.handle, base) != hipSuccess) {
+            (void)hipGetLastError();
+            return dccl::ncclUnhandledCudaError;
+        }
+        it = x->exported.insert_or_assign(b, e).first;
+    }
+    std::memcpy(handle_out, &it->second.handle, kHandleBytes);
+    *off_out = reinterpret_cast<uintptr_t>(p) - b;
+    return dccl::ncclSuccess;
+}
+
+// Close the oldest mappings so that this call's imports fit under kMaxOpenPerXport.  Runs before any
+// import of the call (every earlier call's kernels have drained: arrive() synchronised the stream).
+void trim_mappings(IpcXport* x, size_t incoming) {
+    while (!x->open_order.empty() && x->opened.size() + incoming > kMaxOpenPerXport) {
+        auto old = x->opened.find(x->open_order.front());
+        if (old != x->opened.end()) {
+            (void)hipIpcCloseMemHandle(old->second);
+            x->opened.erase(old);
+        }
+        x->open_order.pop_front();
+    }
+}
+
+ncclResult_t import_ptr(IpcXport* x, const unsigned char* handle, uint64_t off, unsigned char** out) {
+    const std::string key(reinterpret_cast<const char*>(handle), kHandleBytes);
+    auto it = x->opened.find(key);
+    if (it == x->opened.end()) {
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handle, kHandleBytes);
+        void* base = nullptr;
+        if (hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            (void)hipGetLastError();
+            return dccl::ncclUnhandledCudaError;
+        }
+        it = x->opened.emplace(key, base).first;
+        x->open_order.push_back(key);
+    }
+    *out = static_cast<unsigned char*>(it->second) + off;
+    return dccl::ncclSuccess;
+}
+
+// Peer addresses of one collective's two buffers, own rank included.
+struct Peers {
+    std::vector<const unsigned char*> in;
+    std::vector<unsigned char*> out;
+};
+
+// This rank's stream has drained (its inputs / outputs are complete) and every rank got here.
+ncclResult_t arrive(dcclComm* c, hipStream_t st) {
+    if (hipStreamSynchronize(st) != hipSuccess) {
+        (void)hipGetLastError();
+        if (c->ipc) xport(c)->ctl->abort.store(1);
+        return dccl::ncclUnhandledCudaError;
+    }
+    if (c->ipc) return shm_barrier(xport(c));
+    c->group->barrier();
+    return dccl::ncclSuccess;
+}
+
+ncclResult_t fail(dcclComm* c, ncclResult_t rc) {
+    if (c->ipc && rc != dccl::ncclSuccess) xport(c)->ctl->abort.store(1);
+    return rc;
+}
+
+// Publish (in, out), wait for every rank, then resolve every rank's (in, out) in this process.
+ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Peers* P) {
+    const uint32_t W = c->world, r = c->rank;
+    P->in.assign(W, nullptr);
+    P->out.assign(W, nullptr);
+    ncclResult_t rc = dccl::ncclSuccess;
+    if (c->ipc) {
+        ShmSlot& s = xport(c)->ctl->slot[r];
+        rc = export_ptr(xport(c), in, s.h_in, &s.off_in);
+        if (rc == dccl::ncclSuccess) rc = export_ptr(xport(c), out, s.h_out, &s.off_out);
+        if (rc != dccl::ncclSuccess) return fail(c, rc);
+    } else {
+        c->group->pub_in[r] = in;
+        c->group->pub_out[r] = out;
+    }
+    if ((rc = arrive(c, st)) != dccl::ncclSuccess) return rc;
+    if (c->ipc) trim_mappings(xport(c), 2 * size_t(W));
+    for (uint32_t p = 0; p < W; ++p) {
+        if (p == r) {
+            P->in[p] = static_cast<const unsigned char*>(in);
+            P->out[p] = static_cast<unsigned char*>(out);
+        } else if (c->ipc) {
+            const ShmSlot& s = xport(c)->ctl->slot[p];
+            unsigned char* pi = nullptr;
+            unsigned char* po = nullptr;
+            rc = import_ptr(xport(c), s.h_in, s.off_in, &pi);
+            if (rc == dccl::ncclSuccess) rc = import_ptr(xport(c), s.h_out, s.off_out, &po);
+            if (rc != dccl::ncclSuccess) return fail(c, rc);
+            P->in[p] = pi;
+            P->out[p] = po;
+        } else {
+            P->in[p] = static_cast<const unsigned char*>(c->group->pub_in[p]);
+            P->out[p] = static_cast<unsigned char*>(c->group->pub_out[p]);
+        }
+    }
+    return dccl::ncclSuccess;
+}
+
+// dst = the ring's combine chain for one chunk: contributions of ranks first, first+1, ...,
+// first+W-2 (their `in` buffers at byte offset `off`), then `own` last.
+ncclResult_t chain(const Peers& P, uint32_t W, uint32_t first, size_t off, const void* own, void* dst, size_t elems,
+                   int dtype, int op, hipStream_t st) {
+    const void* sends[kDirectMaxWorld];
+    for (uint32_t j = 0; j + 1 < W; ++j) sends[j] = P.in[(first + j) % W] + off;
+    return static_cast<ncclResult_t>(
+        dccl_local_reduce_chain(sends, int(W - 1), own, dst, dtype, elems, op, static_cast<void*>(st)));
+}
+
+ncclResult_t copy_pairs(const std::vector<const void*>& src, const std::vector<void*>& dst, size_t bytes,
+                        hipStream_t st) {
+    return static_cast<ncclResult_t>(dccl_copy_multi(src.data(), dst.data(), int(src.size()), bytes, st));
+}
+
+}  // namespace
+
+ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
+    if (world == 0 || world > kMaxRanks || rank >= world) return dccl::ncclInvalidArgument;
+    if (hipGetDevice(&c->device) != hipSuccess) {
+        (void)hipGetLastError();
+        return dccl::ncclUnhandledCudaError;
+    }
+    const std::string path = bootstrap_path();
+    std::string name;
+    int fd = -1;
+    if (rank == 0) {
+        std::random_device rd;
+        name = "/dccl_ipc_" + std::to_string(::getpid()) + "_" + std::to_string(rd());
+        fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0 || ftruncate(fd, sizeof(ShmCtl)) != 0) {
+            if (fd >= 0) ::close(fd);
+            return dccl::ncclSystemError;
+        }
+    } else {
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+        while (fd < 0 && std::chrono::steady_clock::now() < deadline) {
+            std::ifstream f(path);
+            if (std::getline(f, name) && !name.empty()) fd = shm_open(name.c_str(), O_RDWR, 0600);
+            if (fd < 0) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        }
+        if (fd < 0) return dccl::ncclSystemError;
+    }
+    void* m = mmap(nullptr, sizeof(ShmCtl), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    if (m == MAP_FAILED) return dccl::ncclSystemError;
+    auto* ctl = static_cast<ShmCtl*>(m);
+    if (rank == 0) {
+        std::memset(m, 0, sizeof(ShmCtl));  // fresh segment; atomics are plain words here
+        ctl->world = world;
+        ctl->magic.store(kMagic, std::memory_order_release);
+        const std::string tmp = path + ".tmp";
+        {
+            std::ofstream f(tmp, std::ios::trunc);
+            f << name << "\n";
+            if (!f) return dccl::ncclSystemError;
+        }
+        if (std::rename(tmp.c_str(), path.c_str()) != 0) return dccl::ncclSystemError;
+    } else {
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+        while (ctl->magic.load(std::memory_order_acquire) != kMagic) {
+            if (std::chrono::steady_clock::now() > deadline) return dccl::ncclSystemError;
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        if (ctl->world != world) return dccl::ncclInvalidUsage;
+    }
+    auto* x = new IpcXport;
+    x->ctl = ctl;
+    if (const char* t = std::getenv("DCCL_IPC_TIMEOUT_S")) x->timeout_s = std::strtod(t, nullptr);
+    ctl->joined.fetch_add(1);
+    c->ipc = x;
+    c->rank = rank;
+    c->world = world;
+    const ncclResult_t rc = shm_barrier(x);  // everyone mapped the segment
+    if (rc == dccl::ncclSuccess && rank == 0) {   // nothing left to find by name
+        shm_unlink(name.c_str());
+        std::remove(path.c_str());
+    }
+    return rc;
+}
+
+ncclResult_t ipc_leave(dcclComm* c) {
+    IpcXport* x = xport(c);
+    if (x == nullptr) return dccl::ncclInvalidArgument;
+    const ncclResult_t rc = shm_barrier(x);  // no peer still reads our buffers
+    for (auto& kv : x->opened) (void)hipIpcCloseMemHandle(kv.second);
+    munmap(x->ctl, sizeof(ShmCtl));
+    delete x;
+    c->ipc = nullptr;
+    return rc;
+}
+
+bool direct_selected(const dcclComm* c) {
+    if (c->ipc != nullptr) return true;
+    if (c->rccl != nullptr || c->world > kDirectMaxWorld) return false;
+    const char* a = std::getenv("DCCL_ALLREDUCE_ALGORITHM");
+    return a != nullptr && std::string(a) == "direct";
+}
+
+// ncclAllReduce: the ring all-reduce (all_reduce_ring.cpp:8-79) leaves chunk r+1 reduced on rank r;
+// here rank r reduces that chunk from every rank's input in the ring's order, then pulls every other
+// chunk from the rank that reduced it.
+ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t count, int dtype, int op,
+                               hipStream_t st) {
+    const uint32_t W = c->world, r = c->rank;
+    if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
+    const size_t esz = size_of_dtype(dtype), slot_elems = count / W, slot = slot_elems * esz;
+    Peers P;
+    ncclResult_t rc = exchange(c, send, recv, st, &P);
+    if (rc != dccl::ncclSuccess) return rc;
+    const uint32_t mine = (r + 1) % W;
+    rc = chain(P, W, mine, mine * slot, P.in[r] + mine * slot, P.out[r] + mine * slot, slot_elems, dtype, op, st);
+    if (rc != dccl::ncclSuccess) return fail(c, rc);
+    if ((rc = arrive(c, st)) != dccl::ncclSuccess) return rc;  // every chunk reduced by its owner
+    std::vector<const void*> src;
+    std::vector<void*> dst;
+    for (uint32_t k = 0; k < W; ++k) {
+        if (k == mine) continue;
+        src.push_back(P.out[(k + W - 1) % W] + k * slot);  // chunk k lives on rank k-1
+        dst.push_back(P.out[r] + k * slot);
+    }
+    if ((rc = copy_pairs(src, dst, slot, st)) != dccl::ncclSuccess) return fail(c, rc);
+    return arrive(c, st);  // peers are done reading our buffers
+}
+
+// ncclReduceScatter: the ring with rank maps (o+W-1)%W / (n+1)%W (dccl.cpp:551-698) leaves slot o on
+// rank o, combined in the order o+1, o+2, ..., o-1, o.
+ncclResult_t direct_reduce_scatter(dcclComm* c, const void* send, void* recv, size_t recvcount, int dtype, int op,
+                                   hipStream_t st) {
+    const uint32_t W = c->world, r = c->rank;
+    if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
+    const size_t slot = recvcount * size_of_dtype(dtype);
+    Peers P;
+    ncclResult_t rc = exchange(c, send, recv, st, &P);
+    if (rc != dccl::ncclSuccess) return rc;
+    rc = chain(P, W, (r + 1) % W, r * slot, P.in[r] + r * slot, recv, recvcount, dtype, op, st);
+    if (rc != dccl::ncclSuccess) return fail(c, rc);
+    return arrive(c, st);
+}
+
+// ncclReduce: the reference runs the reduce-scatter ring with the same maps, then gathers the slots
+// at the root (dccl.cpp:745-846); here the root reduces every slot itself.
+ncclResult_t direct_reduce(dcclComm* c, const void* send, void* recv, size_t count, int dtype, int op, uint32_t root,
+                           hipStream_t st) {
+    const uint32_t W = c->world, r = c->rank;
+    if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
+    const size_t slot_elems = count / W, slot = slot_elems * size_of_dtype(dtype);
+    Peers P;
+    ncclResult_t rc = exchange(c, send, r == root ? recv : const_cast<void*>(send), st, &P);
+    if (rc != dccl::ncclSuccess) return rc;
+    if (r == root) {
+        for (uint32_t o = 0; o < W && rc == dccl::ncclSuccess; ++o)
+            rc = chain(P, W, (o + 1) % W, o * slot, P.in[o] + o * slot, P.out[r] + o * slot, slot_elems, dtype, op,
+                       st);
+        if (rc != dccl::ncclSuccess) return fail(c, rc);
+    }
+    return arrive(c, st);
+}
+
+ncclResult_t direct_all_gather(dcclComm* c, const void* send, void* recv, size_t sendcount, int dtype,
+                               hipStream_t st) {
+    const uint32_t W = c->world, r = c->rank;
+    if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
+    const size_t slot = sendcount * size_of_dtype(dtype);
+    Peers P;
+    ncclResult_t rc = exchange(c, send, recv, st, &P);
+    if (rc != dccl::ncclSuccess) return rc;
+    std::vector<const void*> src;
+    std::vector<void*> dst;
+    for (uint32_t p = 0; p < W; ++p) {
+        if (p == r && P.in[r] == P.out[r] + r * slot) continue;  // already in place
+        src.push_back(P.in[p]);
+        dst.push_back(P.out[r] + p * slot);
+    }
+    if ((rc = copy_pairs(src, dst, slot, st)) != dccl::ncclSuccess) return fail(c, rc);
+    return arrive(c, st);
+}
+
+ncclResult_t direct_broadcast(dcclComm* c, const void* send, void* recv, size_t count, int dtype, uint32_t root,
+                              hipStream_t st) {
+    const uint32_t r = c->rank;
+    const size_t bytes = count * size_of_dtype(dtype);
+    Peers P;
+    ncclResult_t rc = exchange(c, r == root ? send : recv, recv, st, &P);
+    if (rc != dccl::ncclSuccess) return rc;
+    if (P.in[root] != P.out[r]) {
+        std::vector<const void*> src{P.in[root]};
+        std::vector<void*> dst{P.out[r]};
+        if ((rc = copy_pairs(src, dst, bytes, st)) != dccl::ncclSuccess) return fail(c, rc);
+    }
+    return arrive(c, st);
+}
+
+}  // namespace dccl_amd

@@ -117,6 +117,81 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Multi-source copy (the all-gather half of the direct collectives): pair y copies `bytes`
+// from src[y] to dst[y]; every pair in one launch, so reads from up to 8 peers (8 xGMI links)
+// are in flight together.  Requires src[y] and dst[y] to share a 16-B phase.
+// ---------------------------------------------------------------------------------
+struct CopyList { const unsigned char* src[8]; unsigned char* dst[8]; };
+
+__global__ __launch_bounds__(64) void copy_multi_kernel(CopyList cl, size_t bytes) {
+    const unsigned char* s = cl.src[blockIdx.y];
+    unsigned char* d = cl.dst[blockIdx.y];
+    size_t head = (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15;
+    if (head > bytes) head = bytes;
+    const size_t nvec = (bytes - head) / 16;
+    const u32x4* vs = reinterpret_cast<const u32x4*>(s + head);
+    u32x4* vd = reinterpret_cast<u32x4*>(d + head);
+    for (size_t i = size_t(blockIdx.x) * 64 + threadIdx.x; i < nvec; i += size_t(gridDim.x) * 64)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(vs + i), vd + i);
+    if (blockIdx.x == 0) {
+        for (size_t b = threadIdx.x; b < head; b += 64) d[b] = s[b];
+        for (size_t b = head + nvec * 16 + threadIdx.x; b < bytes; b += 64) d[b] = s[b];
+    }
+}
+
+template <typename T, int OP, int K>
+int launch_chain_vec(SendList sl, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream) {
+    using C = DefaultCfg;
+    size_t grid = ceil_div(sp.nvec, C::TILE);
+    if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    void* args[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&reduce_chain_vec_kernel<T, OP, K, C>), grid, args, stream, C::BLOCK,
+                  multi_lds(K));
+}
+
+template <typename T, int OP>
+int reduce_chain_typed(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
+                       hipStream_t stream) {
+    SendList sl{};
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(dst), ao = reinterpret_cast<uintptr_t>(own);
+    bool elem_ok = ((ad | ao) % sizeof(T)) == 0, vec_ok = elem_ok && ((ad ^ ao) & 15) == 0;
+    for (int k = 0; k < nsend; ++k) {
+        sl.p[k] = static_cast<const unsigned char*>(sends[k]);
+        const uintptr_t a = reinterpret_cast<uintptr_t>(sends[k]);
+        if (a % sizeof(T)) elem_ok = vec_ok = false;
+        if ((a ^ ad) & 15) vec_ok = false;
+    }
+    const auto o = static_cast<const unsigned char*>(own);
+    auto d = static_cast<unsigned char*>(dst);
+    if (!vec_ok) {
+        const size_t grid = ceil_div(count, size_t(kBlock));
+        void* args[] = {&sl, &nsend, const_cast<const unsigned char**>(&o), &d, &count};
+        const void* fn = elem_ok ? reinterpret_cast<const void*>(&reduce_chain_scalar_kernel<T, OP, true>)
+                                 : reinterpret_cast<const void*>(&reduce_chain_scalar_kernel<T, OP, false>);
+        return launch(fn, grid, args, stream);
+    }
+    const Split sp = split_for_vectors<T>(ad, count);
+    switch (nsend) {
+    case 1: return launch_chain_vec<T, OP, 1>(sl, o, d, sp, stream);
+    case 2: return launch_chain_vec<T, OP, 2>(sl, o, d, sp, stream);
+    case 3: return launch_chain_vec<T, OP, 3>(sl, o, d, sp, stream);
+    case 4: return launch_chain_vec<T, OP, 4>(sl, o, d, sp, stream);
+    case 5: return launch_chain_vec<T, OP, 5>(sl, o, d, sp, stream);
+    case 6: return launch_chain_vec<T, OP, 6>(sl, o, d, sp, stream);
+    case 7: return launch_chain_vec<T, OP, 7>(sl, o, d, sp, stream);
+    case 8: return launch_chain_vec<T, OP, 8>(sl, o, d, sp, stream);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+
+struct ReduceChainFn {
+    template <typename T, int OP>
+    static int run(const void* const* sends, int nsend, const void* own, void* dst, size_t count, hipStream_t stream) {
+        return reduce_chain_typed<T, OP>(sends, nsend, own, dst, count, stream);
+    }
+};
+
 struct ReduceFn {
     template <typename T, int OP>
     static int run(const void* send, void* recv, size_t count, hipStream_t stream) {
@@ -154,4 +229,43 @@ extern "C" int dccl_local_reduce_multi(const void* const* sends, int nsend, void
     for (int k = 0; k < nsend; ++k)
         if (sends[k] == nullptr) return DCCL_INVALID_ARGUMENT;
     return dispatch<ReduceMultiFn>(dtype, op, sends, nsend, recv, count, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dccl_local_reduce_chain(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
+                                       size_t count, int op, void* stream) {
+    const int v = validate(dtype, op);
+    if (v != DCCL_SUCCESS) return v;
+    if (nsend < 1 || nsend > 8 || sends == nullptr) return DCCL_INVALID_ARGUMENT;
+    if (count == 0) return DCCL_SUCCESS;
+    if (own == nullptr || dst == nullptr) return DCCL_INVALID_ARGUMENT;
+    for (int k = 0; k < nsend; ++k)
+        if (sends[k] == nullptr) return DCCL_INVALID_ARGUMENT;
+    return dispatch<ReduceChainFn>(dtype, op, sends, nsend, own, dst, count, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int dccl_copy_multi(const void* const* srcs, void* const* dsts, int npairs, size_t bytes, void* stream) {
+    if (npairs < 0 || npairs > 8 || (npairs > 0 && (srcs == nullptr || dsts == nullptr))) return DCCL_INVALID_ARGUMENT;
+    if (npairs == 0 || bytes == 0) return DCCL_SUCCESS;
+    CopyList cl{};
+    bool vec_ok = true;
+    for (int y = 0; y < npairs; ++y) {
+        if (srcs[y] == nullptr || dsts[y] == nullptr) return DCCL_INVALID_ARGUMENT;
+        cl.src[y] = static_cast<const unsigned char*>(srcs[y]);
+        cl.dst[y] = static_cast<unsigned char*>(dsts[y]);
+        if ((reinterpret_cast<uintptr_t>(srcs[y]) ^ reinterpret_cast<uintptr_t>(dsts[y])) & 15) vec_ok = false;
+    }
+    const auto st = static_cast<hipStream_t>(stream);
+    if (!vec_ok) {  // rare: differing 16-B phases; the runtime's copy handles any alignment
+        for (int y = 0; y < npairs; ++y)
+            if (hipMemcpyAsync(dsts[y], srcs[y], bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+                return DCCL_UNHANDLED_DEVICE_ERROR;
+        return DCCL_SUCCESS;
+    }
+    size_t gx = ceil_div(bytes / 16 + 1, 64);
+    if (gx > (size_t(1) << 20)) gx = size_t(1) << 20;
+    void* args[] = {&cl, &bytes};
+    return hipLaunchKernel(reinterpret_cast<const void*>(&copy_multi_kernel), dim3(unsigned(gx), unsigned(npairs)),
+                           dim3(64), args, 0, st) == hipSuccess
+               ? DCCL_SUCCESS
+               : DCCL_UNHANDLED_DEVICE_ERROR;
 }

@@ -198,6 +198,57 @@ __global__ __launch_bounds__(kBlock) void reduce_multi_scalar_kernel(SendList se
 }
 
 // ---------------------------------------------------------------------------------
+// Chain kernel: the association order of the reference's ring reduce-scatter for one chunk,
+// in one pass over all contributions:
+//     dst = op(own, op(s{K-1}, ... op(s2, op(s1, s0))))
+// Every application is op(recv = the next rank's own data, send = the partial that arrived),
+// exactly as reduce_scatter_ring.cpp:84-94 applies it, so results are bit-identical to the ring
+// for every dtype and op (Max/Min NaN and signed-zero selection included).  `own` may alias `dst`.
+// ---------------------------------------------------------------------------------
+template <typename T, int OP, int K, typename C>
+__global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sends, const unsigned char* own,
+                                                                    unsigned char* dst, size_t head, size_t nvec,
+                                                                    size_t tail) {
+    static_assert(C::UNROLL == 1, "one vector per lane");
+    const size_t off = head * sizeof(T);
+    const u32x4* vo = reinterpret_cast<const u32x4*>(own + off);
+    u32x4* vd = reinterpret_cast<u32x4*>(dst + off);
+    const size_t ntiles = (nvec + C::TILE - 1) / C::TILE;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t i = t * C::TILE + threadIdx.x;
+        if (i < nvec) {
+            u32x4 s[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) s[k] = ld16<true>(reinterpret_cast<const u32x4*>(sends.p[k] + off) + i);
+            const u32x4 o = ld16<true>(vo + i);
+            u32x4 acc = s[0];
+#pragma unroll
+            for (int k = 1; k < K; ++k) acc = combine16<T, OP>(s[k], acc);
+            __builtin_nontemporal_store(combine16<T, OP>(o, acc), vd + i);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < head + tail) {
+        const size_t i = threadIdx.x < head ? threadIdx.x : head + nvec * Pack<T>::N + (threadIdx.x - head);
+        T acc = ld_elem<T, true>(sends.p[0], i);
+#pragma unroll
+        for (int k = 1; k < K; ++k) acc = Combine<T, OP>::apply(ld_elem<T, true>(sends.p[k], i), acc);
+        st_elem<T, true>(dst, i, Combine<T, OP>::apply(ld_elem<T, true>(own, i), acc));
+    }
+}
+
+template <typename T, int OP, bool ALIGNED>
+__global__ __launch_bounds__(kBlock) void reduce_chain_scalar_kernel(SendList sends, int nsend,
+                                                                     const unsigned char* own, unsigned char* dst,
+                                                                     size_t count) {
+    const size_t stride = size_t(gridDim.x) * kBlock;
+    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < count; i += stride) {
+        T acc = ld_elem<T, ALIGNED>(sends.p[0], i);
+        for (int k = 1; k < nsend; ++k) acc = Combine<T, OP>::apply(ld_elem<T, ALIGNED>(sends.p[k], i), acc);
+        st_elem<T, ALIGNED>(dst, i, Combine<T, OP>::apply(ld_elem<T, ALIGNED>(own, i), acc));
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // Host-side launch helpers
 // ---------------------------------------------------------------------------------
 constexpr size_t kMaxGrid = size_t(1) << 24;  // grid-stride beyond this (2^24 x 64 threads)

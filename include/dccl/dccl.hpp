@@ -78,6 +78,12 @@ ncclResult_t dcclCommInitRank(ncclComm_t* comm, uint32_t world_size, uint32_t ra
  *  RANK/WORLD_SIZE, id exchanged through a file in DCCL_BOOTSTRAP_DIR). Device buffers only. */
 ncclResult_t dcclGetUniqueId(void* unique_id);
 ncclResult_t dcclCommInitRccl(ncclComm_t* comm, uint32_t world_size, uint32_t rank, const void* unique_id);
+/** MI355X-build extension: cross-process communicator on the IPC peer-read transport, one process
+ *  per GPU of one node (the current HIP device).  Collectives read peers' buffers directly over
+ *  xGMI.  ncclCommInit selects it when DCCL_TRANSPORT=ipc (rank/world from
+ *  RANK/WORLD_SIZE, rendezvous through DCCL_BOOTSTRAP_DIR).  Device buffers only, world <= 8
+ *  for the collectives, no ncclSend/ncclRecv. */
+ncclResult_t dcclCommInitIpc(ncclComm_t* comm, uint32_t world_size, uint32_t rank);
 ncclResult_t ncclCommFinalize(ncclComm_t comm);
 
 /** Page-lock host memory for direct DMA (device memory: accepted, nothing to do). */

@@ -7,9 +7,13 @@
  *                         `world` ranks joined (dcclCommInitRank)
  *   dccl_get_unique_id /  cross-process group over the RCCL (xGMI) transport, one process per
  *   dccl_comm_init_rccl   GPU; the 128-byte id travels out of band (dcclCommInitRccl)
+ *   dccl_comm_init_ipc    cross-process group over the IPC peer-read transport (one process per GPU
+ *                         on one node; rendezvous through DCCL_BOOTSTRAP_DIR, dcclCommInitIpc)
  *   dccl_all_reduce       ncclAllReduce       (/root/reference/include/dccl/dccl.hpp:206-207)
  *   dccl_reduce_scatter   ncclReduceScatter   (/root/reference/include/dccl/dccl.hpp:243-244)
  *   dccl_all_gather       ncclAllGather       (/root/reference/include/dccl/dccl.hpp:392-393)
+ *   dccl_reduce           ncclReduce          (/root/reference/include/dccl/dccl.hpp:346-347)
+ *   dccl_broadcast        ncclBroadcast       (/root/reference/include/dccl/dccl.hpp:289-290)
  * A null / finalized communicator returns ncclInvalidArgument (4) instead of throwing.
  */
 #ifndef DCCL_COMM_H_
@@ -22,11 +26,15 @@ extern "C" {
 int dccl_comm_init_rank(void** comm, uint32_t world, uint32_t rank);
 int dccl_get_unique_id(void* unique_id_128);
 int dccl_comm_init_rccl(void** comm, uint32_t world, uint32_t rank, const void* unique_id_128);
+int dccl_comm_init_ipc(void** comm, uint32_t world, uint32_t rank);
 int dccl_comm_finalize(void* comm);
 int dccl_all_reduce(const void* send, void* recv, size_t count, int dtype, int op, void* comm, void* stream);
 int dccl_reduce_scatter(const void* send, void* recv, size_t recvcount, int dtype, int op, void* comm,
                         void* stream);
 int dccl_all_gather(const void* send, void* recv, size_t sendcount, int dtype, void* comm, void* stream);
+int dccl_reduce(const void* send, void* recv, size_t count, int dtype, int op, int root, void* comm,
+                void* stream);
+int dccl_broadcast(const void* send, void* recv, size_t count, int dtype, int root, void* comm, void* stream);
 int dccl_rccl_available(void);
 #ifdef __cplusplus
 }

@@ -62,6 +62,26 @@ int dccl_local_reduce_multi(const void* const* sends, int nsend, void* recv, int
                             int op, void* stream);
 
 /*
+ * Chain combine: the whole combine sequence of the ring reduce-scatter for one chunk, in one pass:
+ *   dst[i] = op(own[i], op(sends[k-1][i], ... op(sends[1][i], sends[0][i])))
+ * Each step is op(recv = next rank's data, send = partial so far), exactly as the ring applies it
+ * (/root/reference/src/core/reduce_scatter_ring.cpp:73-101: rank c+j combines its own chunk c with
+ * the partial received from rank c+j-1), so the result is bit-identical to W-1 ring steps when
+ * sends[j] is rank c+j's chunk and `own` is the last rank's.  `own` may equal `dst`.
+ * 1 <= nsend <= 8.  Used by the direct (xGMI peer-read) collectives, DESIGN.md §7.3.
+ */
+int dccl_local_reduce_chain(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
+                            size_t count, int op, void* stream);
+
+/*
+ * Multi-source device copy: dsts[y][0..bytes) = srcs[y][0..bytes) for y < npairs (<= 8), in one
+ * launch, so the reads of several peers' chunks use several xGMI links at once (the all-gather
+ * half of the direct collectives; replaces W-1 ring all-gather steps,
+ * /root/reference/src/core/all_gather_ring.cpp:44-64).
+ */
+int dccl_copy_multi(const void* const* srcs, void* const* dsts, int npairs, size_t bytes, void* stream);
+
+/*
  * Host combine, synchronous: `send` and `recv` are host pointers (the RDMA
  * receive buffers of the reference's host path).  Replaces the reference's CPU
  * boundary do_host_reduce<DT>

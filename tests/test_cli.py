@@ -152,28 +152,34 @@ def test_cli_rejects_uneven_count_cpu():
 
 # ------------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpu_flag", [-1, 0])
+@pytest.mark.parametrize("gpu_flag,algo", [(-1, "ring"), (0, "ring"), (0, "direct")])
 @pytest.mark.parametrize("kind", ["float32", "uint32"])
-def test_c1_known_answers(gpu_flag, kind):
-    """BASELINE C1: dccl_cli -a all_reduce -c 1024, 4 ranks; the reference's bit patterns."""
+def test_c1_known_answers(gpu_flag, algo, kind):
+    """BASELINE C1: dccl_cli -a all_reduce -c 1024, 4 ranks; the reference's bit patterns, through the
+    ring and (device buffers) through the direct peer-read collectives."""
     g = json.load(open(os.path.join(GOLDEN, "c1_ring.json")))
     for reps in ("1", "2", "10", "1000"):
         rc, rows, err = run_cli("-a", "all_reduce", "-t", kind, "-c", g["count"], "-n", g["world_size"],
-                                "-r", reps, "-g", gpu_flag)
+                                "-r", reps, "-g", gpu_flag, env={"DCCL_ALLREDUCE_ALGORITHM": algo})
         assert rc == 0, err
         for row in rows:
             assert row["uniform"] and int(row["first"], 16) == int(g[kind][reps], 16), (reps, row)
         if reps == "1000":
-            print("C1 latency us/call", [row["us_per_call"] for row in rows])
+            print("C1", algo, "latency us/call", [row["us_per_call"] for row in rows])
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("scratch", ["0", "1"])  # fused recv+combine (default) / reference scratchpad shape
+@pytest.mark.parametrize("algo", ["ring", "ring-scratch", "direct"])  # fused recv+combine / scratchpad / peer-read
 @pytest.mark.parametrize("gpu_flag,device", [(-1, False), (0, True)])
 @pytest.mark.parametrize("api", ["all_reduce", "reduce_scatter", "reduce", "all_gather", "broadcast"])
-def test_cli_apis_against_oracle(api, gpu_flag, device, scratch):
-    if api in ("all_gather", "broadcast") and scratch == "1":
+def test_cli_apis_against_oracle(api, gpu_flag, device, algo):
+    if api in ("all_gather", "broadcast") and algo == "ring-scratch":
         pytest.skip("no combine in this api")
+    if algo == "direct" and not device:
+        pytest.skip("the direct collectives read peers' device memory")
+    env = {"DCCL_RS_SCRATCH": "1" if algo == "ring-scratch" else "0",
+           "DCCL_ALLREDUCE_ALGORITHM": "direct" if algo == "direct" else "ring"}
     for W, n, dtype, op in [(4, 1024, "float32", 0), (3, 3 * 1001, "float64", 1), (2, 4096, "int8", 2),
-                            (8, 8 * 513, "bfloat16", 3), (5, 5 * 77, "uint64", 0), (4, 4 * (1 << 18), "float32", 0)]:
-        check_api(api, W, n, dtype, op, gpu_flag, device, env={"DCCL_RS_SCRATCH": scratch})
+                            (8, 8 * 513, "bfloat16", 3), (5, 5 * 77, "uint64", 0), (4, 4 * (1 << 18), "float32", 0),
+                            (6, 6 * 4099, "float16", 2), (7, 7 * 1000, "int32", 1)]:
+        check_api(api, W, n, dtype, op, gpu_flag, device, env=env)

@@ -1,0 +1,259 @@
+"""Direct (peer-read) collectives, DESIGN.md §7.3.
+
+GPU: the chain combine (dccl_local_reduce_chain) against the oracle applied in the ring's order,
+the multi-source copy, the direct collectives of in-process ranks (threads on one GPU) against the
+ring simulation + oracle (bit-exact), and the cross-process IPC transport with 2-4 processes
+sharing the box's GPU.  CPU: argument checks of the new entry points.
+"""
+import multiprocessing as mp
+import os
+import threading
+import uuid
+
+import numpy as np
+import pytest
+
+import oracle
+from tests import ringsim
+
+SEED = 0xDCC1
+
+
+def chain_expected(sends, own, dt, op):
+    acc = np.array(sends[0], copy=True)
+    for s in sends[1:]:
+        acc = oracle.combine(acc, s, dt, op)  # op(recv = s, send = acc)
+    return oracle.combine(acc, own, dt, op)   # op(recv = own, send = acc)
+
+
+def test_chain_and_copy_argument_checks_cpu():
+    import dccl_amd
+    assert dccl_amd.local_reduce_chain([], 0, 0, 7, 16, 0) == 4           # nsend 0
+    assert dccl_amd.local_reduce_chain([0] * 9, 0, 0, 7, 16, 0) == 4      # nsend 9
+    assert dccl_amd.local_reduce_chain([8], 8, 8, 7, 16, 4) == 5          # Avg
+    assert dccl_amd.local_reduce_chain([8], 8, 8, 11, 16, 0) == 4         # dtype
+    assert dccl_amd.local_reduce_chain([8], 8, 8, 7, 0, 0) == 0           # count 0
+    assert dccl_amd.local_reduce_chain([0], 8, 8, 7, 16, 0) == 4          # NULL send
+    assert dccl_amd.copy_multi([0] * 9, [0] * 9, 16) == 4
+    assert dccl_amd.copy_multi([], [], 16) == 0
+    assert dccl_amd.copy_multi([0], [8], 16) == 4
+
+
+def test_ipc_comm_rejects_bad_rank_cpu():
+    import ctypes
+    import dccl_amd
+    h = ctypes.c_void_p()
+    assert dccl_amd.lib.dccl_comm_init_ipc(ctypes.byref(h), 2, 2) == 4
+    assert dccl_amd.lib.dccl_comm_init_ipc(ctypes.byref(h), 0, 0) == 4
+    assert dccl_amd.lib.dccl_comm_init_ipc(None, 2, 0) == 4
+
+
+# ----------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", list(range(10)))
+def test_chain_against_oracle(gpu, dt):
+    import torch
+    import dccl_amd
+    from tests.test_gpu_parity import rand_inputs
+    rng = np.random.default_rng(dt)
+    esz = dccl_amd.size_of_type(dt)
+    for op in (0, 1, 2, 3):
+        for k, n, off in ((1, 1, 0), (2, 17, 0), (3, 4099, 0), (7, 65537, 0), (8, 1000, 0), (4, 3001, 4),
+                          (5, 777, 2 * esz)):
+            arrs = [rand_inputs(rng, dt, n)[0] for _ in range(k + 1)]
+            sends, own = arrs[:k], arrs[k]
+            want = chain_expected(sends, own, dt, op)
+            dev = [torch.from_numpy(a.view(np.uint8).copy()).cuda() for a in sends]
+            # own and dst in one buffer at `off` bytes; sends at the same 16-B phase only when off % 16 == 0
+            t_own = torch.zeros(n * esz + off + 64, dtype=torch.uint8, device="cuda")
+            t_own[off:off + n * esz].copy_(torch.from_numpy(own.view(np.uint8).copy()))
+            p_own = t_own.data_ptr() + off
+            assert dccl_amd.local_reduce_chain([d.data_ptr() for d in dev], p_own, p_own, dt, n, op) == 0
+            got = t_own[off:off + n * esz].cpu().numpy().view(own.dtype)
+            torch.cuda.synchronize()
+            ok = got.tobytes() == want.tobytes()
+            if not ok and dt in (6, 7, 8, 9):  # NaN payloads are not pinned
+                from tests.test_oracle import fp_equal
+                ok = fp_equal(got, want, dt)
+            assert ok, (op, k, n, off)
+            # separate dst: own untouched
+            t_dst = torch.zeros(n * esz + off + 64, dtype=torch.uint8, device="cuda")
+            t_own[off:off + n * esz].copy_(torch.from_numpy(own.view(np.uint8).copy()))
+            assert dccl_amd.local_reduce_chain([d.data_ptr() for d in dev], p_own, t_dst.data_ptr() + off, dt, n,
+                                               op) == 0
+            torch.cuda.synchronize()
+            assert t_own[off:off + n * esz].cpu().numpy().tobytes() == own.tobytes()
+            assert (t_dst[off:off + n * esz].cpu().numpy().view(own.dtype).tobytes() == got.tobytes())
+
+
+@pytest.mark.gpu
+def test_copy_multi(gpu):
+    import torch
+    import dccl_amd
+    for nbytes, soff, doff in ((1, 0, 0), (15, 3, 3), (4096, 0, 0), ((1 << 20) + 7, 5, 5), (1000, 1, 2)):
+        srcs = [torch.randint(0, 255, (nbytes + 64,), dtype=torch.uint8, device="cuda") for _ in range(8)]
+        dsts = [torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda") for _ in range(8)]
+        assert dccl_amd.copy_multi([s.data_ptr() + soff for s in srcs], [d.data_ptr() + doff for d in dsts],
+                                   nbytes) == 0
+        torch.cuda.synchronize()
+        for s, d in zip(srcs, dsts):
+            assert torch.equal(d[doff:doff + nbytes], s[soff:soff + nbytes])
+            assert int(d[:doff].sum()) == 0 and int(d[doff + nbytes:].sum()) == 0
+
+
+def _inputs(W, n, dt, op):
+    return [oracle.synth(n, dt, op, SEED, r) for r in range(W)]
+
+
+def _ring_expected(api, inputs, dt, op, root=0):
+    W = len(inputs)
+    slot = inputs[0].size // W
+
+    def combine(s, r):
+        assert oracle.expected_reduce(np.ascontiguousarray(s), r, dt, op) == 0
+
+    def copy(d, s):
+        d[:] = s
+
+    bufs = [x.copy() for x in inputs]
+    if api == "all_reduce":
+        return ringsim.ring_allreduce(bufs, combine, copy)
+    if api == "reduce_scatter":
+        ringsim.reduce_scatter_ring(bufs, combine, *ringsim.rs_maps())
+        return [bufs[r][r * slot:(r + 1) * slot] for r in range(W)]
+    if api == "reduce":
+        ringsim.reduce_scatter_ring(bufs, combine, *ringsim.rs_maps())
+        return np.concatenate([bufs[r][r * slot:(r + 1) * slot] for r in range(W)])
+    raise ValueError(api)
+
+
+def _run_direct_rank(comm, r, W, n, dt, op, api, stream, torch):
+    """One rank's part: returns the host copy of the output buffer."""
+    import dccl_amd
+    esz = dccl_amd.size_of_type(dt)
+    x = oracle.synth(n, dt, op, SEED, r)
+    send = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+    out_bytes = {"all_reduce_inplace": 0, "reduce_scatter": n // W * esz, "all_gather": W * n * esz}.get(api, n * esz)
+    out = torch.zeros(out_bytes, dtype=torch.uint8, device="cuda") if out_bytes else send
+    torch.cuda.synchronize()  # inputs and zeroed outputs complete before the collective's stream runs
+    s, o = send.data_ptr(), out.data_ptr()
+    if api in ("all_reduce_inplace", "all_reduce"):
+        rc = comm.all_reduce(s, o, n, dt, op, stream)
+    elif api == "reduce_scatter":
+        rc = comm.reduce_scatter(s, o, n // W, dt, op, stream)
+    elif api == "reduce":
+        rc = comm.reduce(s, o, n, dt, op, 1 % W, stream)
+    elif api == "all_gather":
+        rc = comm.all_gather(s, o, n, dt, stream)
+    elif api == "broadcast":
+        rc = comm.broadcast(s, o, n, dt, W - 1, stream)
+    else:
+        raise ValueError(api)
+    assert rc == 0, (api, rc)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def _check(api, outs, W, n, dt, op):
+    npd = oracle.NP_DTYPES[dt]
+    inputs = _inputs(W, n, dt, op)
+    if api in ("all_reduce", "all_reduce_inplace"):
+        want = _ring_expected("all_reduce", inputs, dt, op)
+        for r in range(W):
+            assert outs[r].view(npd).tobytes() == want[r].tobytes(), (api, r)
+    elif api == "reduce_scatter":
+        want = _ring_expected("reduce_scatter", inputs, dt, op)
+        for r in range(W):
+            assert outs[r].view(npd).tobytes() == want[r].tobytes(), (api, r)
+    elif api == "reduce":
+        want = _ring_expected("reduce", inputs, dt, op)
+        assert outs[1 % W].view(npd).tobytes() == want.tobytes()
+    elif api == "all_gather":
+        want = np.concatenate(inputs)
+        for r in range(W):
+            assert outs[r].view(npd).tobytes() == want.tobytes(), (api, r)
+    elif api == "broadcast":
+        for r in range(W):
+            assert outs[r].view(npd).tobytes() == inputs[W - 1].tobytes(), (api, r)
+
+
+APIS = ["all_reduce_inplace", "all_reduce", "reduce_scatter", "reduce", "all_gather", "broadcast"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,n,dt,op", [(2, 2 * 4099, 7, 0), (4, 4 * 65536, 9, 2), (8, 8 * 1001, 4, 1),
+                                       (3, 3 * 777, 6, 3), (5, 5 * 77, 5, 0)])
+def test_direct_in_process(gpu, monkeypatch, W, n, dt, op):
+    import torch
+    import dccl_amd
+    monkeypatch.setenv("DCCL_ALLREDUCE_ALGORITHM", "direct")
+    for api in APIS:
+        outs, errs = [None] * W, []
+
+        def worker(r):
+            try:
+                comm = dccl_amd.Comm.in_process(W, r)
+                try:
+                    st = torch.cuda.Stream()
+                    outs[r] = _run_direct_rank(comm, r, W, n, dt, op, api, st.cuda_stream, torch)
+                finally:
+                    comm.finalize()
+            except Exception as e:  # pragma: no cover - reported below
+                errs.append((r, repr(e)))
+
+        ts = [threading.Thread(target=worker, args=(r,)) for r in range(W)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=300)
+        assert not errs, (api, errs)
+        _check(api, outs, W, n, dt, op)
+
+
+def _ipc_rank(r, W, n, dt, op, tag, q):
+    os.environ["DCCL_BOOTSTRAP_TAG"] = tag
+    try:
+        import torch
+        import dccl_amd
+        torch.cuda.set_device(0)
+        comm = dccl_amd.Comm.ipc(W, r)
+        outs = {}
+        try:
+            st = torch.cuda.Stream()
+            for api in APIS:
+                outs[api] = _run_direct_rank(comm, r, W, n, dt, op, api, st.cuda_stream, torch)
+            outs["host_rejected"] = comm.all_reduce(np.zeros(4, np.float32).ctypes.data,
+                                                    np.zeros(4, np.float32).ctypes.data, 4, 7, 0) == 5
+        finally:
+            outs["finalize"] = comm.finalize()
+        q.put((r, outs, None))
+    except Exception as e:  # pragma: no cover - reported by the parent
+        q.put((r, None, repr(e)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,n,dt,op", [(2, 2 * 65536, 7, 0), (4, 4 * 4099, 2, 1), (3, 3 * 1000, 9, 3)])
+def test_ipc_transport_processes(gpu, W, n, dt, op):
+    """One process per rank (all on the box's one GPU), buffers exported with hipIpcGetMemHandle and
+    read by the peers: every direct collective bit-exact against the ring simulation."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    tag = "test_" + uuid.uuid4().hex[:12]
+    ps = [ctx.Process(target=_ipc_rank, args=(r, W, n, dt, op, tag, q)) for r in range(W)]
+    for p in ps:
+        p.start()
+    results = {}
+    try:
+        for _ in range(W):
+            r, outs, err = q.get(timeout=240)
+            assert err is None, (r, err)
+            results[r] = outs
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for api in APIS:
+        _check(api, [results[r][api] for r in range(W)], W, n, dt, op)
+    assert all(results[r]["host_rejected"] for r in range(W))
+    assert all(results[r]["finalize"] == 0 for r in range(W))
