@@ -21,8 +21,9 @@ Rank 0 prints ONE JSON line:
                    restatement, single thread, timed on this host on a bounded sample (rank 0, N=1)
 Extra keys: payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
 rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately),
-dccl_allreduce_rccl (N>1: the namespace-dccl ncclAllReduce — ring with the gfx950 combine — over
-the RCCL p2p transport, checked against and timed beside RCCL's own all_reduce; under a watchdog).
+dccl_allreduce (N>1: the namespace-dccl ncclAllReduce over the RCCL p2p ring and over the direct
+IPC peer-read transport, checked against each other and RCCL's own all_reduce, timed beside it;
+under a watchdog).
 """
 from __future__ import annotations
 
@@ -206,60 +207,79 @@ def run_with_watchdog(fn, seconds: float):
     return box["value"], True
 
 
-def dccl_allreduce_rccl(world: int, rank: int, dev, count: int, iters: int = 5) -> dict:
-    """the namespace-dccl ncclAllReduce (ring RS with the gfx950 combine + ring AG)
-    over the RCCL p2p transport, one process per GPU; checked against RCCL's own all_reduce
-    (int32: bit-exact; fp32: |d| <= (W-1) eps sum|x|, a different association order) and timed."""
+def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5) -> dict:
+    """the namespace-dccl ncclAllReduce end to end on one node, one process per GPU,
+    through both cross-process transports:
+      ring    ring RS with the gfx950 combine + ring AG, chunks moved by RCCL send/recv;
+      direct  each GPU reduces its chunk from all peers' buffers at once over xGMI (IPC-mapped,
+              dccl_local_reduce_chain in the ring's order) and pulls the other chunks.
+    Both are checked against RCCL's own all_reduce (int32: bit-exact; fp32: |d| <= (W-1) eps sum|x|, a
+    different association order) and against each other (fp32: bit-exact, same order), and timed."""
+    os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")
+    transports = os.environ.get("DCCL_BENCH_AR_TRANSPORTS", "ring,direct").split(",")
     uid = None
-    if rank == 0:
+    if rank == 0 and "ring" in transports:
         try:
             uid = dccl_amd.Comm.unique_id()
         except Exception:  # every rank must still reach the broadcast below
             uid = None
     obj = [uid]
     dist.broadcast_object_list(obj, src=0)
-    if obj[0] is None:
-        raise RuntimeError("rank 0 could not create an RCCL unique id (librccl not loadable?)")
-    comm = dccl_amd.Comm.rccl(world, rank, obj[0])
-    out = {"count": count, "world": world}
+    comms = {}
+    if obj[0] is not None:
+        comms["ring"] = dccl_amd.Comm.rccl(world, rank, obj[0])
+    if "direct" in transports:
+        comms["direct"] = dccl_amd.Comm.ipc(world, rank)
+    out = {"count": count, "world": world, "bytes": count * 4}
     try:
         st = torch.cuda.current_stream(dev)
         g = torch.Generator(device=dev).manual_seed(1234 + rank)
         xi = torch.randint(-2**20, 2**20, (count,), device=dev, generator=g, dtype=torch.int32)
-        yi = xi.clone()
-        dccl_amd.check(comm.all_reduce(yi.data_ptr(), yi.data_ptr(), count, 2, 0, st.cuda_stream), "all_reduce i32")
-        ri = xi.clone()
-        dist.all_reduce(ri)
-        torch.cuda.synchronize(dev)
-        out["int32_sum_bit_exact_vs_rccl"] = bool(torch.equal(yi, ri))
         xf = torch.rand(count, device=dev, generator=g).mul_(2).sub_(1)
-        yf = xf.clone()
-        dccl_amd.check(comm.all_reduce(yf.data_ptr(), yf.data_ptr(), count, 7, 0, st.cuda_stream), "all_reduce f32")
-        rf = xf.clone()
+        ri, rf = xi.clone(), xf.clone()
+        dist.all_reduce(ri)
         dist.all_reduce(rf)
-        torch.cuda.synchronize(dev)
-        bound = (world - 1) * 1.2e-7 * world  # |x| < 1
-        out["fp32_max_abs_diff_vs_rccl"] = float((yf - rf).abs().max())
-        out["fp32_within_bound"] = out["fp32_max_abs_diff_vs_rccl"] <= bound
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            dccl_amd.check(comm.all_reduce(yf.data_ptr(), yf.data_ptr(), count, 7, 0, st.cuda_stream), "all_reduce")
-        torch.cuda.synchronize(dev)
-        t_dccl = (time.perf_counter() - t0) / iters
+        yf_by = {}
+        for name, comm in comms.items():
+            yi = xi.clone()
+            yf = xf.clone()
+            torch.cuda.synchronize(dev)
+            dccl_amd.check(comm.all_reduce(yi.data_ptr(), yi.data_ptr(), count, 2, 0, st.cuda_stream), name)
+            dccl_amd.check(comm.all_reduce(yf.data_ptr(), yf.data_ptr(), count, 7, 0, st.cuda_stream), name)
+            torch.cuda.synchronize(dev)
+            bound = (world - 1) * 1.2e-7 * world  # |x| < 1
+            diff = float((yf - rf).abs().max())
+            res = {"int32_sum_bit_exact_vs_rccl": bool(torch.equal(yi, ri)),
+                   "fp32_max_abs_diff_vs_rccl": diff, "fp32_within_bound": diff <= bound}
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                dccl_amd.check(comm.all_reduce(yf.data_ptr(), yf.data_ptr(), count, 7, 0, st.cuda_stream), name)
+            torch.cuda.synchronize(dev)
+            t = (time.perf_counter() - t0) / iters
+            res.update({"ms": round(t * 1e3, 3), "busbw_gb_s": round(2 * (world - 1) / world * count * 4 / t / 1e9, 1)})
+            out[name] = res
+            yf_by[name] = yf
+        if "ring" in yf_by and "direct" in yf_by:
+            # same association order: the first all_reduce of each path must agree bit for bit
+            a_, b_ = xf.clone(), xf.clone()
+            torch.cuda.synchronize(dev)
+            dccl_amd.check(comms["ring"].all_reduce(a_.data_ptr(), a_.data_ptr(), count, 7, 0, st.cuda_stream), "r")
+            dccl_amd.check(comms["direct"].all_reduce(b_.data_ptr(), b_.data_ptr(), count, 7, 0, st.cuda_stream), "d")
+            torch.cuda.synchronize(dev)
+            out["fp32_direct_bit_exact_vs_ring"] = bool(torch.equal(a_.view(torch.int32), b_.view(torch.int32)))
         dist.barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
             dist.all_reduce(rf)
         torch.cuda.synchronize(dev)
-        t_rccl = (time.perf_counter() - t0) / iters
-        nbytes = count * 4
-        out.update({"dccl_ms": round(t_dccl * 1e3, 3), "rccl_allreduce_ms": round(t_rccl * 1e3, 3),
-                    "dccl_busbw_gb_s": round(2 * (world - 1) / world * nbytes / t_dccl / 1e9, 1),
-                    "rccl_busbw_gb_s": round(2 * (world - 1) / world * nbytes / t_rccl / 1e9, 1),
-                    "note": "RCCL's own all_reduce is an informational comparison: its combine is RCCL's"})
+        t = (time.perf_counter() - t0) / iters
+        out["rccl_allreduce"] = {"ms": round(t * 1e3, 3),
+                                 "busbw_gb_s": round(2 * (world - 1) / world * count * 4 / t / 1e9, 1),
+                                 "note": "RCCL's own all_reduce, informational: its combine is RCCL's"}
     finally:
-        comm.finalize()
+        for comm in comms.values():
+            comm.finalize()
     return out
 
 
@@ -364,12 +384,15 @@ def main():
                               "note": "RCCL all_gather_into_tensor of the reduced shards over xGMI "
                                       "(every GPU ends with the full result); not in value"}
         del gathered, src
-        if backend == "nccl" and os.environ.get("DCCL_BENCH_NO_COLLECTIVE", "0") != "1":
+        # DCCL_BENCH_AR_TRANSPORTS=direct with the gloo backend rehearses the direct path with several
+        # processes on one GPU (RCCL refuses two ranks on one device)
+        rehearse = backend == "gloo" and os.environ.get("DCCL_BENCH_AR_TRANSPORTS") == "direct"
+        if (backend == "nccl" or rehearse) and os.environ.get("DCCL_BENCH_NO_COLLECTIVE", "0") != "1":
             count = (256 << 20) // 4 // world * world
-            ar_res, finished = run_with_watchdog(lambda: dccl_allreduce_rccl(world, rank, dev, count), 180.0)
-            extra["dccl_allreduce_rccl"] = ar_res
+            ar_res, finished = run_with_watchdog(lambda: dccl_allreduce_multi(world, rank, dev, count), 240.0)
+            extra["dccl_allreduce"] = ar_res
             if not finished:
-                extra["dccl_allreduce_rccl"]["abandoned"] = True
+                extra["dccl_allreduce"]["abandoned"] = True
 
     if rank == 0:
         traffic = None
@@ -409,7 +432,7 @@ def main():
         if world == 1 and not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(res), flush=True)
-    ar = extra.get("dccl_allreduce_rccl", {})
+    ar = extra.get("dccl_allreduce", {})
     if ar.get("abandoned") or "error" in ar:
         os._exit(0)  # a rank may be stuck inside RCCL: never wait for it at teardown
     if world > 1:

@@ -14,7 +14,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_dccl_allreduce_rccl_world1():
+def test_dccl_allreduce_world1(monkeypatch):
     import torch
     import torch.distributed as dist
 
@@ -24,12 +24,16 @@ def test_dccl_allreduce_rccl_world1():
         pytest.skip("librccl not loadable")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1, device_id=dev)
+    port = _port()
+    monkeypatch.setenv("DCCL_BOOTSTRAP_TAG", f"bench_test_{port}")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
     try:
-        res, finished = bench.run_with_watchdog(lambda: bench.dccl_allreduce_rccl(1, 0, dev, 1 << 20, iters=2), 120)
+        res, finished = bench.run_with_watchdog(lambda: bench.dccl_allreduce_multi(1, 0, dev, 1 << 20, iters=2), 120)
         assert finished, res
         assert "error" not in res, res
-        assert res["int32_sum_bit_exact_vs_rccl"] and res["fp32_within_bound"]
+        for name in ("ring", "direct"):
+            assert res[name]["int32_sum_bit_exact_vs_rccl"] and res[name]["fp32_within_bound"], res
+        assert res["fp32_direct_bit_exact_vs_ring"], res
     finally:
         dist.destroy_process_group()
 
@@ -40,3 +44,25 @@ def test_watchdog_reports_timeout():
     import bench
     res, finished = bench.run_with_watchdog(lambda: time.sleep(5), 0.2)
     assert not finished and "timed out" in res["error"]
+
+
+def test_bench_direct_allreduce_two_processes_one_gpu():
+    """bench.py's N>1 path rehearsed with two ranks on the box's one GPU: gloo for torch.distributed,
+    the direct IPC all-reduce between the two processes checked against gloo's all_reduce."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {**os.environ, "DCCL_BENCH_BACKEND": "gloo", "DCCL_BENCH_AR_TRANSPORTS": "direct",
+           "DCCL_BOOTSTRAP_TAG": f"bench_rehearsal_{_port()}"}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--mib", "64", "--no-cpu", "--no-host-staged"]
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, p.stdout[-3000:]
+    res = json.loads(lines[0])
+    ar = res["dccl_allreduce"]
+    assert "error" not in ar, ar
+    assert ar["direct"]["int32_sum_bit_exact_vs_rccl"] and ar["direct"]["fp32_within_bound"], ar
