@@ -109,6 +109,43 @@ def time_kernel(ps: int, pr: int, dt: int, n: int, op: int, stream, steps: int) 
     return ev0.elapsed_time(ev1) / steps
 
 
+_NATIVE_CHILD = r"""
+import json, sys, time
+sys.path.insert(0, sys.argv[1])
+import oracle
+n, budget = int(sys.argv[2]), float(sys.argv[3])
+nat = oracle.reference_native()
+if nat is None:
+    print(json.dumps(None)); sys.exit(0)
+s = oracle.synth(n, 7, 0, 0xDCC1, 0); r = oracle.synth(n, 7, 0, 0xDCC1, 1)
+nat.ref_host_reduce(s.ctypes.data, r.ctypes.data, n, 7, 0)
+reps, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < budget:
+    nat.ref_host_reduce(s.ctypes.data, r.ctypes.data, n, 7, 0); reps += 1
+print(json.dumps({"seconds_per_pass": (time.perf_counter() - t0) / reps, "passes": reps}))
+"""
+
+
+def native_variant(budget_s: float, n: int) -> dict | None:
+    """The reference loop with its Benchmark flags (-Ofast -march=native, CMakeLists.txt:26), a labelled
+    variant.  It was compiled for the build container's CPU, so it runs in a child process: an
+    instruction the box's CPU lacks ends the child, not the bench."""
+    import subprocess
+    try:
+        p = subprocess.run([sys.executable, "-c", _NATIVE_CHILD, ROOT, str(n), str(budget_s)],
+                           capture_output=True, text=True, timeout=budget_s + 60)
+        if p.returncode != 0:
+            return {"error": f"child exited with {p.returncode}"}
+        res = json.loads(p.stdout.strip().splitlines()[-1])
+    except Exception as e:  # reported, never fatal
+        return {"error": repr(e)}
+    if res is None:
+        return None
+    t = res["seconds_per_pass"]
+    return {"value": round(3 * n * 4 / t / GIB, 2), "payload_gib_s": round(n * 4 / t / GIB, 2), "cores": 1,
+            "passes": res["passes"], "flags": "-Ofast -march=native (reference Benchmark build, build-container CPU)"}
+
+
 def cpu_baseline(budget_s: float) -> dict | None:
     """Reference CPU loop (oracle/_ref) single-threaded, plus all host threads, fp32 Sum."""
     try:
@@ -120,17 +157,16 @@ def cpu_baseline(budget_s: float) -> dict | None:
     fn = (lambda s, r, n: ref.ref_host_reduce(s, r, n, 7, 0)) if ref is not None else \
         (lambda s, r, n: oracle.restatement().oracle_host_reduce(s, r, n, 7, 0))
     n = (256 << 20) // 4  # 256 MiB per operand sample (BASELINE config C2 size)
-    s = oracle.aligned_empty(n, np.float32)
-    r = oracle.aligned_empty(n, np.float32)
-    s[:] = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32)
-    r[:] = 0
+    s = oracle.synth(n, 7, 0, SEED, 0)  # the same counter-based operands as the device run
+    r = oracle.synth(n, 7, 0, SEED, 1)
     ps, pr = s.ctypes.data, r.ctypes.data
     fn(ps, pr, n)  # page in
     reps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s * 0.6:
+    while time.perf_counter() - t0 < budget_s * 0.45:
         fn(ps, pr, n)
         reps += 1
     t1 = (time.perf_counter() - t0) / reps
+    native = native_variant(budget_s * 0.2, n)
     # the box's CPU share (OMP_NUM_THREADS; 16 per GPU on the pool): 64-B aligned contiguous
     # slices, one persistent thread each (ctypes drops the GIL during the call)
     nthr = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
@@ -144,7 +180,7 @@ def cpu_baseline(budget_s: float) -> dict | None:
     with ThreadPoolExecutor(max_workers=nthr) as pool:
         list(pool.map(work, bounds))  # warm the threads
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < budget_s * 0.4 or reps_mt == 0:
+        while time.perf_counter() - t0 < budget_s * 0.35 or reps_mt == 0:
             list(pool.map(work, bounds))
             reps_mt += 1
         tmt = (time.perf_counter() - t0) / reps_mt
@@ -160,11 +196,12 @@ def cpu_baseline(budget_s: float) -> dict | None:
     return {
         "value": round(3 * nbytes / t1 / GIB, 2), "unit": "GiB/s (HBM-traffic basis 3*N*4 B, fp32 Sum)",
         "cores": 1, "kind": kind,
-        "sample": f"fp32 Sum, 256 MiB per operand host buffers (64-B aligned), {reps} passes in "
-                  f"{t1 * reps:.1f}s, Release flags -O3 -mprefer-vector-width=512",
+        "sample": f"fp32 Sum, 256 MiB per operand host buffers (64-B aligned, splitmix64 operands, seed 0xDCC1), "
+                  f"{reps} passes in {t1 * reps:.1f}s, Release flags -O3 -mprefer-vector-width=512",
         "payload_gib_s": round(nbytes / t1 / GIB, 2),
         "all_cores": {"value": round(3 * nbytes / tmt / GIB, 2), "cores": nthr, "passes": reps_mt,
                       "payload_gib_s": round(nbytes / tmt / GIB, 2)},
+        "native_flags_variant": native,
         "cpu_model": cpu_model,
     }
 

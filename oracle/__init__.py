@@ -21,6 +21,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 _RESTATEMENT = os.path.join(HERE, "liboracle_host_reduce.so")
 _REFERENCE = os.path.join(HERE, "_ref", "libref_host_reduce.so")
+_REFERENCE_NATIVE = os.path.join(HERE, "_ref", "libref_host_reduce_native.so")
 
 # ncclDataType_t -> numpy dtype (fp16 / bf16 travel as raw uint16 bit patterns)
 NP_DTYPES = {
@@ -71,6 +72,14 @@ def reference():
     if "ref" not in _cache:
         _cache["ref"] = _bind(_REFERENCE, ["ref_host_reduce"]) if os.path.exists(_REFERENCE) else None
     return _cache["ref"]
+
+
+def reference_native():
+    """The reference loop built with its Benchmark flags (-Ofast -march=native), or None."""
+    if "ref_native" not in _cache:
+        _cache["ref_native"] = (_bind(_REFERENCE_NATIVE, ["ref_host_reduce"])
+                                if os.path.exists(_REFERENCE_NATIVE) else None)
+    return _cache["ref_native"]
 
 
 def _ptr(a: np.ndarray) -> int:
