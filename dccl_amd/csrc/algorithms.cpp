@@ -102,4 +102,122 @@ ncclResult_t all_reduce_ring(dccl::dcclComm* c, void* buffer, void* scratch, siz
                            [W](uint32_t x) { return (x + W - 1) % W; });
 }
 
+// ------------------------------------------------------------------------------------------
+// Rabenseifner all-reduce (DCCL_ALLREDUCE_ALGORITHM=rabenseifner):
+//   /root/reference/src/core/all_reduce_recursive_halving_and_doubling.cpp:8-201
+//   /root/reference/src/core/reduce_scatter_recursive_halving.cpp:12-116
+//   /root/reference/src/core/all_gather_recursive_doubling.cpp:12-92
+// Same fold of a non-power-of-two world onto 2^k ranks, same halving order and the same
+// op(recv = own part, send = peer's part) at every step, so every reduced block is bit-identical to
+// the reference's.  One deliberate fix: the reference's recursive-doubling all-gather sends one slice
+// per step (its step_bsize doubling sits inside a comment, all_gather_recursive_doubling.cpp:85), so
+// with a subworld of 4 or more ranks some blocks never arrive; here step s moves 2^s slices and every
+// rank ends with the whole result.
+// ------------------------------------------------------------------------------------------
+namespace {
+
+inline uint32_t floor_log2(uint32_t n) {
+    uint32_t k = 0;
+    while ((n >> (k + 1)) != 0) ++k;
+    return k;
+}
+
+inline uint32_t reverse_low_bits(uint32_t x, uint32_t nbits) {
+    uint32_t r = 0;
+    for (uint32_t b = 0; b < nbits; ++b) r = (r << 1) | ((x >> b) & 1u);
+    return r;
+}
+
+// Send [sbuf, sbytes) to `peer` (skipped if sbuf is null) and receive `rbytes` from it into rbuf
+// (skipped if rbuf is null).
+ncclResult_t swap(dccl::dcclComm* c, uint32_t peer, const void* sbuf, size_t sbytes, void* rbuf, size_t rbytes,
+                  bool device, hipStream_t st) {
+    if (c->rccl != nullptr)
+        return static_cast<ncclResult_t>(rccl_exchange(c->rccl, sbuf, sbytes, peer, rbuf, rbytes, peer, st));
+    ncclResult_t rc = dccl::ncclSuccess;
+    if (sbuf != nullptr) rc = xport_send(c, peer, sbuf, sbytes, device, st);
+    if (rc == dccl::ncclSuccess && rbuf != nullptr) rc = xport_recv(c, peer, rbuf, rbytes, device, st);
+    if (sbuf != nullptr) {
+        const ncclResult_t rw = xport_wait_send(c, peer, device, st);
+        if (rc == dccl::ncclSuccess) rc = rw;
+    }
+    return rc;
+}
+
+// Send [sbuf, elems) to `peer` and combine what it sends into dst: dst = op(dst, peer's part).
+ncclResult_t swap_combine(dccl::dcclComm* c, uint32_t peer, const void* sbuf, void* dst, size_t elems, int dtype,
+                          int op, void* scratch, bool device, hipStream_t st) {
+    const size_t bytes = elems * size_of_dtype(dtype);
+    if (c->rccl != nullptr) {
+        ncclResult_t rc = ensure_scratch(c, bytes, true);
+        if (rc == dccl::ncclSuccess)
+            rc = static_cast<ncclResult_t>(rccl_exchange(c->rccl, sbuf, bytes, peer, c->dev_scratch, bytes, peer, st));
+        return rc == dccl::ncclSuccess ? combine(c->dev_scratch, dst, dtype, elems, op, true, st) : rc;
+    }
+    ncclResult_t rc = xport_send(c, peer, sbuf, bytes, device, st);
+    if (rc == dccl::ncclSuccess) {
+        if (scratch != nullptr) {  // the reference's shape: land in the scratchpad, then combine
+            rc = xport_recv(c, peer, scratch, bytes, device, st);
+            if (rc == dccl::ncclSuccess) rc = combine(scratch, dst, dtype, elems, op, device, st);
+        } else {
+            rc = xport_recv_combine(c, peer, dst, elems, dtype, op, device, st);
+        }
+    }
+    const ncclResult_t rw = xport_wait_send(c, peer, device, st);
+    return rc == dccl::ncclSuccess ? rw : rc;
+}
+
+}  // namespace
+
+ncclResult_t all_reduce_rabenseifner(dccl::dcclComm* c, void* buffer, void* scratch, size_t count, int dtype, int op,
+                                     bool device, hipStream_t st) {
+    const uint32_t W = c->world, me = c->rank;
+    const uint32_t k = floor_log2(W), sub = 1u << k, rem = W - sub;
+    if (count % sub) return dccl::ncclInvalidArgument;  // all_reduce_recursive_halving_and_doubling.cpp:50-54
+    if (W == 1) return dccl::ncclSuccess;
+    const size_t esz = size_of_dtype(dtype), total = count * esz, half = total / 2;
+    auto* base = static_cast<unsigned char*>(buffer);
+    // fold: ranks below 2*rem pair up as (leader 2i, follower 2i+1) -> new rank i; the rest shift down
+    auto to_new = [rem](uint32_t o) { return o < 2 * rem ? o / 2 : o - rem; };
+    auto to_old = [rem](uint32_t n) { return n < rem ? n * 2 : n + rem; };
+    const bool leader = me < 2 * rem && me % 2 == 0, follower = me < 2 * rem && me % 2 == 1;
+    ncclResult_t rc = dccl::ncclSuccess;
+    if (leader) {  // keep the first half: first = op(mine, follower's); get the second half back reduced
+        rc = swap_combine(c, me + 1, base + half, base, count / 2, dtype, op, scratch, device, st);
+        if (rc == dccl::ncclSuccess) rc = swap(c, me + 1, nullptr, 0, base + half, half, device, st);
+    } else if (follower) {  // reduce the second half: second = op(mine, leader's); hand it to the leader
+        rc = swap_combine(c, me - 1, base, base + half, count / 2, dtype, op, scratch, device, st);
+        if (rc == dccl::ncclSuccess) rc = swap(c, me - 1, base + half, half, nullptr, 0, device, st);
+    }
+    if (rc != dccl::ncclSuccess) return rc;
+    if (!follower) {
+        const uint32_t my = to_new(me);
+        // recursive halving reduce-scatter (reduce_scatter_recursive_halving.cpp:68-110)
+        unsigned char* region = base;
+        size_t bytes = total;
+        for (uint32_t s = 0; s < k && rc == dccl::ncclSuccess; ++s) {
+            const uint32_t peer = to_old(my ^ (1u << s));
+            bytes /= 2;
+            unsigned char* keep = ((my >> s) & 1u) ? region + bytes : region;
+            unsigned char* give = ((my >> s) & 1u) ? region : region + bytes;
+            rc = swap_combine(c, peer, give, keep, bytes / esz, dtype, op, scratch, device, st);
+            region = keep;
+        }
+        // recursive doubling all-gather (all_gather_recursive_doubling.cpp:48-76), 2^s slices at step s
+        const size_t slice = total / sub;
+        uint32_t block = reverse_low_bits(my, k);
+        for (uint32_t s = 0; s < k && rc == dccl::ncclSuccess; ++s) {
+            const uint32_t peer = to_old(my ^ (1u << (k - s - 1)));
+            block &= ~((1u << s) - 1u);
+            const uint32_t rblock = block ^ (1u << s);
+            const size_t len = slice << s;
+            rc = swap(c, peer, base + size_t(block) * slice, len, base + size_t(rblock) * slice, len, device, st);
+        }
+    }
+    if (rc != dccl::ncclSuccess) return rc;
+    if (leader) return swap(c, me + 1, base, total, nullptr, 0, device, st);  // :182-188
+    if (follower) return swap(c, me - 1, nullptr, 0, base, total, device, st);  // :189-195
+    return dccl::ncclSuccess;
+}
+
 }  // namespace dccl_amd

@@ -17,5 +17,8 @@ ncclResult_t all_gather_ring(dccl::dcclComm* c, void* buffer, size_t slot_elems,
                              hipStream_t st, const RankMap& to_new, const RankMap& to_old);
 ncclResult_t all_reduce_ring(dccl::dcclComm* c, void* buffer, void* scratch, size_t count, int dtype, int op,
                              bool device, hipStream_t st);
+// DCCL_ALLREDUCE_ALGORITHM=rabenseifner: fold to 2^k ranks, recursive halving RS, recursive doubling AG.
+ncclResult_t all_reduce_rabenseifner(dccl::dcclComm* c, void* buffer, void* scratch, size_t count, int dtype, int op,
+                                     bool device, hipStream_t st);
 
 }  // namespace dccl_amd

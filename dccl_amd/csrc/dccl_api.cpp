@@ -217,6 +217,25 @@ bool ipc_requested() {
     return t != nullptr && std::string(t) == "ipc";
 }
 
+enum class Algorithm { kRing, kRabenseifner, kDirect, kUnknown };
+
+// DCCL_ALLREDUCE_ALGORITHM (the reference's DCCL/allreduce_algorithm key, dccl.hpp:38-46): ring
+// (default), rabenseifner, or direct.  The reference silently skips the reduction for any other
+// value (dccl.cpp:412-501); here it is ncclInvalidUsage.
+Algorithm allreduce_algorithm() {
+    const char* a = std::getenv(DCCL_ALLREDUCE_ALGORITHM_CONFSTR);
+    if (a == nullptr || *a == 0 || std::string(a) == DCCL_ALLREDUCE_RING) return Algorithm::kRing;
+    if (std::string(a) == DCCL_ALLREDUCE_RABENSEIFNER) return Algorithm::kRabenseifner;
+    if (std::string(a) == "direct") return Algorithm::kDirect;
+    return Algorithm::kUnknown;
+}
+
+uint32_t floor_log2_u32(uint32_t n) {
+    uint32_t k = 0;
+    while ((n >> (k + 1)) != 0) ++k;
+    return k;
+}
+
 // Cross-process transports move device memory only.
 bool cross_process(const dcclComm* c) { return c->rccl != nullptr || c->ipc != nullptr; }
 
@@ -340,12 +359,21 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
     if (cross_process(comm) && !dev) return ncclInvalidUsage;  // the cross-process transports move device memory
     const size_t total = count * size_of_dtype(datatype);
     const uint32_t W = comm->world;
-    if (W > 1 && (count < W || count % W)) return ncclInvalidArgument;
+    const Algorithm algo = allreduce_algorithm();  // dccl.cpp:412-413,454
+    if (algo == Algorithm::kUnknown) return ncclInvalidUsage;
+    if (algo == Algorithm::kRabenseifner && comm->ipc != nullptr) return ncclInvalidUsage;
+    if (W > 1 && algo == Algorithm::kRabenseifner && count % (1u << floor_log2_u32(W)))
+        return ncclInvalidArgument;  // all_reduce_recursive_halving_and_doubling.cpp:50-54
+    if (W > 1 && algo != Algorithm::kRabenseifner && (count < W || count % W)) return ncclInvalidArgument;
     if (W > 1 && dev && direct_selected(comm))
         return direct_all_reduce(comm, sendbuff, recvbuff, count, datatype, op, stream);
     if ((rc = copy_bytes(recvbuff, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:393-408
     if (W == 1) return ncclSuccess;
     void* scratch = nullptr;
+    if (algo == Algorithm::kRabenseifner) {  // scratchpad of half the buffer (dccl.cpp:458-466)
+        if ((rc = ring_scratch(comm, total / 2, dev, &scratch)) != ncclSuccess) return rc;
+        return all_reduce_rabenseifner(comm, recvbuff, scratch, count, datatype, op, dev, stream);
+    }
     if ((rc = ring_scratch(comm, total / W, dev, &scratch)) != ncclSuccess) return rc;
     return all_reduce_ring(comm, recvbuff, scratch, count, datatype, op, dev, stream);
 }

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import oracle
-from tests import ringsim
+from tests import rabsim, ringsim
 from tests.test_oracle import GOLDEN
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -53,7 +53,7 @@ def inputs(W, n, dtype, device):
     return sends, recvs
 
 
-def expected(api, W, n, dtype, op, device, repeat=1, faithful=False):
+def expected(api, W, n, dtype, op, device, repeat=1, faithful=False, algo="ring"):
     """What the API must leave in each rank's buffer.
 
     faithful=False combines with the intended semantics (oracle.expected_reduce): the build's
@@ -71,7 +71,9 @@ def expected(api, W, n, dtype, op, device, repeat=1, faithful=False):
 
     slot = n // W
     for _ in range(repeat):
-        if api == "all_reduce":
+        if api == "all_reduce" and algo == "rabenseifner":
+            rabsim.rabenseifner_allreduce(sends, combine, faithful=faithful)
+        elif api == "all_reduce":
             ringsim.ring_allreduce(sends, combine, copy)
         elif api == "reduce_scatter":
             work = [s.copy() for s in sends]
@@ -101,7 +103,7 @@ def check_api(api, W, n, dtype, op, gpu_flag, device, env=None):
                             env=env)
     assert rc == 0, err
     assert len(rows) == W
-    want = expected(api, W, n, dtype, op, device)
+    want = expected(api, W, n, dtype, op, device, algo=(env or {}).get("DCCL_ALLREDUCE_ALGORITHM", "ring"))
     for r, row in enumerate(rows):
         assert row["rc"] == 0
         assert int(row["fnv1a"], 16) == fnv1a(want[r].tobytes()), (api, r, row)
@@ -150,6 +152,27 @@ def test_cli_rejects_uneven_count_cpu():
     assert rc == 2 and all(r["rc"] == 4 for r in rows)
 
 
+def test_rabenseifner_simulation_cpu():
+    """The restated Rabenseifner (tests/rabsim.py) reduces correctly for every world size once its
+    all-gather moves 2^s slices per step; the reference's one-slice all-gather leaves blocks undelivered
+    for subworlds of 4+ ranks (W >= 4) and agrees with the fixed one below that."""
+    rng = np.random.default_rng(5)
+    for W in range(1, 10):
+        n = 8 * 37
+        xs = [rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32) for _ in range(W)]
+
+        def combine(s, r):
+            assert oracle.expected_reduce(np.ascontiguousarray(s), r, 2, 0) == 0
+
+        fixed = rabsim.rabenseifner_allreduce([x.copy() for x in xs], combine)
+        faithful = rabsim.rabenseifner_allreduce([x.copy() for x in xs], combine, faithful=True)
+        want = np.sum(np.stack(xs).astype(np.int64), axis=0).astype(np.int32)  # wrapping sum, order-free
+        for r in range(W):
+            assert np.array_equal(fixed[r], want), (W, r)
+        same = all(np.array_equal(a, b) for a, b in zip(fixed, faithful))
+        assert same == (W < 4), W
+
+
 # ------------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @pytest.mark.parametrize("gpu_flag,algo", [(-1, "ring"), (0, "ring"), (0, "direct")])
@@ -166,6 +189,25 @@ def test_c1_known_answers(gpu_flag, algo, kind):
             assert row["uniform"] and int(row["first"], 16) == int(g[kind][reps], 16), (reps, row)
         if reps == "1000":
             print("C1", algo, "latency us/call", [row["us_per_call"] for row in rows])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scratch", ["0", "1"])
+@pytest.mark.parametrize("gpu_flag,device", [(-1, False), (0, True)])
+def test_cli_rabenseifner_against_simulation(gpu_flag, device, scratch):
+    """DCCL_ALLREDUCE_ALGORITHM=rabenseifner: every reduced block bit-exact against the restated
+    reference algorithm + oracle (with the all-gather fix), for folded and power-of-two worlds."""
+    env = {"DCCL_ALLREDUCE_ALGORITHM": "rabenseifner", "DCCL_RS_SCRATCH": scratch}
+    for W, n, dtype, op in [(2, 1024, "float32", 0), (3, 3 * 1000, "float64", 1), (4, 4096, "int8", 2),
+                            (5, 8 * 513, "bfloat16", 3), (6, 6 * 1024, "uint64", 0), (7, 4 * 4099, "float16", 2),
+                            (8, 8 * 4096, "float32", 0), (8, 8 * 77, "int32", 1)]:
+        check_api("all_reduce", W, n, dtype, op, gpu_flag, device, env=env)
+
+
+def test_cli_unknown_algorithm_rejected_cpu():
+    rc, rows, _ = run_cli("-a", "all_reduce", "-t", "uint32", "-c", 1024, "-n", 2, "-r", 1, "-g", -1,
+                          env={"DCCL_ALLREDUCE_ALGORITHM": "binary_blocks"})
+    assert rc == 2 and all(r["rc"] == 5 for r in rows)
 
 
 @pytest.mark.gpu
