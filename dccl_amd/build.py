@@ -23,6 +23,8 @@ LIB = os.path.join(OUT_DIR, "libdccl_amd.so")
 BIN_DIR = os.path.join(PKG, "bin")
 CLI_SRC = os.path.join(ROOT, "tools", "dccl_cli.cpp")
 CLI = os.path.join(BIN_DIR, "dccl_cli")
+C_CHECK_SRC = os.path.join(ROOT, "tools", "c_abi_check.c")
+C_CHECK = os.path.join(BIN_DIR, "c_abi_check")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DCCL_OFFLOAD_ARCH", "gfx950")
 
@@ -73,6 +75,12 @@ def build(force: bool = False) -> str:
                                                                           os.path.getmtime(CLI_SRC)):
         subprocess.run([HIPCC, *COMMON, CLI_SRC, "-o", CLI, f"-L{OUT_DIR}", "-ldccl_amd",
                         "-Wl,-rpath,$ORIGIN/../lib", "-pthread"], check=True)
+    # a plain C11 consumer of the C-ABI headers (gcc, no C++ / HIP headers)
+    if force or not os.path.exists(C_CHECK) or os.path.getmtime(C_CHECK) < max(
+            [os.path.getmtime(LIB), os.path.getmtime(C_CHECK_SRC)] + [os.path.getmtime(h) for h in _headers()]):
+        subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-pedantic", "-Werror",
+                        f"-I{os.path.join(ROOT, 'include')}", C_CHECK_SRC, "-o", C_CHECK, f"-L{OUT_DIR}",
+                        "-ldccl_amd", "-Wl,-rpath,$ORIGIN/../lib"], check=True)
     return LIB
 
 

@@ -77,3 +77,23 @@ def test_enum_values_match_reference_header():
     for name, val in [("ncclFloat32", 7), ("ncclBfloat16", 9), ("ncclAvg", 4), ("ncclInvalidArgument", 4),
                       ("ncclUnhandledCudaError", 1), ("ncclMin", 3)]:
         assert re.search(rf"\b{name}\s*=\s*{val}\b", hpp), name
+
+
+def _c_check_binary():
+    path = os.path.join(ROOT, "dccl_amd", "bin", "c_abi_check")
+    if not os.path.exists(path):
+        pytest.skip("c_abi_check not built (python dccl_amd/build.py)")
+    return path
+
+
+def test_plain_c_consumer_cpu():
+    """tools/c_abi_check.c: the headers compile as C11 with -pedantic -Werror, the library links from C,
+    and the validation contract answers from C without a GPU."""
+    p = subprocess.run([_c_check_binary()], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "ok" in p.stdout, p.stdout + p.stderr
+
+
+@pytest.mark.gpu
+def test_plain_c_consumer_gpu(gpu):
+    p = subprocess.run([_c_check_binary(), "gpu"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "ok" in p.stdout, p.stdout + p.stderr
