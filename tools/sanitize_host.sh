@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Build the host-side C++ (transport, ring algorithms, API, host staging, CLI) with a host
+# Build the host-side C++ (transports, ring / direct algorithms, API, host staging, CLI) with a host
 # sanitizer and drive the CPU-runnable collective paths (host buffers, no combine: all_gather,
 # broadcast, world-size-1 all_reduce) through dccl_cli with 2-8 thread-ranks.
 #   tools/sanitize_host.sh thread|address|undefined
@@ -12,7 +12,7 @@ mkdir -p "$out"
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 flags=(-std=c++17 -O1 -g -fPIC "-Xarch_host" "-fsanitize=$kind" -I"$root/include" -I"$root/dccl_amd/csrc" --offload-arch=gfx950)
 objs=()
-for f in comm algorithms dccl_api host_staged rccl_transport; do
+for f in comm algorithms dccl_api direct host_staged rccl_transport; do
   "$HIPCC" "${flags[@]}" -c "$root/dccl_amd/csrc/$f.cpp" -o "$out/$f.o"
   objs+=("$out/$f.o")
 done
