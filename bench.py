@@ -23,7 +23,8 @@ Extra keys: payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident o
 rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately),
 dccl_allreduce (N>1: the namespace-dccl ncclAllReduce over the RCCL p2p ring and over the direct
 IPC peer-read transport, checked against each other and RCCL's own all_reduce, timed beside it;
-under a watchdog).
+in a child process per rank, so a fault or hang there cannot take the bench line with it).
+Progress goes to stderr, one line per phase.
 """
 from __future__ import annotations
 
@@ -320,7 +321,72 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
     return out
 
 
+def progress(msg: str) -> None:
+    """One line on stderr per phase, so a long multi-GPU run is never silent (the JSON line is stdout)."""
+    print(f"[bench] rank {os.environ.get('RANK', '0')}: {msg}", file=sys.stderr, flush=True)
+
+
+CHILD_TIMEOUT_S = 150.0
+
+
+def collective_in_child(world: int, rank: int, local: int, backend: str) -> dict:
+    """Run dccl_allreduce_multi in a child process per rank, with its own process group on a fresh port.
+    The namespace-dccl collectives (RCCL p2p ring, IPC peer reads) are reported extras, never `value`: a
+    fault or hang inside them ends the child, which is killed after CHILD_TIMEOUT_S, while this process,
+    its measurement and the JSON line survive.  Every parent waits at most that long and joins no
+    collective of the child, so no rank can be left behind."""
+    import socket
+    import subprocess
+    port = [0]
+    if rank == 0:
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port[0] = sk.getsockname()[1]
+    dist.broadcast_object_list(port, src=0)
+    env = {**os.environ, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port[0]), "RANK": str(rank),
+           "WORLD_SIZE": str(world), "LOCAL_RANK": str(local), "DCCL_BENCH_BACKEND": backend,
+           "DCCL_BOOTSTRAP_TAG": f"bench_child_{port[0]}"}
+    torch.cuda.synchronize()
+    progress(f"namespace-dccl all_reduce extras in a child process (port {port[0]})")
+    t0 = time.perf_counter()
+    try:
+        p = subprocess.run([sys.executable, os.path.abspath(__file__), "--collective-child"], env=env,
+                           stdout=subprocess.PIPE, stderr=None, text=True, timeout=CHILD_TIMEOUT_S)
+    except subprocess.TimeoutExpired:
+        return {"error": f"child timed out after {CHILD_TIMEOUT_S:.0f}s and was killed"}
+    progress(f"child exited with {p.returncode} after {time.perf_counter() - t0:.1f}s")
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    res = json.loads(lines[-1]) if lines else {}
+    if p.returncode != 0:
+        res = {**res, "error": res.get("error", f"child exited with {p.returncode}")}
+    return res
+
+
+def collective_child() -> None:
+    """Entry point of the child process started by collective_in_child."""
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    backend = os.environ.get("DCCL_BENCH_BACKEND", "nccl")
+    local = int(os.environ["LOCAL_RANK"]) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(backend)
+    count = (256 << 20) // 4 // world * world
+    res, finished = run_with_watchdog(lambda: dccl_allreduce_multi(world, rank, dev, count), CHILD_TIMEOUT_S - 30)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if not finished or "error" in res:
+        os._exit(3)  # a rank may be stuck inside a collective: never wait for it at teardown
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
+    if "--collective-child" in sys.argv:
+        collective_child()
+        return
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -351,6 +417,7 @@ def main():
         total_bytes = world * n * esz
     nbytes = n * esz
 
+    progress(f"world {world}, backend {backend}, {nbytes >> 20} MiB per operand on {dev}")
     send, recv = operand_pair(n, dt, op, 2 * rank, dev, a.layout)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
@@ -388,6 +455,7 @@ def main():
     else:
         kern_ms_max = kern_ms
     ms_per_step = elapsed / a.steps * 1e3
+    progress(f"timed region done: {ms_per_step:.4f} ms per step, kernel {kern_ms:.4f} ms")
 
     extra = {}
     # the other operand layout, timed briefly on every rank (reported, never in `value`)
@@ -421,15 +489,14 @@ def main():
                               "note": "RCCL all_gather_into_tensor of the reduced shards over xGMI "
                                       "(every GPU ends with the full result); not in value"}
         del gathered, src
+        progress(f"all-gather done: {tag * 1e3:.3f} ms")
         # DCCL_BENCH_AR_TRANSPORTS=direct with the gloo backend rehearses the direct path with several
         # processes on one GPU (RCCL refuses two ranks on one device)
         rehearse = backend == "gloo" and os.environ.get("DCCL_BENCH_AR_TRANSPORTS") == "direct"
         if (backend == "nccl" or rehearse) and os.environ.get("DCCL_BENCH_NO_COLLECTIVE", "0") != "1":
-            count = (256 << 20) // 4 // world * world
-            ar_res, finished = run_with_watchdog(lambda: dccl_allreduce_multi(world, rank, dev, count), 240.0)
-            extra["dccl_allreduce"] = ar_res
-            if not finished:
-                extra["dccl_allreduce"]["abandoned"] = True
+            del send, recv, s2, r2
+            torch.cuda.empty_cache()
+            extra["dccl_allreduce"] = collective_in_child(world, rank, local, backend)
 
     if rank == 0:
         traffic = None
@@ -469,9 +536,6 @@ def main():
         if world == 1 and not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(res), flush=True)
-    ar = extra.get("dccl_allreduce", {})
-    if ar.get("abandoned") or "error" in ar:
-        os._exit(0)  # a rank may be stuck inside RCCL: never wait for it at teardown
     if world > 1:
         try:
             dist.barrier()

@@ -8,7 +8,7 @@ out=gpurun_out/${TAG:-r1}
 mkdir -p "$out"
 export TMPDIR=/tmp
 echo "== pytest -m gpu"
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$out/pytest_gpu.log" 2>&1 || { tail -60 "$out/pytest_gpu.log"; exit 1; }
+timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -p no:cacheprovider > "$out/pytest_gpu.log" 2>&1 || { tail -60 "$out/pytest_gpu.log"; exit 1; }
 tail -3 "$out/pytest_gpu.log"
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
