@@ -343,7 +343,10 @@ def collective_in_child(world: int, rank: int, local: int, backend: str) -> dict
             sk.bind(("127.0.0.1", 0))
             port[0] = sk.getsockname()[1]
     dist.broadcast_object_list(port, src=0)
-    env = {**os.environ, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port[0]), "RANK": str(rank),
+    # not the launcher's agent store (torchrun exports TORCHELASTIC_USE_AGENT_STORE): the child's rank 0
+    # hosts its own store on the fresh port
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env = {**env, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port[0]), "RANK": str(rank),
            "WORLD_SIZE": str(world), "LOCAL_RANK": str(local), "DCCL_BENCH_BACKEND": backend,
            "DCCL_BOOTSTRAP_TAG": f"bench_child_{port[0]}"}
     torch.cuda.synchronize()
@@ -369,10 +372,12 @@ def collective_child() -> None:
     local = int(os.environ["LOCAL_RANK"]) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    import datetime
+    limit = datetime.timedelta(seconds=60)
     if backend == "nccl":
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", device_id=dev, timeout=limit)
     else:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, timeout=limit)
     count = (256 << 20) // 4 // world * world
     res, finished = run_with_watchdog(lambda: dccl_allreduce_multi(world, rank, dev, count), CHILD_TIMEOUT_S - 30)
     if rank == 0:

@@ -113,6 +113,7 @@ def _load():
         "dccl_tune_multi_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_size_t,
                                             c_void_p]),
         "dccl_synth_fill": (c_int, [c_void_p, c_int, c_size_t, c_int, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),
+        "dccl_tune_ceiling": (c_int, [c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     })
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -132,7 +133,7 @@ EXPORTED_SYMBOLS = [
     "dccl_comm_init_rank", "dccl_get_unique_id", "dccl_comm_init_rccl", "dccl_comm_finalize", "dccl_all_reduce",
     "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available", "dccl_tune_skew_f32_sum",
     "dccl_synth_fill", "dccl_tune_multi_f32_sum", "dccl_local_reduce_chain", "dccl_copy_multi",
-    "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast",
+    "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_tune_ceiling",
 ]
 
 

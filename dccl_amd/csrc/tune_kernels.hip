@@ -207,3 +207,52 @@ extern "C" int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void
     default: return tune_multi_k<8>(variant, sl, r, sp, st, lds_bytes);
     }
 }
+
+// ---------------------------------------------------------------------------------
+// Tuning only: HBM ceiling probes in the shipped shape (one-wave blocks, one 16-B vector per
+// lane, every access non-temporal), to place the combine's 2-read/1-write mix between the
+// chip's own streaming limits.  kind 0: read send; 1: read send and recv; 2: write recv;
+// 3: copy send -> recv; 4: the combine itself (control).  The read-only kinds fold the loaded
+// vectors into a value that is stored only when `sink` is non-null, which callers never pass,
+// so no byte is written but no load can be elided.
+// ---------------------------------------------------------------------------------
+namespace {
+template <int KIND>
+__global__ __launch_bounds__(64) void tune_ceiling_kernel(const u32x4* __restrict__ s, u32x4* __restrict__ r,
+                                                          size_t nvec, u32x4* __restrict__ sink) {
+    const size_t i = size_t(blockIdx.x) * 64 + threadIdx.x;
+    if (i >= nvec) return;
+    if constexpr (KIND == 0) {
+        const u32x4 a = __builtin_nontemporal_load(s + i);
+        if (sink) sink[i] = a;
+    } else if constexpr (KIND == 1) {
+        const u32x4 a = __builtin_nontemporal_load(s + i);
+        const u32x4 b = __builtin_nontemporal_load(r + i);
+        if (sink) sink[i] = a ^ b;
+    } else if constexpr (KIND == 2) {
+        const uint32_t v = uint32_t(i);
+        __builtin_nontemporal_store(u32x4{v, v, v, v}, r + i);
+    } else if constexpr (KIND == 3) {
+        __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), r + i);
+    } else {
+        const u32x4 a = __builtin_nontemporal_load(s + i);
+        const u32x4 b = __builtin_nontemporal_load(r + i);
+        __builtin_nontemporal_store(combine16<float, kSum>(b, a), r + i);
+    }
+}
+}  // namespace
+
+extern "C" int dccl_tune_ceiling(int kind, const void* send, void* recv, size_t count_f32, void* stream) {
+    if (count_f32 % 256 || ((reinterpret_cast<uintptr_t>(send) | reinterpret_cast<uintptr_t>(recv)) & 15))
+        return DCCL_INVALID_ARGUMENT;
+    const void* fns[] = {reinterpret_cast<const void*>(&tune_ceiling_kernel<0>),
+                         reinterpret_cast<const void*>(&tune_ceiling_kernel<1>),
+                         reinterpret_cast<const void*>(&tune_ceiling_kernel<2>),
+                         reinterpret_cast<const void*>(&tune_ceiling_kernel<3>),
+                         reinterpret_cast<const void*>(&tune_ceiling_kernel<4>)};
+    if (kind < 0 || kind > 4) return DCCL_INVALID_ARGUMENT;
+    size_t nvec = count_f32 / 4;
+    void* sink = nullptr;
+    void* args[] = {&send, &recv, &nvec, &sink};
+    return launch(fns[kind], nvec / 64, args, static_cast<hipStream_t>(stream), 64);
+}

@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Where the combine sits between the chip's own HBM streaming limits (MI355X).
+
+Times, interleaved in one process, the shipped access shape (one-wave blocks, 16 B per lane, all
+non-temporal) doing: read one operand, read both, write one, copy one into the other, and the fp32
+Sum combine (2 reads + 1 write).  Operands are 1 GiB each, carved from one allocation as in bench.py
+(recv, then send 4 KiB past its end).  Reports the bytes each kernel actually moves per second, so
+the combine's rate can be compared with the pure-read and pure-write ceilings of the same shape.
+
+    python tools/ceiling_probe.py [--mib 1024] [--rounds 7] [--iters 20] [--out file]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import dccl_amd  # noqa: E402
+
+KINDS = {0: ("read send", 1), 1: ("read send + recv", 2), 2: ("write recv", 1), 3: ("copy send -> recv", 2),
+         4: ("combine recv += send", 3)}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--mib", type=int, default=1024)
+    p.add_argument("--rounds", type=int, default=7)
+    p.add_argument("--iters", type=int, default=20)
+    p.add_argument("--out", default="")
+    a = p.parse_args()
+    n = (a.mib << 20) // 4
+    pool = torch.empty(2 * n * 4 + 4096, dtype=torch.uint8, device="cuda")
+    recv = pool[: n * 4].view(torch.float32)
+    send = pool[n * 4 + 4096:].view(torch.float32)
+    send.uniform_(-1, 1)
+    recv.uniform_(-1, 1)
+    st = torch.cuda.current_stream().cuda_stream
+    lib = dccl_amd.lib
+    for k in KINDS:
+        assert lib.dccl_tune_ceiling(k, send.data_ptr(), recv.data_ptr(), n, st) == 0, k
+    torch.cuda.synchronize()
+    times = {k: [] for k in KINDS}
+    for _ in range(a.rounds):
+        for k in KINDS:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                lib.dccl_tune_ceiling(k, send.data_ptr(), recv.data_ptr(), n, st)
+            e1.record()
+            e1.synchronize()
+            times[k].append(e0.elapsed_time(e1) / a.iters)
+    rows = []
+    for k, (name, streams) in KINDS.items():
+        med = statistics.median(times[k])
+        moved = streams * n * 4
+        rows.append({"kind": k, "what": name, "bytes_moved": moved, "ms_median": round(med, 4),
+                     "ms_min": round(min(times[k]), 4), "gb_s": round(moved / (med * 1e-3) / 1e9, 1),
+                     "frac_of_8tbs": round(moved / (med * 1e-3) / 8e12, 4)})
+    out = {"mib_per_operand": a.mib, "device": torch.cuda.get_device_name(0), "rows": rows}
+    txt = json.dumps(out, indent=1)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(txt)
+    print(txt)
+
+
+if __name__ == "__main__":
+    main()

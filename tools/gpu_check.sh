@@ -24,6 +24,11 @@ if [[ "${PROF:-1}" != 0 ]]; then
   echo "== pmc WRITE_SIZE"
   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/pmc_write" -o write -- python3 tools/pmc_probe.py > "$out/pmc_write.log" 2>&1
 fi
+if [[ -n "${CEILING:-}" ]]; then
+  echo "== HBM ceiling probes"
+  timeout -k 10 300 python tools/ceiling_probe.py --out "$out/ceiling.json" > "$out/ceiling.log" 2>&1
+  cat "$out/ceiling.log"
+fi
 if [[ -n "${SUITE:-}" ]]; then
   echo "== suite ($SUITE)"
   timeout -k 10 900 python tools/bench_suite.py --parts "$SUITE" --out "$out/suite.json" > "$out/suite.log" 2>&1
