@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-host-staged", action="store_true")
+    p.add_argument("--no-other-layout", action="store_true",
+                   help="skip timing the other operand layout (profiling runs: one layout per kernel average)")
     p.add_argument("--layout", default="pooled", choices=["pooled", "separate"],
                    help="operand placement in HBM (see operand_pair); the other layout is also timed briefly")
     return p.parse_args()
@@ -464,14 +466,15 @@ def main():
 
     extra = {}
     # the other operand layout, timed briefly on every rank (reported, never in `value`)
-    other = "separate" if a.layout == "pooled" else "pooled"
-    del send, recv
-    torch.cuda.empty_cache()
-    s2, r2 = operand_pair(n, dt, op, 2 * rank, dev, other)
-    k2 = time_kernel(s2.data_ptr(), r2.data_ptr(), dt, n, op, stream, max(10, a.steps // 4))
-    extra["other_layout"] = {"layout": other, "kernel_ms_avg": round(k2, 4),
-                             "frac": round(3 * nbytes / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    send, recv = s2, r2  # the all-gather below only needs a reduced shard of the right size
+    if not a.no_other_layout:
+        other = "separate" if a.layout == "pooled" else "pooled"
+        del send, recv
+        torch.cuda.empty_cache()
+        send, recv = operand_pair(n, dt, op, 2 * rank, dev, other)
+        k2 = time_kernel(send.data_ptr(), recv.data_ptr(), dt, n, op, stream, max(10, a.steps // 4))
+        extra["other_layout"] = {"layout": other, "kernel_ms_avg": round(k2, 4),
+                                 "frac": round(3 * nbytes / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    # the all-gather below only needs a reduced shard of the right size
     if world > 1:  # the one exchange step of C5: RCCL all-gather of the reduced shards (separate)
         width = max(b - a_ for a_, b in bounds) if strong else n
         src = recv if width == n else torch.cat([recv, recv.new_zeros(width - n)])
@@ -499,7 +502,7 @@ def main():
         # processes on one GPU (RCCL refuses two ranks on one device)
         rehearse = backend == "gloo" and os.environ.get("DCCL_BENCH_AR_TRANSPORTS") == "direct"
         if (backend == "nccl" or rehearse) and os.environ.get("DCCL_BENCH_NO_COLLECTIVE", "0") != "1":
-            del send, recv, s2, r2
+            del send, recv
             torch.cuda.empty_cache()
             extra["dccl_allreduce"] = collective_in_child(world, rank, local, backend)
 

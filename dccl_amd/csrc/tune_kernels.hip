@@ -209,50 +209,66 @@ extern "C" int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void
 }
 
 // ---------------------------------------------------------------------------------
-// Tuning only: HBM ceiling probes in the shipped shape (one-wave blocks, one 16-B vector per
-// lane, every access non-temporal), to place the combine's 2-read/1-write mix between the
-// chip's own streaming limits.  kind 0: read send; 1: read send and recv; 2: write recv;
-// 3: copy send -> recv; 4: the combine itself (control).  The read-only kinds fold the loaded
-// vectors into a value that is stored only when `sink` is non-null, which callers never pass,
-// so no byte is written but no load can be elided.
+// Tuning only: HBM ceiling probes, to place the combine's 2-read/1-write mix between the chip's
+// own streaming limits.  Shape A = the shipped one (one-wave blocks, one 16-B vector per lane);
+// shape B = 256-thread blocks, 4 vectors per lane (a quarter of the workgroups, the same bytes).
+// Every access is non-temporal.  Loaded values are consumed by an empty asm statement, so no
+// load can be elided and no byte is written.
+//   0 read send (A)          1 read send + recv (A)    2 write recv (A)    3 copy send -> recv (A)
+//   4 the fp32 Sum combine (A, control)                5 read send + recv (B)
+//   6 write recv (B)         7 empty workgroups (A's grid: dispatch cost alone)
+//   8 the combine (A) with the recv load issued before the send load
 // ---------------------------------------------------------------------------------
 namespace {
-template <int KIND>
-__global__ __launch_bounds__(64) void tune_ceiling_kernel(const u32x4* __restrict__ s, u32x4* __restrict__ r,
-                                                          size_t nvec, u32x4* __restrict__ sink) {
-    const size_t i = size_t(blockIdx.x) * 64 + threadIdx.x;
-    if (i >= nvec) return;
-    if constexpr (KIND == 0) {
-        const u32x4 a = __builtin_nontemporal_load(s + i);
-        if (sink) sink[i] = a;
-    } else if constexpr (KIND == 1) {
-        const u32x4 a = __builtin_nontemporal_load(s + i);
-        const u32x4 b = __builtin_nontemporal_load(r + i);
-        if (sink) sink[i] = a ^ b;
-    } else if constexpr (KIND == 2) {
-        const uint32_t v = uint32_t(i);
-        __builtin_nontemporal_store(u32x4{v, v, v, v}, r + i);
-    } else if constexpr (KIND == 3) {
-        __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), r + i);
-    } else {
-        const u32x4 a = __builtin_nontemporal_load(s + i);
-        const u32x4 b = __builtin_nontemporal_load(r + i);
-        __builtin_nontemporal_store(combine16<float, kSum>(b, a), r + i);
+__device__ __forceinline__ void consume(u32x4 v) { asm volatile("" ::"v"(v)); }
+
+template <int KIND, int BLOCK, int U>
+__global__ __launch_bounds__(BLOCK) void tune_ceiling_kernel(const u32x4* __restrict__ s, u32x4* __restrict__ r,
+                                                             size_t nvec) {
+    const size_t base = size_t(blockIdx.x) * BLOCK * U + threadIdx.x;
+    if constexpr (KIND == 7) return;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + size_t(u) * BLOCK;
+        if (i >= nvec) continue;
+        if constexpr (KIND == 0) {
+            consume(__builtin_nontemporal_load(s + i));
+        } else if constexpr (KIND == 1 || KIND == 5) {
+            consume(__builtin_nontemporal_load(s + i));
+            consume(__builtin_nontemporal_load(r + i));
+        } else if constexpr (KIND == 2 || KIND == 6) {
+            const uint32_t v = uint32_t(i);
+            __builtin_nontemporal_store(u32x4{v, v, v, v}, r + i);
+        } else if constexpr (KIND == 3) {
+            __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), r + i);
+        } else if constexpr (KIND == 8) {
+            const u32x4 b = __builtin_nontemporal_load(r + i);
+            const u32x4 a = __builtin_nontemporal_load(s + i);
+            __builtin_nontemporal_store(combine16<float, kSum>(b, a), r + i);
+        } else {
+            const u32x4 a = __builtin_nontemporal_load(s + i);
+            const u32x4 b = __builtin_nontemporal_load(r + i);
+            __builtin_nontemporal_store(combine16<float, kSum>(b, a), r + i);
+        }
     }
+}
+
+struct CeilingEntry { const void* fn; int block, unroll; };
+template <int KIND, int BLOCK, int U>
+CeilingEntry ceiling_entry() {
+    return {reinterpret_cast<const void*>(&tune_ceiling_kernel<KIND, BLOCK, U>), BLOCK, U};
 }
 }  // namespace
 
 extern "C" int dccl_tune_ceiling(int kind, const void* send, void* recv, size_t count_f32, void* stream) {
-    if (count_f32 % 256 || ((reinterpret_cast<uintptr_t>(send) | reinterpret_cast<uintptr_t>(recv)) & 15))
+    if (count_f32 % 4096 || ((reinterpret_cast<uintptr_t>(send) | reinterpret_cast<uintptr_t>(recv)) & 15))
         return DCCL_INVALID_ARGUMENT;
-    const void* fns[] = {reinterpret_cast<const void*>(&tune_ceiling_kernel<0>),
-                         reinterpret_cast<const void*>(&tune_ceiling_kernel<1>),
-                         reinterpret_cast<const void*>(&tune_ceiling_kernel<2>),
-                         reinterpret_cast<const void*>(&tune_ceiling_kernel<3>),
-                         reinterpret_cast<const void*>(&tune_ceiling_kernel<4>)};
-    if (kind < 0 || kind > 4) return DCCL_INVALID_ARGUMENT;
+    const CeilingEntry tab[] = {ceiling_entry<0, 64, 1>(),  ceiling_entry<1, 64, 1>(),  ceiling_entry<2, 64, 1>(),
+                                ceiling_entry<3, 64, 1>(),  ceiling_entry<4, 64, 1>(),  ceiling_entry<5, 256, 4>(),
+                                ceiling_entry<6, 256, 4>(), ceiling_entry<7, 64, 1>(),  ceiling_entry<8, 64, 1>()};
+    if (kind < 0 || kind >= int(sizeof(tab) / sizeof(tab[0]))) return DCCL_INVALID_ARGUMENT;
     size_t nvec = count_f32 / 4;
-    void* sink = nullptr;
-    void* args[] = {&send, &recv, &nvec, &sink};
-    return launch(fns[kind], nvec / 64, args, static_cast<hipStream_t>(stream), 64);
+    void* args[] = {&send, &recv, &nvec};
+    const CeilingEntry& e = tab[kind];
+    return launch(e.fn, nvec / (size_t(e.block) * e.unroll), args, static_cast<hipStream_t>(stream), e.block);
 }

@@ -30,8 +30,11 @@ int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count, int waves
  * with `lds_bytes` (<= 64 KiB) of unused dynamic LDS per block to cap resident blocks per CU. */
 int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
                             size_t lds_bytes, void* stream);
-/* HBM ceiling probes in the shipped shape: kind 0 read send, 1 read send+recv, 2 write recv,
- * 3 copy send->recv, 4 the fp32 Sum combine.  count_f32 % 256 == 0, 16-B aligned operands. */
+/* HBM ceiling probes (see tune_kernels.hip): kind 0 read send, 1 read send+recv, 2 write recv,
+ * 3 copy send->recv, 4 the fp32 Sum combine, all in the shipped shape; 5 read send+recv and
+ * 6 write recv in 256-thread x 4-vector blocks; 7 empty workgroups on the shipped grid;
+ * 8 the combine with the recv load issued first.
+ * count_f32 % 4096 == 0, 16-B aligned operands. */
 int dccl_tune_ceiling(int kind, const void* send, void* recv, size_t count_f32, void* stream);
 #ifdef __cplusplus
 }

@@ -3,7 +3,8 @@
 
 Times, interleaved in one process, the shipped access shape (one-wave blocks, 16 B per lane, all
 non-temporal) doing: read one operand, read both, write one, copy one into the other, and the fp32
-Sum combine (2 reads + 1 write).  Operands are 1 GiB each, carved from one allocation as in bench.py
+Sum combine (2 reads + 1 write); the read-both and write probes again in 256-thread x 4-vector
+blocks (a quarter of the workgroups); and the shipped grid of empty workgroups (dispatch alone).  Operands are 1 GiB each, carved from one allocation as in bench.py
 (recv, then send 4 KiB past its end).  Reports the bytes each kernel actually moves per second, so
 the combine's rate can be compared with the pure-read and pure-write ceilings of the same shape.
 
@@ -21,7 +22,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
 
 KINDS = {0: ("read send", 1), 1: ("read send + recv", 2), 2: ("write recv", 1), 3: ("copy send -> recv", 2),
-         4: ("combine recv += send", 3)}
+         4: ("combine recv += send", 3), 5: ("read send + recv, 256x4 blocks", 2),
+         6: ("write recv, 256x4 blocks", 1), 7: ("empty workgroups, shipped grid", 0),
+         8: ("combine, recv load first", 3)}
+SPLITS = (2, 4)  # the production combine split into this many slices on as many streams
 
 
 def main():
@@ -41,14 +45,33 @@ def main():
     lib = dccl_amd.lib
     for k in KINDS:
         assert lib.dccl_tune_ceiling(k, send.data_ptr(), recv.data_ptr(), n, st) == 0, k
+    streams = [torch.cuda.Stream() for _ in range(max(SPLITS))]
+
+    def split_combine(parts):
+        # slices of the production combine on `parts` streams, joined back into the current stream
+        start = torch.cuda.Event()
+        start.record()
+        per = n // parts
+        for j in range(parts):
+            sj = streams[j]
+            sj.wait_event(start)
+            dccl_amd.check(dccl_amd.local_reduce(send.data_ptr() + 4 * j * per, recv.data_ptr() + 4 * j * per, 7,
+                                                 per, 0, sj.cuda_stream))
+            done = torch.cuda.Event()
+            done.record(sj)
+            torch.cuda.current_stream().wait_event(done)
+
     torch.cuda.synchronize()
-    times = {k: [] for k in KINDS}
+    times = {k: [] for k in list(KINDS) + [f"split{p}" for p in SPLITS]}
     for _ in range(a.rounds):
-        for k in KINDS:
+        for k in times:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.iters):
-                lib.dccl_tune_ceiling(k, send.data_ptr(), recv.data_ptr(), n, st)
+                if isinstance(k, str):
+                    split_combine(int(k[5:]))
+                else:
+                    lib.dccl_tune_ceiling(k, send.data_ptr(), recv.data_ptr(), n, st)
             e1.record()
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) / a.iters)
@@ -57,8 +80,15 @@ def main():
         med = statistics.median(times[k])
         moved = streams * n * 4
         rows.append({"kind": k, "what": name, "bytes_moved": moved, "ms_median": round(med, 4),
-                     "ms_min": round(min(times[k]), 4), "gb_s": round(moved / (med * 1e-3) / 1e9, 1),
+                     "ms_min": round(min(times[k]), 4), "gb_s": round(moved / (med * 1e-3) / 1e9, 1), "workgroups_per_us": round(
+                         (n // 256 if k not in (5, 6) else n // 4096) / (med * 1e3), 1),
                      "frac_of_8tbs": round(moved / (med * 1e-3) / 8e12, 4)})
+    for p_ in SPLITS:
+        med = statistics.median(times[f"split{p_}"])
+        rows.append({"kind": f"split{p_}", "what": f"production combine in {p_} slices on {p_} streams",
+                     "bytes_moved": 3 * n * 4, "ms_median": round(med, 4), "ms_min": round(min(times[f"split{p_}"]), 4),
+                     "gb_s": round(3 * n * 4 / (med * 1e-3) / 1e9, 1),
+                     "frac_of_8tbs": round(3 * n * 4 / (med * 1e-3) / 8e12, 4)})
     out = {"mib_per_operand": a.mib, "device": torch.cuda.get_device_name(0), "rows": rows}
     txt = json.dumps(out, indent=1)
     if a.out:

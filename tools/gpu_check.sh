@@ -7,18 +7,20 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/${TAG:-r1}
 mkdir -p "$out"
 export TMPDIR=/tmp
+if [[ -z "${SKIP_TESTS:-}" ]]; then
 echo "== pytest -m gpu"
 timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -p no:cacheprovider > "$out/pytest_gpu.log" 2>&1 || { tail -60 "$out/pytest_gpu.log"; exit 1; }
 tail -3 "$out/pytest_gpu.log"
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
 cat "$out/smoke.log"
+fi
 echo "== bench"
 timeout -k 10 600 python bench.py > "$out/bench.json" 2> "$out/bench.err"
 cat "$out/bench.json"
 if [[ "${PROF:-1}" != 0 ]]; then
   echo "== rocprof kernel trace"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench --output-format csv -- python3 bench.py --steps 20 --no-cpu --no-host-staged > "$out/prof.log" 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --no-cpu --no-host-staged --no-other-layout > "$out/prof.log" 2>&1
   echo "== pmc FETCH_SIZE"
   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc_fetch" -o fetch -- python3 tools/pmc_probe.py > "$out/pmc_fetch.log" 2>&1
   echo "== pmc WRITE_SIZE"
