@@ -21,6 +21,8 @@ Rank 0 prints ONE JSON line:
                    restatement, single thread, timed on this host on a bounded sample (rank 0, N=1)
 Extra keys: payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
 rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately),
+c5 (BASELINE config C5 on every run: --c5-gib GiB per operand sharded over the N GPUs, strong scaling,
+combine time and, N>1, the RCCL all-gather of the reduced shards),
 dccl_allreduce (N>1: the namespace-dccl ncclAllReduce over the RCCL p2p ring and over the direct
 IPC peer-read transport, checked against each other and RCCL's own all_reduce, timed beside it;
 in a child process per rank, so a fault or hang there cannot take the bench line with it).
@@ -62,6 +64,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-host-staged", action="store_true")
+    p.add_argument("--c5-gib", type=float, default=16.0,
+                   help="BASELINE C5 extra on every run: one buffer of this many GiB per operand sharded over "
+                        "the N GPUs, combine + RCCL all-gather, reported as `c5` (0 disables)")
     p.add_argument("--no-other-layout", action="store_true",
                    help="skip timing the other operand layout (profiling runs: one layout per kernel average)")
     p.add_argument("--layout", default="pooled", choices=["pooled", "separate"],
@@ -323,6 +328,67 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
     return out
 
 
+def c5_extra(a, world: int, rank: int, dev, backend: str, coll_dev) -> dict:
+    """BASELINE config C5 measured inside every bench run, so the driver's 1/2/4/8-GPU runs report it too:
+    one buffer of a.c5_gib GiB per operand (fp32 Sum) split into contiguous 256-B aligned shards
+    (dccl_amd/shard.py), each GPU combining its shard (strong scaling: fixed total work), then the one
+    exchange step, an RCCL all-gather of the reduced shards over xGMI (every GPU ends with the whole
+    result).  Timings are barrier-bracketed and max-over-ranks, like the headline."""
+    from dccl_amd.shard import all_bounds
+    esz, dt, op = 4, 7, 0
+    total = int(a.c5_gib * GIB) // esz
+    bounds = all_bounds(total, esz, world)
+    n = bounds[rank][1] - bounds[rank][0]
+    send, recv = operand_pair(n, dt, op, 2 * rank, dev, "pooled")
+    stream = torch.cuda.current_stream(dev)
+    steps = 10
+    for _ in range(2):
+        dccl_amd.check(dccl_amd.local_reduce(send.data_ptr(), recv.data_ptr(), dt, n, op, stream.cuda_stream))
+
+    def bracket(fn, iters):
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=coll_dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    tc = bracket(lambda: dccl_amd.check(dccl_amd.local_reduce(send.data_ptr(), recv.data_ptr(), dt, n, op,
+                                                               stream.cuda_stream)), steps)
+    out = {"total_gib_per_operand": a.c5_gib, "shard_bytes_per_operand_max": max(b - a_ for a_, b in bounds) * esz,
+           "steps": steps, "combine_ms": round(tc * 1e3, 4),
+           "value": round(3 * total * esz / tc / GIB, 2), "unit": "GiB/s (3*N*4 B over all GPUs)",
+           "frac_of_n_hbm_peaks": round(3 * total * esz / tc / 1e9 / (HBM_PEAK_GBS * world), 4),
+           "scaling": "strong"}
+    del send
+    if world > 1:
+        width = max(b - a_ for a_, b in bounds)
+        src = recv if width == n else torch.cat([recv, recv.new_zeros(width - n)])
+        src = src.to(coll_dev)
+        del recv
+        gathered = torch.empty(world * width, dtype=src.dtype, device=coll_dev)
+        dist.all_gather_into_tensor(gathered, src)
+        tg = bracket(lambda: dist.all_gather_into_tensor(gathered, src), 3)
+        out["allgather"] = {"ms": round(tg * 1e3, 3), "backend": backend,
+                            "algbw_gb_s": round(total * esz / tg / 1e9, 1),
+                            "busbw_gb_s": round((world - 1) * width * esz / tg / 1e9, 1)}
+        out["combine_plus_allgather_ms"] = round((tc + tg) * 1e3, 3)
+        del gathered, src
+    torch.cuda.empty_cache()
+    progress(f"C5 ({a.c5_gib:g} GiB sharded): combine {tc * 1e3:.3f} ms" +
+             (f", all-gather {out['allgather']['ms']} ms" if world > 1 else ""))
+    return out
+
+
 def progress(msg: str) -> None:
     """One line on stderr per phase, so a long multi-GPU run is never silent (the JSON line is stdout)."""
     print(f"[bench] rank {os.environ.get('RANK', '0')}: {msg}", file=sys.stderr, flush=True)
@@ -475,7 +541,7 @@ def main():
         extra["other_layout"] = {"layout": other, "kernel_ms_avg": round(k2, 4),
                                  "frac": round(3 * nbytes / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     # the all-gather below only needs a reduced shard of the right size
-    if world > 1:  # the one exchange step of C5: RCCL all-gather of the reduced shards (separate)
+    if world > 1:  # the exchange step: RCCL all-gather of the reduced shards (reported separately)
         width = max(b - a_ for a_, b in bounds) if strong else n
         src = recv if width == n else torch.cat([recv, recv.new_zeros(width - n)])
         src = src.to(coll_dev)
@@ -498,11 +564,17 @@ def main():
                                       "(every GPU ends with the full result); not in value"}
         del gathered, src
         progress(f"all-gather done: {tag * 1e3:.3f} ms")
+    if a.c5_gib > 0 and not strong:
+        del send, recv
+        torch.cuda.empty_cache()
+        extra["c5"] = c5_extra(a, world, rank, dev, backend, coll_dev)
+        send = recv = None
+    if world > 1:
         # DCCL_BENCH_AR_TRANSPORTS=direct with the gloo backend rehearses the direct path with several
         # processes on one GPU (RCCL refuses two ranks on one device)
         rehearse = backend == "gloo" and os.environ.get("DCCL_BENCH_AR_TRANSPORTS") == "direct"
         if (backend == "nccl" or rehearse) and os.environ.get("DCCL_BENCH_NO_COLLECTIVE", "0") != "1":
-            del send, recv
+            send = recv = None
             torch.cuda.empty_cache()
             extra["dccl_allreduce"] = collective_in_child(world, rank, local, backend)
 

@@ -57,12 +57,37 @@ def test_bench_direct_allreduce_two_processes_one_gpu():
            "DCCL_BOOTSTRAP_TAG": f"bench_rehearsal_{_port()}"}
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "3",
-           "--warmup", "1", "--mib", "64", "--no-cpu", "--no-host-staged"]
+           "--warmup", "1", "--mib", "64", "--c5-gib", "0.25", "--no-cpu", "--no-host-staged"]
     p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
     assert len(lines) == 1, p.stdout[-3000:]
     res = json.loads(lines[0])
+    c5 = res["c5"]
+    assert c5["combine_ms"] > 0 and c5["allgather"]["ms"] > 0, c5
     ar = res["dccl_allreduce"]
     assert "error" not in ar, ar
     assert ar["direct"]["int32_sum_bit_exact_vs_rccl"] and ar["direct"]["fp32_within_bound"], ar
+
+
+def test_bench_single_gpu_line():
+    """bench.py at N=1 prints exactly one JSON line with the contract's keys and the C5 extra."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--mib", "64", "--c5-gib", "0.5",
+           "--no-host-staged", "--cpu-seconds", "1"]
+    p = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[-3000:]
+    res = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert key in res, key
+    assert res["n_gpus"] == 1 and res["value"] > 0
+    assert res["roofline"]["bound"] == "hbm" and 0 < res["roofline"]["frac"] < 1.5
+    assert res["cpu_baseline"]["cores"] >= 1 and res["cpu_baseline"]["value"] > 0
+    c5 = res["c5"]
+    assert c5["scaling"] == "strong" and c5["combine_ms"] > 0 and "allgather" not in c5
