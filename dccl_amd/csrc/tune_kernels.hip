@@ -272,3 +272,48 @@ extern "C" int dccl_tune_ceiling(int kind, const void* send, void* recv, size_t 
     const CeilingEntry& e = tab[kind];
     return launch(e.fn, nvec / (size_t(e.block) * e.unroll), args, static_cast<hipStream_t>(stream), e.block);
 }
+
+// ---------------------------------------------------------------------------------
+// Tuning only: write-only streaming probe over block shapes and store policies, to find the
+// chip's write ceiling (the one-wave shape is dispatch-bound when it only writes).
+// Variant v: (block, vectors per lane, store policy 0 = plain, 1 = nt, 2 = sc1 via asm).
+// ---------------------------------------------------------------------------------
+namespace {
+template <int BLOCK, int U, int POL>
+__global__ __launch_bounds__(BLOCK) void tune_write_kernel(u32x4* __restrict__ r, size_t nvec) {
+    const size_t base = size_t(blockIdx.x) * BLOCK * U + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + size_t(u) * BLOCK;
+        if (i >= nvec) continue;
+        const uint32_t v = uint32_t(i);
+        const u32x4 o{v, v, v, v};
+        if constexpr (POL == 0) r[i] = o;
+        if constexpr (POL == 1) __builtin_nontemporal_store(o, r + i);
+        if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(r + i), "v"(o) : "memory");
+    }
+}
+struct WriteEntry { const void* fn; int block, unroll, policy; };
+template <int B, int U, int P>
+WriteEntry write_entry() { return {reinterpret_cast<const void*>(&tune_write_kernel<B, U, P>), B, U, P}; }
+const WriteEntry kWrite[] = {
+    write_entry<64, 1, 1>(),  write_entry<64, 2, 1>(),  write_entry<64, 4, 1>(),  write_entry<64, 8, 1>(),
+    write_entry<128, 4, 1>(), write_entry<256, 1, 1>(), write_entry<256, 2, 1>(), write_entry<256, 4, 1>(),
+    write_entry<256, 8, 1>(), write_entry<512, 4, 1>(), write_entry<256, 4, 0>(), write_entry<64, 4, 0>(),
+    write_entry<256, 4, 2>(), write_entry<1024, 4, 1>(),
+};
+}  // namespace
+
+extern "C" int dccl_tune_write_num_variants(void) { return int(sizeof(kWrite) / sizeof(kWrite[0])); }
+
+extern "C" int dccl_tune_write_probe(int variant, void* recv, size_t count_f32, int* block, int* unroll, int* policy,
+                                     void* stream) {
+    if (variant < 0 || variant >= dccl_tune_write_num_variants()) return DCCL_INVALID_ARGUMENT;
+    if (count_f32 % 32768 || (reinterpret_cast<uintptr_t>(recv) & 15)) return DCCL_INVALID_ARGUMENT;
+    const WriteEntry& e = kWrite[variant];
+    *block = e.block; *unroll = e.unroll; *policy = e.policy;
+    if (stream == reinterpret_cast<void*>(~uintptr_t(0))) return DCCL_SUCCESS;  // info only
+    size_t nvec = count_f32 / 4;
+    void* args[] = {&recv, &nvec};
+    return launch(e.fn, nvec / (size_t(e.block) * e.unroll), args, static_cast<hipStream_t>(stream), e.block);
+}

@@ -36,6 +36,11 @@ int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void* recv, siz
  * 8 the combine with the recv load issued first.
  * count_f32 % 4096 == 0, 16-B aligned operands. */
 int dccl_tune_ceiling(int kind, const void* send, void* recv, size_t count_f32, void* stream);
+/* Write-only streaming probe: variant -> (block, vectors per lane, store policy 0 plain / 1 nt / 2 sc1);
+ * stream == (void*)~0 only reports the shape.  count_f32 % 32768 == 0. */
+int dccl_tune_write_num_variants(void);
+int dccl_tune_write_probe(int variant, void* recv, size_t count_f32, int* block, int* unroll, int* policy,
+                          void* stream);
 #ifdef __cplusplus
 }
 #endif

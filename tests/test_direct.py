@@ -232,7 +232,8 @@ def _ipc_rank(r, W, n, dt, op, tag, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,n,dt,op", [(2, 2 * 65536, 7, 0), (4, 4 * 4099, 2, 1), (3, 3 * 1000, 9, 3)])
+@pytest.mark.parametrize("W,n,dt,op", [(2, 2 * 65536, 7, 0), (4, 4 * 4099, 2, 1), (3, 3 * 1000, 9, 3),
+                                      (8, 8 * 65536, 7, 0)])
 def test_ipc_transport_processes(gpu, W, n, dt, op):
     """One process per rank (all on the box's one GPU), buffers exported with hipIpcGetMemHandle and
     read by the peers: every direct collective bit-exact against the ring simulation."""

@@ -89,7 +89,34 @@ def main():
                      "bytes_moved": 3 * n * 4, "ms_median": round(med, 4), "ms_min": round(min(times[f"split{p_}"]), 4),
                      "gb_s": round(3 * n * 4 / (med * 1e-3) / 1e9, 1),
                      "frac_of_8tbs": round(3 * n * 4 / (med * 1e-3) / 8e12, 4)})
-    out = {"mib_per_operand": a.mib, "device": torch.cuda.get_device_name(0), "rows": rows}
+    # write-only ceiling over block shapes and store policies (dccl_tune_write_probe)
+    import ctypes
+    wrows = []
+    nw = lib.dccl_tune_write_num_variants()
+    shapes = []
+    for v in range(nw):
+        b, u, pol = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        assert lib.dccl_tune_write_probe(v, recv.data_ptr(), n, ctypes.byref(b), ctypes.byref(u), ctypes.byref(pol),
+                                         ctypes.c_void_p(~0 & ((1 << 64) - 1))) == 0
+        shapes.append((b.value, u.value, ("plain", "nt", "sc1")[pol.value]))
+    dummy = [ctypes.c_int() for _ in range(3)]
+    wt = {v: [] for v in range(nw)}
+    for _ in range(a.rounds):
+        for v in range(nw):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                lib.dccl_tune_write_probe(v, recv.data_ptr(), n, *[ctypes.byref(x) for x in dummy], st)
+            e1.record()
+            e1.synchronize()
+            wt[v].append(e0.elapsed_time(e1) / a.iters)
+    for v in range(nw):
+        med = statistics.median(wt[v])
+        b, u, pol = shapes[v]
+        wrows.append({"block": b, "vectors_per_lane": u, "store": pol, "ms_median": round(med, 4),
+                      "gb_s": round(n * 4 / (med * 1e-3) / 1e9, 1), "frac_of_8tbs": round(n * 4 / (med * 1e-3) / 8e12, 4)})
+    wrows.sort(key=lambda x: x["ms_median"])
+    out = {"mib_per_operand": a.mib, "device": torch.cuda.get_device_name(0), "rows": rows, "write_shapes": wrows}
     txt = json.dumps(out, indent=1)
     if a.out:
         with open(a.out, "w") as f:
