@@ -155,10 +155,45 @@ extern "C" int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count
 // ---------------------------------------------------------------------------------
 // Tuning only: k-way fp32 Sum (dccl_local_reduce_multi's kernel) with an explicit shape.
 // Variant v: 0 = shipped (64 threads, 1 vector, all nt), 1 = 64 threads x 2 vectors,
-// 2 = 256 threads x 1 vector, 3 = only send loads nt, 4 = 64 threads x 4 vectors; `lds_bytes` of
+// 2 = 256 threads x 1 vector, 3 = only send loads nt, 4 = 64 threads x 4 vectors,
+// 5/6/7 = staged: recv + s0 first, then the other sends 1/2/3 at a time (aligned operands only); `lds_bytes` of
 // unused dynamic LDS per block caps the resident blocks per CU (160 KiB / lds_bytes).
 // ---------------------------------------------------------------------------------
 namespace {
+// Staged k-way: first recv and s0 together, then the remaining sends G at a time; each stage
+// waits for its loads before the next stage issues (the empty asm consumes the accumulator and
+// fences memory), so a wave never has more than max(2, G) 16-B loads per lane in flight and
+// the chip sees the two-stream read pattern it streams fastest (tools/ceiling_probe.py).
+template <int K, int G>
+__global__ __launch_bounds__(64) void tune_multi_staged_kernel(SendList sends, unsigned char* __restrict__ recv,
+                                                               size_t nvec) {
+    const size_t i = size_t(blockIdx.x) * 64 + threadIdx.x;
+    if (i < nvec) {
+        u32x4* vr = reinterpret_cast<u32x4*>(recv);
+        u32x4 acc = combine16<float, kSum>(__builtin_nontemporal_load(vr + i),
+                                           __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sends.p[0]) + i));
+#pragma unroll
+        for (int k0 = 1; k0 < K; k0 += G) {
+            asm volatile("" : "+v"(acc)::"memory");
+            u32x4 sv[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                if (k0 + g < K) sv[g] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sends.p[k0 + g]) + i);
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                if (k0 + g < K) acc = combine16<float, kSum>(acc, sv[g]);
+        }
+        __builtin_nontemporal_store(acc, vr + i);
+    }
+}
+template <int K, int G>
+int tune_multi_staged(SendList sl, unsigned char* r, Split sp, hipStream_t stream, size_t lds) {
+    if (sp.head || sp.tail) return DCCL_INVALID_ARGUMENT;
+    void* args[] = {&sl, &r, &sp.nvec};
+    return launch(reinterpret_cast<const void*>(&tune_multi_staged_kernel<K, G>), ceil_div(sp.nvec, 64), args, stream,
+                  64, lds);
+}
+
 template <int K, typename C>
 int tune_multi_launch(SendList sl, unsigned char* r, Split sp, hipStream_t stream, size_t lds = 0) {
     size_t grid = ceil_div(sp.nvec, C::TILE);
@@ -175,6 +210,9 @@ int tune_multi_k(int variant, SendList sl, unsigned char* r, Split sp, hipStream
     case 2: return tune_multi_launch<K, VecCfg<256, 1, 7, false, 1>>(sl, r, sp, st, lds);
     case 3: return tune_multi_launch<K, VecCfg<64, 1, 1, false, 1>>(sl, r, sp, st, lds);
     case 4: return tune_multi_launch<K, VecCfg<64, 4, 7, false, 1>>(sl, r, sp, st, lds);
+    case 5: return tune_multi_staged<K, 1>(sl, r, sp, st, lds);
+    case 6: return tune_multi_staged<K, 2>(sl, r, sp, st, lds);
+    case 7: return tune_multi_staged<K, 3>(sl, r, sp, st, lds);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }

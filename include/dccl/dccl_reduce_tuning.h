@@ -26,7 +26,7 @@ int dccl_tune_reduce_f32_sum_lds(const void* send, void* recv, size_t count, int
 /* Block of `waves` one-wave tiles; each wave pairs recv tile w with send tile (w+skew)%waves,
  * exchanging send through LDS (tests address-pair decorrelation). */
 int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count, int waves, int skew, void* stream);
-/* k-way fp32 Sum (the dccl_local_reduce_multi kernel) in shape `variant` 0-4 (see tune_kernels.hip),
+/* k-way fp32 Sum (the dccl_local_reduce_multi kernel) in shape `variant` 0-7 (see tune_kernels.hip),
  * with `lds_bytes` (<= 64 KiB) of unused dynamic LDS per block to cap resident blocks per CU. */
 int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
                             size_t lds_bytes, void* stream);

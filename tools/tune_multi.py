@@ -22,7 +22,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
 
 PEAK = 8.0e12
-VARIANTS = {0: "64x1 nt-all (shipped)", 1: "64x2 nt-all", 2: "256x1 nt-all", 3: "64x1 nt-send", 4: "64x4 nt-all"}
+VARIANTS = {0: "64x1 nt-all (shipped)", 1: "64x2 nt-all", 2: "256x1 nt-all", 3: "64x1 nt-send", 4: "64x4 nt-all",
+            5: "staged: recv+s0, then 1 send at a time", 6: "staged: recv+s0, then 2 at a time",
+            7: "staged: recv+s0, then 3 at a time"}
 LDS_PER_CU = 160 << 10
 WAVES = [32, 24, 20, 16, 13, 11, 9, 7, 5]  # one-wave blocks resident per CU, set through unused LDS
 
@@ -63,13 +65,15 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--mib", type=int, default=1024)
     p.add_argument("--out", default="gpurun_out/tune_multi.json")
+    p.add_argument("--ks", default="1,2,3,4,5,6,7,8")
+    p.add_argument("--no-waves", action="store_true", help="skip the occupancy-cap sweep of variant 0")
     a = p.parse_args()
     nbytes = a.mib << 20
     n = nbytes // 4
     st = torch.cuda.current_stream().cuda_stream
     rows = []
     for layout in ("separate", "staggered"):
-        for k in range(1, 9):
+        for k in [int(x) for x in a.ks.split(",")]:
             keep, ptrs = operands(k, nbytes, layout)
             for j, q in enumerate(ptrs):
                 dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, j, st))
@@ -83,7 +87,7 @@ def main():
                 ms = median_ms(lambda: dccl_amd.lib.dccl_tune_multi_f32_sum(arr, k, recv, n, v, 0, st))
                 row[f"v{v}_ms"] = round(ms, 4)
                 row[f"v{v}_frac"] = round((k + 2) * nbytes / (ms * 1e-3) / PEAK, 4)
-            for w in WAVES:
+            for w in ([] if a.no_waves else WAVES):
                 ms = median_ms(lambda: dccl_amd.lib.dccl_tune_multi_f32_sum(arr, k, recv, n, 0, lds_for(w), st))
                 row[f"w{w}_frac"] = round((k + 2) * nbytes / (ms * 1e-3) / PEAK, 4)
             rows.append(row)
