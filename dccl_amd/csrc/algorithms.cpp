@@ -25,6 +25,17 @@ namespace dccl_amd {
 
 namespace {
 inline uint32_t mod(int64_t a, uint32_t w) { return static_cast<uint32_t>(((a % w) + w) % w); }
+
+// Take the acknowledgements of `posted` sends to `peer` (every posted message is acknowledged, even
+// after a failed step, so the channel stays in step); the first error wins.
+ncclResult_t collect_acks(dccl::dcclComm* c, uint32_t peer, uint32_t posted, bool device, hipStream_t st,
+                          ncclResult_t rc) {
+    for (uint32_t i = 0; i < posted; ++i) {
+        const ncclResult_t rw = xport_wait_send(c, peer, device, st);
+        if (rc == dccl::ncclSuccess) rc = rw;
+    }
+    return rc;
+}
 }  // namespace
 
 ncclResult_t reduce_scatter_ring(dccl::dcclComm* c, void* buffer, void* scratch, size_t count, int dtype, int op,
@@ -46,22 +57,25 @@ ncclResult_t reduce_scatter_ring(dccl::dcclComm* c, void* buffer, void* scratch,
         }
         return rc;
     }
-    for (uint32_t s = 0; s + 1 < W; ++s) {
-        ncclResult_t rc = xport_send(c, to, data(int64_t(r) - s), slot_bytes, device, st);
-        if (rc == dccl::ncclSuccess) {
-            if (scratch != nullptr) {  // reference shape: land in the scratchpad, then combine
-                rc = xport_recv(c, from, scratch, slot_bytes, device, st);
-                if (rc == dccl::ncclSuccess)
-                    rc = combine(scratch, data(int64_t(r) - s - 1), dtype, slot_elems, op, device, st);
-            } else {  // fused: combine straight from the peer's chunk
-                rc = xport_recv_combine(c, from, data(int64_t(r) - s - 1), slot_elems, dtype, op, device, st);
-            }
+    // A chunk this rank sends at step s (slot r-s) is never written again by this rank during the
+    // reduce-scatter (it writes slots r-1 ... r+1, each before sending it), so the acknowledgements
+    // are collected once, after the last step, instead of after every step: a step's critical path
+    // then holds one cross-stream hand-off (the peer's chunk is ready) instead of two.
+    ncclResult_t rc = dccl::ncclSuccess;
+    uint32_t posted = 0;
+    for (uint32_t s = 0; s + 1 < W && rc == dccl::ncclSuccess; ++s) {
+        rc = xport_send(c, to, data(int64_t(r) - s), slot_bytes, device, st);
+        if (rc != dccl::ncclSuccess) break;
+        ++posted;
+        if (scratch != nullptr) {  // reference shape: land in the scratchpad, then combine
+            rc = xport_recv(c, from, scratch, slot_bytes, device, st);
+            if (rc == dccl::ncclSuccess)
+                rc = combine(scratch, data(int64_t(r) - s - 1), dtype, slot_elems, op, device, st);
+        } else {  // fused: combine straight from the peer's chunk
+            rc = xport_recv_combine(c, from, data(int64_t(r) - s - 1), slot_elems, dtype, op, device, st);
         }
-        const ncclResult_t rw = xport_wait_send(c, to, device, st);
-        if (rc == dccl::ncclSuccess) rc = rw;
-        if (rc != dccl::ncclSuccess) return rc;
     }
-    return dccl::ncclSuccess;
+    return collect_acks(c, to, posted, device, st, rc);
 }
 
 ncclResult_t all_gather_ring(dccl::dcclComm* c, void* buffer, size_t slot_elems, int dtype, bool device,
@@ -79,14 +93,17 @@ ncclResult_t all_gather_ring(dccl::dcclComm* c, void* buffer, size_t slot_elems,
         }
         return dccl::ncclSuccess;
     }
-    for (uint32_t s = 0; s + 1 < W; ++s) {
-        ncclResult_t rc = xport_send(c, to, data(int64_t(r) - s), slot_bytes, device, st);
-        if (rc == dccl::ncclSuccess) rc = xport_recv(c, from, data(int64_t(r) - s - 1), slot_bytes, device, st);
-        const ncclResult_t rw = xport_wait_send(c, to, device, st);
-        if (rc == dccl::ncclSuccess) rc = rw;
-        if (rc != dccl::ncclSuccess) return rc;
+    // As in the reduce-scatter, a slot is written (received) once and only then forwarded, so the
+    // acknowledgements are collected after the last step.
+    ncclResult_t rc = dccl::ncclSuccess;
+    uint32_t posted = 0;
+    for (uint32_t s = 0; s + 1 < W && rc == dccl::ncclSuccess; ++s) {
+        rc = xport_send(c, to, data(int64_t(r) - s), slot_bytes, device, st);
+        if (rc != dccl::ncclSuccess) break;
+        ++posted;
+        rc = xport_recv(c, from, data(int64_t(r) - s - 1), slot_bytes, device, st);
     }
-    return dccl::ncclSuccess;
+    return collect_acks(c, to, posted, device, st, rc);
 }
 
 ncclResult_t all_reduce_ring(dccl::dcclComm* c, void* buffer, void* scratch, size_t count, int dtype, int op,

@@ -54,9 +54,10 @@ ncclResult_t xport_send(dccl::dcclComm* c, uint32_t peer, const void* buf, size_
                         hipStream_t stream) {
     Message m{buf, bytes, device, nullptr};
     if (device) {
-        m.ready = c->ready_events[peer];
+        m.ready = c->ready_events[size_t(peer) * c->event_ring + c->sent[peer] % c->event_ring];
         if (hipEventRecord(m.ready, stream) != hipSuccess) return dccl::ncclUnhandledCudaError;
     }
+    ++c->sent[peer];
     Channel& ch = c->group->channel(c->rank, peer);
     {
         std::lock_guard<std::mutex> lk(ch.mu);
@@ -76,12 +77,13 @@ ncclResult_t xport_recv(dccl::dcclComm* c, uint32_t peer, void* dst, size_t byte
         m = ch.msgs.front();
         ch.msgs.pop_front();
     }
+    const uint64_t n_taken = c->received[peer]++;
     ncclResult_t rc = dccl::ncclSuccess;
     Ack a;
     if (m.bytes != bytes || m.device != device) {
         rc = dccl::ncclInvalidUsage;  // mismatched send/recv pairing
     } else if (device) {
-        a.done = c->done_events[peer];
+        a.done = c->done_events[size_t(peer) * c->event_ring + n_taken % c->event_ring];
         rc = hip_ok(hipStreamWaitEvent(stream, m.ready, 0));
         if (rc == dccl::ncclSuccess) rc = hip_ok(hipMemcpyAsync(dst, m.ptr, bytes, hipMemcpyDeviceToDevice, stream));
         if (rc == dccl::ncclSuccess) rc = hip_ok(hipEventRecord(a.done, stream));
@@ -106,12 +108,13 @@ ncclResult_t xport_recv_combine(dccl::dcclComm* c, uint32_t peer, void* dst, siz
         m = ch.msgs.front();
         ch.msgs.pop_front();
     }
+    const uint64_t n_taken = c->received[peer]++;
     ncclResult_t rc = dccl::ncclSuccess;
     Ack a;
     if (m.bytes != count * size_of_dtype(dtype) || m.device != device) {
         rc = dccl::ncclInvalidUsage;
     } else if (device) {
-        a.done = c->done_events[peer];
+        a.done = c->done_events[size_t(peer) * c->event_ring + n_taken % c->event_ring];
         rc = hip_ok(hipStreamWaitEvent(stream, m.ready, 0));
         if (rc == dccl::ncclSuccess) rc = combine(m.ptr, dst, dtype, count, op, true, stream);
         // the done event must exist in the stream even after a failed combine: the sender waits on it

@@ -86,10 +86,18 @@ struct dccl::dcclComm {
     int device = -1;  // HIP device current at init
     void* rccl = nullptr;  // non-null: cross-process RCCL transport (rccl_transport.hpp), device buffers only
     void* ipc = nullptr;   // non-null: cross-process IPC peer-read transport (direct.hpp), device buffers only
-    // Per-peer event pairs for the stream-ordered device transport (reused every step:
-    // a stream wait captures the event's state at the time of the wait).
-    std::vector<hipEvent_t> ready_events;  // indexed by destination rank
-    std::vector<hipEvent_t> done_events;   // indexed by source rank
+    // Events of the stream-ordered device transport: a ring of `event_ring` per peer, indexed by the
+    // channel's message count, so that no event is recorded again before every wait on its previous
+    // record has been enqueued.  A ring phase posts at most W-1 messages to one peer before it
+    // collects their acknowledgements (algorithms.cpp), and the acknowledgement of a message is
+    // posted only after the receiver enqueued its wait, hence a ring of W-1 suffices.  (With one event
+    // per peer a receiver could end up waiting on the sender's NEXT record, and with every rank doing
+    // so the streams would wait on each other in a cycle.)
+    uint32_t event_ring = 1;
+    std::vector<hipEvent_t> ready_events;  // [destination rank * event_ring + message % event_ring]
+    std::vector<hipEvent_t> done_events;   // [source rank * event_ring + message % event_ring]
+    std::vector<uint64_t> sent;            // messages posted to each peer
+    std::vector<uint64_t> received;        // messages taken from each peer
     // Scratchpads (the reference keeps thread_local ones, /root/reference/src/core/dccl.cpp:57-84)
     void* dev_scratch = nullptr;
     size_t dev_scratch_bytes = 0;

@@ -132,12 +132,15 @@ ncclResult_t join(dcclComm** out, uint32_t world, int64_t want_rank) {
     }
     c->group = g;
     c->world = world;
-    c->ready_events.assign(world, nullptr);
-    c->done_events.assign(world, nullptr);
+    c->event_ring = world > 2 ? world - 1 : 1;
+    c->ready_events.assign(size_t(world) * c->event_ring, nullptr);
+    c->done_events.assign(size_t(world) * c->event_ring, nullptr);
+    c->sent.assign(world, 0);
+    c->received.assign(world, 0);
     if (dev >= 0) {
-        for (uint32_t p = 0; p < world; ++p) {
-            if (hipEventCreateWithFlags(&c->ready_events[p], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&c->done_events[p], hipEventDisableTiming) != hipSuccess)
+        for (size_t i = 0; i < c->ready_events.size(); ++i) {
+            if (hipEventCreateWithFlags(&c->ready_events[i], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->done_events[i], hipEventDisableTiming) != hipSuccess)
                 return dccl::ncclUnhandledCudaError;
         }
     }
