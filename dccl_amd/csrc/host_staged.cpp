@@ -11,7 +11,8 @@
 // over NSLOT device slots, so PCIe in both directions and the HBM combine overlap
 // (SURVEY.md §8(f) row 1).  Page-locked user buffers (dccl_register_host_memory, the
 // analogue of dcclRegisterCacheMemory, dccl.cpp:503-549) are DMA'd directly; pageable ones
-// are bounced through per-thread pinned staging buffers by the calling thread.
+// are bounced through per-thread pinned staging buffers by the calling thread and a small pool of
+// copy threads (DCCL_HOST_COPY_THREADS; one bounce core is slower than the PCIe link).
 //
 // Page-locked operands (and pageable ones up to 16 MiB, bounced) skip the DMA pipeline: one kernel
 // loads and stores the host memory directly over PCIe; the pipeline serves large pageable operands.
@@ -20,10 +21,13 @@
 // locks, no global mutable state; each thread owns its streams and slots per device.
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "dccl/dccl_reduce.h"
@@ -34,6 +38,81 @@ namespace {
 
 constexpr int kSlots = 3;
 constexpr size_t kChunkBytes = size_t(16) << 20;  // per operand per slot
+constexpr size_t kParallelCopyMin = size_t(1) << 20;  // smaller bounces stay on the calling thread
+
+// Bounce copies of pageable operands, split into contiguous 64-B aligned slices over the calling
+// thread and n-1 workers.  One copy at a time: a Stager, and so its pool, belongs to one thread.
+// DCCL_HOST_COPY_THREADS sets n (default 4; 1 = the calling thread alone).
+class CopyPool {
+public:
+    explicit CopyPool(int n) : n_(n < 1 ? 1 : n) {
+        for (int i = 1; i < n_; ++i) workers_.emplace_back([this, i] { loop(i); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        go_.notify_all();
+        for (std::thread& t : workers_) t.join();
+    }
+    void copy(void* dst, const void* src, size_t bytes) {
+        if (n_ == 1 || bytes < kParallelCopyMin) {
+            std::memcpy(dst, src, bytes);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            dst_ = static_cast<unsigned char*>(dst);
+            src_ = static_cast<const unsigned char*>(src);
+            bytes_ = bytes;
+            pending_ = n_ - 1;
+            ++gen_;
+        }
+        go_.notify_all();
+        slice(0);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+    }
+
+private:
+    void slice(int i) const {
+        const size_t per = (bytes_ / size_t(n_)) & ~size_t(63);
+        const size_t b = per * size_t(i), e = (i == n_ - 1) ? bytes_ : b + per;
+        std::memcpy(dst_ + b, src_ + b, e - b);
+    }
+    void loop(int i) {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(m_);
+        for (;;) {
+            go_.wait(lk, [&] { return gen_ != seen; });
+            seen = gen_;
+            if (stop_) return;
+            lk.unlock();
+            slice(i);
+            lk.lock();
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+
+    const int n_;
+    std::vector<std::thread> workers_;
+    std::mutex m_;
+    std::condition_variable go_, done_;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+    int pending_ = 0;
+    unsigned char* dst_ = nullptr;
+    const unsigned char* src_ = nullptr;
+    size_t bytes_ = 0;
+};
+
+int copy_threads() {
+    const char* e = std::getenv("DCCL_HOST_COPY_THREADS");
+    const int n = e ? std::atoi(e) : 4;
+    return n < 1 ? 1 : (n > 64 ? 64 : n);
+}
 
 struct Slot {
     void* d_send = nullptr;
@@ -91,16 +170,21 @@ private:
     int drain_slot(Slot& sl) {  // finish a bounced D2H: wait, then copy to user memory
         if (!sl.pending_dst) return DCCL_SUCCESS;
         if (hipEventSynchronize(sl.out_done) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
-        std::memcpy(sl.pending_dst, sl.h_recv, sl.pending_bytes);
+        bounce(sl.pending_dst, sl.h_recv, sl.pending_bytes);
         sl.pending_dst = nullptr;
         sl.pending_bytes = 0;
         return DCCL_SUCCESS;
+    }
+    void bounce(void* dst, const void* src, size_t bytes) {  // pageable <-> pinned staging copy
+        if (!pool_) pool_ = std::make_unique<CopyPool>(copy_threads());
+        pool_->copy(dst, src, bytes);
     }
 
     int device_;
     bool ready_ = false;
     hipStream_t in_ = nullptr, comp_ = nullptr, out_ = nullptr;
     Slot slots_[kSlots];
+    std::unique_ptr<CopyPool> pool_;  // created at the first pageable bounce
 };
 
 // Page-locked host memory: returns the device-side alias the GPU can load/store through
@@ -135,17 +219,17 @@ int Stager::run_zero_copy(const unsigned char* send, unsigned char* recv, void* 
     Slot& sl = slots_[0];
     if ((dsend == nullptr || drecv == nullptr) && bytes > kChunkBytes) return DCCL_INTERNAL_ERROR;  // bounce size
     if (dsend == nullptr) {  // pageable: bounce through the slot's pinned buffer
-        std::memcpy(sl.h_send, send, bytes);
+        bounce(sl.h_send, send, bytes);
         if (hipHostGetDevicePointer(&dsend, sl.h_send, 0) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
     }
     const bool bounce_recv = drecv == nullptr;
     if (bounce_recv) {
-        std::memcpy(sl.h_recv, recv, bytes);
+        bounce(sl.h_recv, recv, bytes);
         if (hipHostGetDevicePointer(&drecv, sl.h_recv, 0) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
     }
     int rc = dccl_local_reduce(dsend, drecv, dtype, count, op, comp_);
     if (hipStreamSynchronize(comp_) != hipSuccess && rc == DCCL_SUCCESS) rc = DCCL_UNHANDLED_DEVICE_ERROR;
-    if (rc == DCCL_SUCCESS && bounce_recv) std::memcpy(recv, sl.h_recv, bytes);
+    if (rc == DCCL_SUCCESS && bounce_recv) bounce(recv, sl.h_recv, bytes);
     return rc;
 }
 
@@ -169,10 +253,10 @@ int Stager::run(const unsigned char* send, unsigned char* recv, int dtype, size_
         if (hipStreamWaitEvent(in_, sl.out_done, 0) != hipSuccess) { rc = DCCL_UNHANDLED_DEVICE_ERROR; break; }
         const unsigned char* src_s = send + off * esz;
         const unsigned char* src_r = recv + off * esz;
-        if (!send_pinned) { std::memcpy(sl.h_send, src_s, bytes); src_s = static_cast<unsigned char*>(sl.h_send); }
+        if (!send_pinned) { bounce(sl.h_send, src_s, bytes); src_s = static_cast<unsigned char*>(sl.h_send); }
         if (!recv_pinned) {
             // h_recv is also the D2H landing zone of this slot: its previous use was drained above.
-            std::memcpy(sl.h_recv, src_r, bytes);
+            bounce(sl.h_recv, src_r, bytes);
             src_r = static_cast<unsigned char*>(sl.h_recv);
         }
         if (hipMemcpyAsync(sl.d_send, src_s, bytes, hipMemcpyHostToDevice, in_) != hipSuccess ||

@@ -202,10 +202,11 @@ def test_multi_matches_sequential(dccl, k):
 
 # ----------------------------------------------------------------------------- host path
 @pytest.mark.parametrize("zero_copy", ["default", "0"])
-@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("pinned", ["none", "both", "send"])
 def test_host_staged(dccl, pinned, zero_copy, monkeypatch):
     """Host operands: zero-copy kernel (page-locked, or pageable <= 16 MiB bounced) and the
-    3-stream DMA pipeline (large pageable, or DCCL_HOST_ZEROCOPY_MAX=0)."""
+    3-stream DMA pipeline (large pageable, or DCCL_HOST_ZEROCOPY_MAX=0).  "send" is Derecho's
+    shape: a registered RDMA scratchpad combined into a pageable user chunk."""
     if zero_copy == "0":
         monkeypatch.setenv("DCCL_HOST_ZEROCOPY_MAX", "0")
     rng = np.random.default_rng(400)
@@ -216,17 +217,44 @@ def test_host_staged(dccl, pinned, zero_copy, monkeypatch):
             op = int(rng.integers(0, 4))
             want = expected(s, r, dt, op)
             s2, r2 = s.copy(), r.copy()
-            if pinned:
-                assert dccl.register_host_memory(s2.ctypes.data, s2.nbytes) == 0
-                assert dccl.register_host_memory(r2.ctypes.data, r2.nbytes) == 0
+            regs = {"none": [], "both": [s2, r2], "send": [s2]}[pinned]
+            for x in regs:
+                assert dccl.register_host_memory(x.ctypes.data, x.nbytes) == 0
             try:
                 assert dccl.local_reduce_host(s2.ctypes.data, r2.ctypes.data, dt, n, op) == 0
             finally:
-                if pinned:
-                    dccl.deregister_host_memory(s2.ctypes.data)
-                    dccl.deregister_host_memory(r2.ctypes.data)
+                for x in regs:
+                    dccl.deregister_host_memory(x.ctypes.data)
             assert fp_equal(r2, want, dt), (dt, n, op)
             assert s2.tobytes() == s.tobytes()
+
+
+@pytest.mark.parametrize("threads", ["1", "3", "8"])
+def test_host_staged_copy_threads(dccl, threads, monkeypatch):
+    """Pageable bounce copies split over DCCL_HOST_COPY_THREADS threads: odd byte counts, every slice
+    boundary, pipeline and zero-copy sizes (the pool is created per thread, so run in a fresh thread)."""
+    import threading
+    monkeypatch.setenv("DCCL_HOST_COPY_THREADS", threads)
+    rng = np.random.default_rng(401)
+    errors = []
+
+    def body():
+        try:
+            torch.cuda.set_device(0)
+            for dt, n in [(0, (1 << 20) + 7), (7, (3 << 20) + 5), (8, 5 * (1 << 20) + 3), (6, 9 * (1 << 20) + 1)]:
+                s, r = rand_inputs(rng, dt, n)
+                op = int(rng.integers(0, 4))
+                want = expected(s, r, dt, op)
+                r2 = r.copy()
+                assert dccl.local_reduce_host(s.ctypes.data, r2.ctypes.data, dt, n, op) == 0
+                assert fp_equal(r2, want, dt), (threads, dt, n, op)
+        except Exception as e:  # surfaced in the test thread
+            errors.append(e)
+
+    t = threading.Thread(target=body)
+    t.start()
+    t.join()
+    assert not errors, errors
 
 
 # ----------------------------------------------------------------------------- ring (C1)
@@ -309,6 +337,33 @@ def test_one_gib_inverse_roundtrip(dccl):
     s.neg_()
     assert dccl.local_reduce(s.data_ptr(), r.data_ptr(), 2, n, 0, 0) == 0
     assert torch.equal(r, r0)
+
+
+@pytest.mark.slow
+def test_grid_stride_past_launch_cap(dccl):
+    """Maximum-size edge of the launch arithmetic: the vector kernel's grid is capped at 2^24 one-wave
+    blocks (16 GiB of 16-B vectors per operand), beyond which blocks stride.  17 GiB + 37 B uint8
+    operands at a 5-B offset (scalar head and tail, a partial last tile, > 1 tile per block), Sum,
+    checked 1 GiB at a time against torch's wrapping uint8 add; bytes before the operands untouched."""
+    off, n = 5, (17 << 30) + 37
+    free, _ = torch.cuda.mem_get_info()
+    if free < 3 * (n + off) + (4 << 30):
+        pytest.skip("needs ~56 GiB of free HBM")
+    g = torch.Generator(device="cuda").manual_seed(17)
+    sb = torch.empty(n + off, dtype=torch.uint8, device="cuda").random_(0, 256, generator=g)
+    rb = torch.empty(n + off, dtype=torch.uint8, device="cuda").random_(0, 256, generator=g)
+    r0 = rb.clone()
+    try:
+        assert dccl.local_reduce(sb.data_ptr() + off, rb.data_ptr() + off, 1, n, 0, 0) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(rb[:off], r0[:off])
+        step = 1 << 30
+        for a in range(off, n + off, step):
+            b = min(a + step, n + off)
+            assert torch.equal(rb[a:b], r0[a:b] + sb[a:b]), a
+    finally:
+        del sb, rb, r0
+        torch.cuda.empty_cache()
 
 
 def test_misaligned_reference_wrong_build_correct(dccl):
