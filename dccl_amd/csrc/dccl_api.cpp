@@ -222,12 +222,14 @@ bool ipc_requested() {
 
 enum class Algorithm { kRing, kRabenseifner, kDirect, kUnknown };
 
-// DCCL_ALLREDUCE_ALGORITHM (the reference's DCCL/allreduce_algorithm key, dccl.hpp:38-46): ring
-// (default), rabenseifner, or direct.  The reference silently skips the reduction for any other
-// value (dccl.cpp:412-501); here it is ncclInvalidUsage.
+// DCCL_ALLREDUCE_ALGORITHM (the reference's DCCL/allreduce_algorithm key, dccl.hpp:38-46): auto
+// (default: the direct collectives for device buffers of an in-process group, direct_selected(), and
+// the ring otherwise), ring, rabenseifner, or direct.  The reference defaults to ring and silently
+// skips the reduction for any other value (dccl.cpp:412-501); here that is ncclInvalidUsage.
 Algorithm allreduce_algorithm() {
     const char* a = std::getenv(DCCL_ALLREDUCE_ALGORITHM_CONFSTR);
-    if (a == nullptr || *a == 0 || std::string(a) == DCCL_ALLREDUCE_RING) return Algorithm::kRing;
+    if (a == nullptr || *a == 0 || std::string(a) == DCCL_ALLREDUCE_RING || std::string(a) == "auto")
+        return Algorithm::kRing;
     if (std::string(a) == DCCL_ALLREDUCE_RABENSEIFNER) return Algorithm::kRabenseifner;
     if (std::string(a) == "direct") return Algorithm::kDirect;
     return Algorithm::kUnknown;

@@ -35,7 +35,8 @@ ncclResult_t ipc_join(dccl::dcclComm* c, uint32_t world, uint32_t rank);
 ncclResult_t ipc_leave(dccl::dcclComm* c);
 
 // True when the collectives of `c` on device buffers take the direct algorithms: always on the
-// IPC transport; on the in-process transport when DCCL_ALLREDUCE_ALGORITHM=direct.
+// IPC transport; on the in-process transport (W <= 8) unless DCCL_ALLREDUCE_ALGORITHM is ring or
+// rabenseifner.
 bool direct_selected(const dccl::dcclComm* c);
 
 ncclResult_t direct_all_reduce(dccl::dcclComm* c, const void* send, void* recv, size_t count, int dtype, int op,

@@ -78,10 +78,16 @@ def _expected_allreduce(inputs, dt, op):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("algo", ["", "ring"])
 @pytest.mark.parametrize("device", [True, False])
 @pytest.mark.parametrize("W,dt,op", [(4, 7, 0), (3, 9, 1), (2, 2, 3), (5, 8, 2)])
-def test_all_reduce_threads(W, dt, op, device):
+def test_all_reduce_threads(W, dt, op, device, algo, monkeypatch):
+    """Thread ranks, bit-exact against the ring simulation + oracle.  algo "" is the default (device
+    buffers take the direct collectives, host buffers the ring); "ring" forces the ring."""
     import torch
+    if algo == "ring" and not device:
+        pytest.skip("host buffers always take the ring")
+    monkeypatch.setenv("DCCL_ALLREDUCE_ALGORITHM", algo)
     rng = np.random.default_rng(W * 10 + dt)
     n = W * 40961
     npd = oracle.NP_DTYPES[dt]
@@ -111,8 +117,10 @@ def test_all_reduce_threads(W, dt, op, device):
 
 
 @pytest.mark.gpu
-def test_reduce_scatter_threads_device():
+@pytest.mark.parametrize("algo", ["", "ring"])
+def test_reduce_scatter_threads_device(algo, monkeypatch):
     import torch
+    monkeypatch.setenv("DCCL_ALLREDUCE_ALGORITHM", algo)
     W, slot, dt, op = 4, 65537, 7, 0
     rng = np.random.default_rng(3)
     inputs = [rng.standard_normal(W * slot).astype(np.float32) for _ in range(W)]
