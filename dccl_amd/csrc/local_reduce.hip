@@ -12,7 +12,8 @@
 //     operand per block and ~1M blocks for 1 GiB; every load and the store non-temporal;
 //   * dtype and op are template parameters (no per-element switch);
 //   * unaligned head / tail elements are folded into block 0 of the same launch;
-//   * operands with different 16-B phases / element misalignment take scalar kernels.
+//   * element-aligned operands with different 16-B phases take the shifted vector kernel
+//     (aligned loads of both, a cross-lane funnel shift of send); element-misaligned ones a byte kernel.
 // No LDS and no MFMA: each element is touched once (BASELINE.json north_star).
 //
 // Roofline: HBM, 3 * count * sizeof(T) algorithmic bytes (read send, read recv, write recv).
@@ -32,6 +33,25 @@ namespace {
 // Default configuration of the shipped kernel.  One-wave blocks, one 16-B vector per lane and operand, every access non-temporal: the
 // fastest shape measured on MI355X at 1 GiB (tools/tune_reduce.py, profiles/r1_tune.json).
 using DefaultCfg = VecCfg<64, 1, kNtSend | kNtRecv | kNtStore, false>;
+// When send's 128-B phase differs from recv's, every 1 KiB send tile straddles 9 lines, one of them
+// shared with the next tile (a wave on another XCD): send is then loaded through the caches, so the
+// shared line is fetched from HBM once (tools/phase_probe.py on MI355X, 1 GiB fp32 Sum: 81.0 % with
+// non-temporal send loads, 84.1 % cached; with equal phases non-temporal is 1 % faster).
+using StraddleCfg = VecCfg<64, 1, kNtRecv | kNtStore, false>;
+// The shifted kernel (operands with different 16-B phases) by the same rule; lane 63's extra send
+// vector is always loaded through the caches.
+constexpr int ShiftPolicy = kNtSend | kNtRecv | kNtStore;
+constexpr int ShiftStraddlePolicy = kNtRecv | kNtStore;
+// recv is aligned to this many bytes by the head scalars (DCCL_REDUCE_ALIGN, a power of two from 16 to
+// 4096; default 128, one line): a recv that straddles lines costs 10-15 % (profiles/r1_s3_phase_probe.json).
+size_t recv_align() {
+    static const size_t v = [] {
+        const char* e = std::getenv("DCCL_REDUCE_ALIGN");
+        const unsigned long long x = e ? std::strtoull(e, nullptr, 10) : 128ull;
+        return (x >= 16 && x <= 4096 && (x & (x - 1)) == 0) ? static_cast<size_t>(x) : size_t(128);
+    }();
+    return v;
+}
 // Optional occupancy cap: DCCL_REDUCE_LDS_CAP bytes of (unused) dynamic LDS per one-wave block
 // (e.g. 7168 admits 22 blocks per CU instead of 32).  Off by default: with operands in a friendly
 // physical placement the uncapped launch is 0.8 % faster (profiles/r1_occupancy_pooled_*.json);
@@ -60,8 +80,15 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
     const auto r = static_cast<unsigned char*>(recv);
     const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
     if ((as | ar) % sizeof(T)) return launch_scalar<T, OP>(s, r, count, false, stream);
-    if ((as ^ ar) & 15) return launch_scalar<T, OP>(s, r, count, true, stream);
-    return launch_vec<T, OP, DefaultCfg>(s, r, split_for_vectors<T>(ar, count), stream, 0, occupancy_lds());
+    const size_t align = recv_align();
+    const Split sp = split_for_vectors<T>(ar, count, align);
+    if ((as ^ ar) & 15) {
+        const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);  // the shifted kernel's send vectors
+        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false>(s, r, count, stream, align)
+                         : launch_shift<T, OP, ShiftPolicy, false>(s, r, count, stream, align);
+    }
+    if ((as ^ ar) & 127) return launch_vec<T, OP, StraddleCfg>(s, r, sp, stream, 0, occupancy_lds());
+    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream, 0, occupancy_lds());
 }
 
 // k-way combine: every resident wave keeps k+1 16-B loads per lane in flight, so the resident waves
@@ -103,7 +130,7 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
                                  : reinterpret_cast<const void*>(&reduce_multi_scalar_kernel<T, OP, false>);
         return launch(fn, grid, args, stream);
     }
-    const Split sp = split_for_vectors<T>(ar, count);
+    const Split sp = split_for_vectors<T>(ar, count, recv_align());
     switch (nsend) {
     case 1: return launch_multi_vec<T, OP, 1>(sl, r, sp, stream);
     case 2: return launch_multi_vec<T, OP, 2>(sl, r, sp, stream);
@@ -171,7 +198,7 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
                                  : reinterpret_cast<const void*>(&reduce_chain_scalar_kernel<T, OP, false>);
         return launch(fn, grid, args, stream);
     }
-    const Split sp = split_for_vectors<T>(ad, count);
+    const Split sp = split_for_vectors<T>(ad, count, recv_align());
     switch (nsend) {
     case 1: return launch_chain_vec<T, OP, 1>(sl, o, d, sp, stream);
     case 2: return launch_chain_vec<T, OP, 2>(sl, o, d, sp, stream);

@@ -44,7 +44,8 @@ __device__ __forceinline__ void st_elem(unsigned char* base, size_t i, T v) {
 
 // ---------------------------------------------------------------------------------
 // Vector kernel.  Operands are split as [head scalars | nvec 16-B vectors | tail
-// scalars]; head aligns recv (and, by construction, send) to 16 B.
+// scalars]; head aligns recv to its 128-B lines (split_for_vectors) and send, which has recv's
+// 16-B phase, to 16 B.
 // ---------------------------------------------------------------------------------
 // Kernel shape: BLOCK threads, UNROLL 16-B vectors per thread per operand, cache POLICY
 // bits, XCD: remap block ids so that each XCD's blocks walk one contiguous range.
@@ -56,6 +57,18 @@ struct VecCfg {
     static constexpr bool XCD = XCD_;
     static constexpr size_t TILE = size_t(BLOCK_) * UNROLL_;
 };
+
+// Block 0's scalar elements outside the vector body: head [0, head) (< the recv alignment) and tail
+// (< one vector).
+template <typename T, int OP>
+__device__ __forceinline__ void edge_scalars(const unsigned char* send, unsigned char* recv, size_t head,
+                                             size_t nvec, size_t tail) {
+    for (size_t j = threadIdx.x; j < head + tail; j += blockDim.x) {
+        const size_t i = j < head ? j : head + nvec * Pack<T>::N + (j - head);
+        const T a = ld_elem<T, true>(recv, i), b = ld_elem<T, true>(send, i);
+        st_elem<T, true>(recv, i, Combine<T, OP>::apply(a, b));
+    }
+}
 
 template <typename T, int OP, typename C>
 __device__ __forceinline__ void full_tile(const u32x4* __restrict__ vs, u32x4* __restrict__ vr, size_t base) {
@@ -106,13 +119,78 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_vec_kernel(const unsigned cha
     if (nfull * C::TILE < nvec && bid == nfull % gridDim.x)
         partial_tile<T, OP, C>(vs, vr, nfull * C::TILE + threadIdx.x, nvec);
 
-    // Scalar head [0, head) and tail [head + nvec*V, count): < 16 elements each.
-    if (blockIdx.x == 0 && threadIdx.x < head + tail) {
-        const size_t i = threadIdx.x < head ? threadIdx.x
-                                            : head + nvec * Pack<T>::N + (threadIdx.x - head);
-        const T a = ld_elem<T, true>(recv, i), b = ld_elem<T, true>(send, i);
-        st_elem<T, true>(recv, i, Combine<T, OP>::apply(a, b));
+    // Scalar head [0, head) and tail [head + nvec*V, count)
+    if (blockIdx.x == 0) edge_scalars<T, OP>(send, recv, head, nvec, tail);
+}
+
+// ---------------------------------------------------------------------------------
+// Shifted vector kernel: element-aligned operands whose 16-B phases differ.  DCCL combines chunk
+// k of a user buffer (offset k*count/W*sizeof(T)) with an aligned scratchpad, so any chunk size
+// that is not a multiple of 16 B lands here.  recv is walked in aligned 16-B vectors from
+// recv + head; the matching send bytes start p bytes (0 < p < 16, a multiple of sizeof(T)) past
+// the 16-B boundary A.  Every lane loads the ALIGNED send vector A[v], takes A[v+1] from its
+// right-hand neighbour (ds_bpermute; lane 63 loads it itself, issued with the other loads), and
+// funnel-shifts the 32 bytes by p (v_alignbyte_b32), so every access stays a 16-B vector.
+// A[nvec] is loaded although only its first p bytes belong to send: an aligned 16-B load never
+// leaves the page of its first byte, which is send's.
+// ---------------------------------------------------------------------------------
+constexpr int kNtExtra = 8;  // policy bit: non-temporal load of lane 63's extra vector
+
+template <int Q>
+__device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, unsigned b) {
+    const unsigned d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    u32x4 o;
+    o.x = __builtin_amdgcn_alignbyte(d[Q + 1], d[Q + 0], b);
+    o.y = __builtin_amdgcn_alignbyte(d[Q + 2], d[Q + 1], b);
+    o.z = __builtin_amdgcn_alignbyte(d[Q + 3], d[Q + 2], b);
+    o.w = __builtin_amdgcn_alignbyte(d[Q + 4], d[Q + 3], b);
+    return o;
+}
+
+// lane l receives lane (l+1) % 64's vector
+__device__ __forceinline__ u32x4 from_next_lane(u32x4 x) {
+    const int a = int((threadIdx.x + 1) & 63) << 2;
+    u32x4 o;
+    o.x = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.x)));
+    o.y = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.y)));
+    o.z = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.z)));
+    o.w = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.w)));
+    return o;
+}
+
+template <typename T, int OP, int POLICY, bool XCD, int TAG = 0>
+__global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* __restrict__ send,
+                                                          unsigned char* __restrict__ recv, size_t head,
+                                                          size_t nvec, size_t tail, unsigned p) {
+    const unsigned char* sa = send + head * sizeof(T);
+    const u32x4* va = reinterpret_cast<const u32x4*>(sa - p);  // A: 16-B aligned
+    u32x4* vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
+    const size_t ntiles = (nvec + 63) / 64;
+    const size_t bid = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const unsigned q = p >> 2, b = p & 3;
+    const bool last_lane = threadIdx.x == 63;
+    for (size_t t = bid; t < ntiles; t += gridDim.x) {  // uniform per wave: every lane reaches the bpermute
+        const size_t v = t * 64 + threadIdx.x;
+        u32x4 lo = {0u, 0u, 0u, 0u}, ex = {0u, 0u, 0u, 0u}, r = {0u, 0u, 0u, 0u};
+        if (v <= nvec) lo = ld16<(POLICY & kNtSend) != 0>(va + v);
+        if (v < nvec) r = ld16<(POLICY & kNtRecv) != 0>(vr + v);
+        if (last_lane && v < nvec) ex = ld16<(POLICY & kNtExtra) != 0>(va + v + 1);
+        u32x4 hi = from_next_lane(lo);
+        if (last_lane) hi = ex;
+        if (v < nvec) {
+            u32x4 s;
+            switch (q) {  // uniform
+            case 0: s = funnel16<0>(lo, hi, b); break;
+            case 1: s = funnel16<1>(lo, hi, b); break;
+            case 2: s = funnel16<2>(lo, hi, b); break;
+            default: s = funnel16<3>(lo, hi, b); break;
+            }
+            const u32x4 o = combine16<T, OP>(r, s);
+            if constexpr ((POLICY & kNtStore) != 0) __builtin_nontemporal_store(o, vr + v);
+            else vr[v] = o;
+        }
     }
+    if (blockIdx.x == 0) edge_scalars<T, OP>(send, recv, head, nvec, tail);
 }
 
 // ---------------------------------------------------------------------------------
@@ -175,13 +253,14 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_multi_vec_kernel(SendList sen
             }
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x < head + tail) {
-        const size_t i = threadIdx.x < head ? threadIdx.x
-                                            : head + nvec * Pack<T>::N + (threadIdx.x - head);
-        T acc = ld_elem<T, true>(recv, i);
+    if (blockIdx.x == 0) {
+        for (size_t j = threadIdx.x; j < head + tail; j += blockDim.x) {
+            const size_t i = j < head ? j : head + nvec * Pack<T>::N + (j - head);
+            T acc = ld_elem<T, true>(recv, i);
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, true>(sends.p[k], i));
-        st_elem<T, true>(recv, i, acc);
+            for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, true>(sends.p[k], i));
+            st_elem<T, true>(recv, i, acc);
+        }
     }
 }
 
@@ -227,12 +306,14 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sen
             __builtin_nontemporal_store(combine16<T, OP>(o, acc), vd + i);
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x < head + tail) {
-        const size_t i = threadIdx.x < head ? threadIdx.x : head + nvec * Pack<T>::N + (threadIdx.x - head);
-        T acc = ld_elem<T, true>(sends.p[0], i);
+    if (blockIdx.x == 0) {
+        for (size_t j = threadIdx.x; j < head + tail; j += blockDim.x) {
+            const size_t i = j < head ? j : head + nvec * Pack<T>::N + (j - head);
+            T acc = ld_elem<T, true>(sends.p[0], i);
 #pragma unroll
-        for (int k = 1; k < K; ++k) acc = Combine<T, OP>::apply(ld_elem<T, true>(sends.p[k], i), acc);
-        st_elem<T, true>(dst, i, Combine<T, OP>::apply(ld_elem<T, true>(own, i), acc));
+            for (int k = 1; k < K; ++k) acc = Combine<T, OP>::apply(ld_elem<T, true>(sends.p[k], i), acc);
+            st_elem<T, true>(dst, i, Combine<T, OP>::apply(ld_elem<T, true>(own, i), acc));
+        }
     }
 }
 
@@ -268,10 +349,13 @@ struct Split {
     size_t head, nvec, tail;
 };
 
+// head scalars bring recv to an `align`-byte boundary (16 or more, a power of two).  Aligning recv to
+// its 128-B lines keeps every tile's recv loads and stores whole-line: a recv that straddles lines
+// costs 10-15 % (tools/phase_probe.py, profiles/r1_s3_phase_probe.json).  head < align / sizeof(T).
 template <typename T>
-inline Split split_for_vectors(uintptr_t recv, size_t count) {
+inline Split split_for_vectors(uintptr_t recv, size_t count, size_t align = 16) {
     constexpr size_t V = Pack<T>::N;
-    size_t head = ((16 - (recv & 15)) & 15) / sizeof(T);
+    size_t head = ((align - (recv & (align - 1))) & (align - 1)) / sizeof(T);
     if (head > count) head = count;
     const size_t rest = count - head;
     const size_t nvec = rest / V;
@@ -287,6 +371,18 @@ int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t s
     void* args[] = {&s, &r, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_vec_kernel<T, OP, C>), grid, args, stream, C::BLOCK,
                   lds_bytes);
+}
+
+// Element-aligned operands with different 16-B phases: the shifted vector kernel.
+template <typename T, int OP, int POLICY, bool XCD, int TAG = 0>
+int launch_shift(const unsigned char* s, unsigned char* r, size_t count, hipStream_t stream, size_t align = 16) {
+    Split sp = split_for_vectors<T>(reinterpret_cast<uintptr_t>(r), count, align);
+    unsigned p = unsigned((reinterpret_cast<uintptr_t>(s) + sp.head * sizeof(T)) & 15);
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    void* args[] = {&s, &r, &sp.head, &sp.nvec, &sp.tail, &p};
+    return launch(reinterpret_cast<const void*>(&reduce_shift_kernel<T, OP, POLICY, XCD, TAG>), grid, args, stream,
+                  64);
 }
 
 }  // namespace dccl_amd

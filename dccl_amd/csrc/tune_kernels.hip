@@ -27,10 +27,18 @@ const TuneEntry kTune[] = {
     DCCL_TV(64, 1, 1, 0),  DCCL_TV(64, 1, 7, 1),  DCCL_TV(64, 2, 7, 0),  DCCL_TV(64, 4, 7, 0),
     DCCL_TV(128, 1, 7, 0), DCCL_TV(128, 1, 5, 0), DCCL_TV(128, 1, 6, 0), DCCL_TV(128, 1, 7, 1),
     DCCL_TV(256, 1, 7, 0), DCCL_TV(256, 1, 7, 1), DCCL_TV(256, 4, 7, 0), DCCL_TV(1024, 1, 7, 0),
-    DCCL_TV(256, 4, 1, 0),
+    DCCL_TV(256, 4, 1, 0), DCCL_TV(64, 1, 6, 1),  DCCL_TV(64, 1, 2, 0),  DCCL_TV(64, 1, 2, 1),
 };
 #undef DCCL_TV
 }  // namespace
+
+// recv alignment of the tuning launches: DCCL_TUNE_ALIGN (default 16, the alignment every earlier
+// tuning table was measured with)
+static size_t tune_align() {
+    const char* e = std::getenv("DCCL_TUNE_ALIGN");
+    const unsigned long long x = e ? std::strtoull(e, nullptr, 10) : 16ull;
+    return (x >= 16 && x <= 4096 && (x & (x - 1)) == 0) ? static_cast<size_t>(x) : size_t(16);
+}
 
 extern "C" int dccl_tune_num_variants(void) { return int(sizeof(kTune) / sizeof(kTune[0])); }
 
@@ -47,7 +55,7 @@ extern "C" int dccl_tune_reduce_f32_sum_lds(const void* send, void* recv, size_t
     const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
     if (((as | ar) & 3) || ((as ^ ar) & 15)) return DCCL_INVALID_ARGUMENT;
     return kTune[variant].fn(static_cast<const unsigned char*>(send), static_cast<unsigned char*>(recv),
-                             split_for_vectors<float>(ar, count), static_cast<hipStream_t>(stream), grid_cap,
+                             split_for_vectors<float>(ar, count, tune_align()), static_cast<hipStream_t>(stream), grid_cap,
                              lds_bytes);
 }
 
@@ -354,4 +362,31 @@ extern "C" int dccl_tune_write_probe(int variant, void* recv, size_t count_f32, 
     size_t nvec = count_f32 / 4;
     void* args[] = {&recv, &nvec};
     return launch(e.fn, nvec / (size_t(e.block) * e.unroll), args, static_cast<hipStream_t>(stream), e.block);
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning only: the shifted kernel (operands with different 16-B phases), fp32 Sum, by cache policy
+// and block order.
+// ---------------------------------------------------------------------------------
+namespace {
+using ShiftFn = int (*)(const unsigned char*, unsigned char*, size_t, hipStream_t, size_t);
+struct ShiftEntry { int policy, xcd; ShiftFn fn; };
+#define DCCL_SV(P, X) ShiftEntry{P, X, &launch_shift<float, kSum, P, X, 1>}
+const ShiftEntry kShift[] = {DCCL_SV(7, false), DCCL_SV(15, false), DCCL_SV(6, false), DCCL_SV(7, true),
+                             DCCL_SV(6, true),  DCCL_SV(3, false),  DCCL_SV(5, false)};
+#undef DCCL_SV
+}  // namespace
+
+extern "C" int dccl_tune_shift_num_variants(void) { return int(sizeof(kShift) / sizeof(kShift[0])); }
+
+extern "C" int dccl_tune_shift_f32_sum(const void* send, void* recv, size_t count, int variant, int* policy,
+                                       int* xcd, void* stream) {
+    if (variant < 0 || variant >= dccl_tune_shift_num_variants()) return DCCL_INVALID_ARGUMENT;
+    const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
+    if (((as | ar) & 3) || ((as ^ ar) & 15) == 0) return DCCL_INVALID_ARGUMENT;
+    if (policy) *policy = kShift[variant].policy;
+    if (xcd) *xcd = kShift[variant].xcd;
+    if (count == 0) return DCCL_SUCCESS;
+    return kShift[variant].fn(static_cast<const unsigned char*>(send), static_cast<unsigned char*>(recv), count,
+                              static_cast<hipStream_t>(stream), tune_align());
 }

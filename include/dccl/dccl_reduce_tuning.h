@@ -38,6 +38,11 @@ int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void* recv, siz
 int dccl_tune_ceiling(int kind, const void* send, void* recv, size_t count_f32, void* stream);
 /* Write-only streaming probe: variant -> (block, vectors per lane, store policy 0 plain / 1 nt / 2 sc1);
  * stream == (void*)~0 only reports the shape.  count_f32 % 32768 == 0. */
+// The shifted kernel for operands with different 16-B phases (fp32 Sum; both element-aligned, phases
+// different), by cache policy bits (1 send, 2 recv, 4 store, 8 lane 63's extra send load) and block order.
+int dccl_tune_shift_num_variants(void);
+int dccl_tune_shift_f32_sum(const void* send, void* recv, size_t count, int variant, int* policy, int* xcd,
+                            void* stream);
 int dccl_tune_write_num_variants(void);
 int dccl_tune_write_probe(int variant, void* recv, size_t count_f32, int* block, int* unroll, int* policy,
                           void* stream);

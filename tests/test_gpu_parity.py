@@ -140,6 +140,31 @@ def test_alignment_cases(dccl, dt):
             assert fp_equal(out, expected(s, r, dt, op), dt), (dt, op, n, soff, roff)
 
 
+@pytest.mark.parametrize("dt", ALL_DTYPES)
+def test_shifted_kernel_every_phase(dccl, dt):
+    """The shifted vector kernel (element-aligned operands, different 16-B phases): every phase
+    difference the dtype allows, in both directions, sizes around the 64-vector tile (partial last
+    tile, last lane's neighbour outside the tile), with head and tail scalars."""
+    rng = np.random.default_rng(300 + dt)
+    esz = np.dtype(oracle.NP_DTYPES[dt]).itemsize
+    per_tile = 64 * (16 // esz)
+    sizes = [1, 16 // esz + 1, per_tile - 1, per_tile + 16 // esz + 3, 3 * per_tile + 5, 40001]
+    for p in range(esz, 16, esz):
+        for soff, roff in ((p, 0), (0, p), (16 + p, 32 + esz if p + esz < 16 else 32)):
+            if (soff - roff) % 16 == 0:
+                continue
+            for n in sizes:
+                s, r = rand_inputs(rng, dt, n)
+                op = int(rng.integers(0, 4))
+                ts, ps = dev_bytes(s, soff)
+                tr, pr = dev_bytes(r, roff)
+                assert dccl.local_reduce(ps, pr, dt, n, op, 0) == 0
+                torch.cuda.synchronize()
+                assert fp_equal(host_of(tr, roff, r), expected(s, r, dt, op), dt), (dt, op, n, soff, roff)
+                nb = n * esz  # nothing outside recv's bytes is written
+                assert not tr[:roff].any() and not tr[roff + nb:].any(), (dt, n, soff, roff)
+
+
 @pytest.mark.parametrize("dt", [6, 9])
 def test_all_16bit_patterns(dccl, dt):
     """Every fp16 / bf16 bit pattern as recv against a fixed set of partners."""

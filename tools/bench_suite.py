@@ -228,16 +228,19 @@ def c1(results):
 
 
 def misaligned(results, mib=1024):
-    """Operands off the 16-B phase of each other (scalar element kernel) or off element alignment
-    (byte-gather kernel): the fallback paths, fp32 Sum, 1 GiB."""
+    """Operands off their 128-B lines (vector kernel), off the 16-B phase of each other (shifted vector
+    kernel) or off element alignment (byte-gather kernel), fp32 Sum, 1 GiB."""
     st = torch.cuda.current_stream().cuda_stream
     nbytes = mib << 20
     n = nbytes // 4 - 4
     s = fill(nbytes, 7, 0, 1)
     r = fill(nbytes, 7, 0, 2)
     rows = []
-    for soff, roff, what in ((0, 0, "aligned (vector path)"), (16, 0, "same 16-B phase, offset 16 B (vector)"),
-                             (4, 0, "4-B phase mismatch (scalar element path)"), (8, 4, "8/4-B offsets (scalar)"),
+    for soff, roff, what in ((0, 0, "aligned (vector path)"),
+                             (16, 0, "same 16-B phase, send off its lines (vector, send cached)"),
+                             (0, 16, "same 16-B phase, recv off its lines (vector, recv realigned by the head)"),
+                             (4, 0, "4-B phase mismatch (shifted vector kernel)"),
+                             (8, 4, "8/4-B offsets (shifted vector kernel, recv realigned)"),
                              (1, 1, "byte offsets, same phase (element-misaligned byte path)")):
         fn = lambda soff=soff, roff=roff: dccl_amd.local_reduce(s.data_ptr() + soff, r.data_ptr() + roff, 7, n, 0, st)
         med, _ = time_launches([fn], rounds=5)
