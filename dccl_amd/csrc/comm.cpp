@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -20,16 +21,26 @@ Group::Group(uint32_t world)
     for (size_t i = 0; i < size_t(world) * world; ++i) chan_.push_back(std::make_unique<Channel>());
 }
 
+// Ranks of a collective arrive within microseconds of each other: poll the generation for up to 2 ms
+// (with the pause hint) before blocking on the condition variable, whose wake-up costs tens of
+// microseconds on the critical path of every direct collective (tools/ipc_latency.py).
 void Group::barrier() {
     std::unique_lock<std::mutex> lk(bmu_);
-    const uint64_t gen = barrier_gen_;
+    const uint64_t gen = barrier_gen_.load(std::memory_order_relaxed);
     if (++barrier_count_ == world_) {
         barrier_count_ = 0;
-        ++barrier_gen_;
+        barrier_gen_.store(gen + 1, std::memory_order_release);
         bcv_.notify_all();
         return;
     }
-    bcv_.wait(lk, [&] { return barrier_gen_ != gen; });
+    lk.unlock();
+    const auto start = std::chrono::steady_clock::now();
+    for (uint32_t i = 1; barrier_gen_.load(std::memory_order_acquire) == gen; ++i) {
+        if ((i & 1023) == 0 && std::chrono::steady_clock::now() - start > std::chrono::milliseconds(2)) break;
+        __builtin_ia32_pause();
+    }
+    lk.lock();
+    bcv_.wait(lk, [&] { return barrier_gen_.load(std::memory_order_acquire) != gen; });
 }
 
 namespace {

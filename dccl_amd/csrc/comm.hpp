@@ -18,6 +18,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
@@ -73,7 +74,7 @@ private:
     std::mutex bmu_;
     std::condition_variable bcv_;
     uint32_t barrier_count_ = 0;
-    uint64_t barrier_gen_ = 0;
+    std::atomic<uint64_t> barrier_gen_{0};  // written under bmu_, polled without it
 };
 
 }  // namespace dccl_amd

@@ -80,16 +80,24 @@ ncclResult_t shm_barrier(IpcXport* x) {
         s->gen.store(g + 1, std::memory_order_release);
         return dccl::ncclSuccess;
     }
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(x->timeout_s);
+    // Spin (with the pause hint) for up to kSpin before sleeping: peers arrive within microseconds of
+    // each other in a collective, and a 20 us sleep costs 50-80 us once the kernel's timer slack is
+    // added, which set the latency of small collectives (tools/ipc_latency.py).
+    constexpr auto kSpin = std::chrono::milliseconds(2);
+    const auto start = std::chrono::steady_clock::now();
+    const auto deadline = start + std::chrono::duration<double>(x->timeout_s);
     for (uint64_t i = 0; s->gen.load(std::memory_order_acquire) == g; ++i) {
         if (s->abort.load(std::memory_order_relaxed)) return dccl::ncclRemoteError;
-        if (i > 4096) {
-            if ((i & 255) == 0 && std::chrono::steady_clock::now() > deadline) {
-                s->abort.store(1, std::memory_order_relaxed);
-                return dccl::ncclSystemError;
-            }
-            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if ((i & 1023) != 1023) {
+            __builtin_ia32_pause();
+            continue;
         }
+        const auto now = std::chrono::steady_clock::now();
+        if (now > deadline) {
+            s->abort.store(1, std::memory_order_relaxed);
+            return dccl::ncclSystemError;
+        }
+        if (now - start > kSpin) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     return dccl::ncclSuccess;
 }
