@@ -24,7 +24,8 @@ rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported 
 c5 (BASELINE config C5 on every run: --c5-gib GiB per operand sharded over the N GPUs, strong scaling,
 combine time and, N>1, the RCCL all-gather of the reduced shards),
 dccl_allreduce (N>1: the namespace-dccl ncclAllReduce over the RCCL p2p ring and over the direct
-IPC peer-read transport, checked against each other and RCCL's own all_reduce, timed beside it;
+IPC peer-read transport, checked against each other and RCCL's own all_reduce, timed beside it, plus
+the namespace-dccl all_gather of each transport against RCCL's all_gather (`dccl_allgather`);
 in a child process per rank, so a fault or hang there cannot take the bench line with it).
 Progress goes to stderr, one line per phase.
 """
@@ -322,10 +323,50 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
         out["rccl_allreduce"] = {"ms": round(t * 1e3, 3),
                                  "busbw_gb_s": round(2 * (world - 1) / world * count * 4 / t / 1e9, 1),
                                  "note": "RCCL's own all_reduce, informational: its combine is RCCL's"}
+        out["dccl_allgather"] = allgather_compare(comms, world, rank, dev, st, count, iters)
     finally:
         for comm in comms.values():
             comm.finalize()
     return out
+
+
+def allgather_compare(comms: dict, world: int, rank: int, dev, st, count: int, iters: int) -> dict:
+    """The exchange step of C5 (and the second half of the direct all-reduce) through the namespace-dccl
+    ncclAllGather of each transport, int32, count/world elements per rank: checked bit for bit against
+    the concatenation of every rank's slice (each rank regenerates all slices from their seeds), timed,
+    and beside RCCL's all_gather_into_tensor when torch.distributed runs on RCCL."""
+    per = count // world
+    slices = [torch.randint(-2**31, 2**31 - 1, (per,), device=dev, dtype=torch.int32,
+                            generator=torch.Generator(device=dev).manual_seed(777 + p)) for p in range(world)]
+    want = torch.cat(slices)
+    mine = slices[rank]
+    res = {"bytes_per_rank": per * 4}
+    y = torch.empty(per * world, dtype=torch.int32, device=dev)
+    for name, comm in comms.items():
+        y.zero_()
+        torch.cuda.synchronize(dev)
+        dccl_amd.check(comm.all_gather(mine.data_ptr(), y.data_ptr(), per, 2, st.cuda_stream), name)
+        torch.cuda.synchronize(dev)
+        ok = bool(torch.equal(y, want))
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dccl_amd.check(comm.all_gather(mine.data_ptr(), y.data_ptr(), per, 2, st.cuda_stream), name)
+        torch.cuda.synchronize(dev)
+        t = (time.perf_counter() - t0) / iters
+        res[name] = {"bit_exact": ok, "ms": round(t * 1e3, 3),
+                     "busbw_gb_s": round((world - 1) * per * 4 / t / 1e9, 1)}
+    if dist.get_backend() == "nccl":
+        dist.all_gather_into_tensor(y, mine)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_gather_into_tensor(y, mine)
+        torch.cuda.synchronize(dev)
+        t = (time.perf_counter() - t0) / iters
+        res["rccl"] = {"ms": round(t * 1e3, 3), "busbw_gb_s": round((world - 1) * per * 4 / t / 1e9, 1)}
+    return res
 
 
 def c5_extra(a, world: int, rank: int, dev, backend: str, coll_dev) -> dict:
