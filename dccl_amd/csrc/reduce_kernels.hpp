@@ -194,8 +194,9 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
 }
 
 // ---------------------------------------------------------------------------------
-// Scalar fallback for operands whose 16-B phases differ (ALIGNED) or that are not
-// even element-aligned (!ALIGNED).  Grid-stride, 4 independent elements per thread.
+// Scalar fallback for operands that are not even element-aligned (!ALIGNED: byte gathers; the
+// pairwise combine's only scalar path since the shifted kernel took over different 16-B phases).
+// ALIGNED is kept for tuning comparisons.  Grid-stride, 4 independent elements per thread.
 // ---------------------------------------------------------------------------------
 template <typename T, int OP, bool ALIGNED>
 __global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(const unsigned char* __restrict__ send,
