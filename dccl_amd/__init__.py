@@ -85,6 +85,8 @@ def _load():
         "dccl_local_reduce_host": (c_int, [c_void_p, c_void_p, c_int, c_size_t, c_int]),
         "dccl_local_reduce_chain": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_void_p, c_int, c_size_t,
                                             c_int, c_void_p]),
+        "dccl_local_reduce_chain_host": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_void_p, c_int,
+                                                 c_size_t, c_int]),
         "dccl_copy_multi": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_size_t, c_void_p]),
         "dccl_register_host_memory": (c_int, [c_void_p, c_size_t]),
         "dccl_deregister_host_memory": (c_int, [c_void_p]),
@@ -139,7 +141,7 @@ EXPORTED_SYMBOLS = [
     "dccl_synth_fill", "dccl_tune_multi_f32_sum", "dccl_local_reduce_chain", "dccl_copy_multi",
     "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_tune_ceiling",
     "dccl_tune_write_num_variants", "dccl_tune_write_probe", "dccl_tune_shift_num_variants",
-    "dccl_tune_shift_f32_sum",
+    "dccl_tune_shift_f32_sum", "dccl_local_reduce_chain_host",
 ]
 
 
@@ -180,6 +182,13 @@ def local_reduce_chain(send_ptrs, own_ptr: int, dst_ptr: int, dtype: int, count:
     arr = (ctypes.c_void_p * max(1, len(send_ptrs)))(*send_ptrs)
     return int(lib.dccl_local_reduce_chain(arr, len(send_ptrs), own_ptr, dst_ptr, int(dtype), int(count), int(op),
                                            stream or None))
+
+
+def local_reduce_chain_host(send_ptrs, own_ptr: int, dst_ptr: int, dtype: int, count: int, op: int) -> int:
+    """The host twin of local_reduce_chain (synchronous, staged through the current GPU)."""
+    arr = (ctypes.c_void_p * max(1, len(send_ptrs)))(*send_ptrs)
+    return int(lib.dccl_local_reduce_chain_host(arr, len(send_ptrs), own_ptr, dst_ptr, int(dtype), int(count),
+                                                int(op)))
 
 
 def copy_multi(src_ptrs, dst_ptrs, nbytes: int, stream: int = 0) -> int:

@@ -372,6 +372,8 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
     if (W > 1 && algo != Algorithm::kRabenseifner && (count < W || count % W)) return ncclInvalidArgument;
     if (W > 1 && dev && direct_selected(comm))
         return direct_all_reduce(comm, sendbuff, recvbuff, count, datatype, op, stream);
+    if (W > 1 && !dev && host_direct_selected(comm, total / W))
+        return direct_all_reduce_host(comm, sendbuff, recvbuff, count, datatype, op);
     if ((rc = copy_bytes(recvbuff, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:393-408
     if (W == 1) return ncclSuccess;
     void* scratch = nullptr;

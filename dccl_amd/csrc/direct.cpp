@@ -30,6 +30,7 @@ constexpr uint64_t kMagic = 0x3143504943434344ull;  // "DCCIPC1"
 constexpr uint32_t kMaxRanks = 64;
 constexpr size_t kHandleBytes = sizeof(hipIpcMemHandle_t);
 constexpr size_t kMaxOpenPerXport = 256;  // mappings kept open; the oldest is closed beyond this
+constexpr size_t kHostChainMaxBytes = size_t(64) << 20;  // staging limit of dccl_local_reduce_chain_host
 
 struct ShmSlot {
     unsigned char h_in[kHandleBytes];
@@ -349,6 +350,43 @@ ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t
     }
     if ((rc = copy_pairs(src, dst, slot, st)) != dccl::ncclSuccess) return fail(c, rc);
     return arrive(c, st);  // peers are done reading our buffers
+}
+
+bool host_direct_selected(const dcclComm* c, size_t slot_bytes) {
+    if (c->ipc != nullptr || c->rccl != nullptr || c->group == nullptr || c->world > kDirectMaxWorld) return false;
+    if (slot_bytes * c->world > kHostChainMaxBytes) return false;
+    const char* a = std::getenv("DCCL_ALLREDUCE_ALGORITHM");
+    if (a == nullptr || *a == 0) return true;
+    const std::string s(a);
+    return s == "auto" || s == "direct";
+}
+
+// The same choreography as direct_all_reduce on host memory: rank r reduces chunk r+1 from every rank's
+// input in the ring's order with one staged chain kernel (one GPU round trip instead of the ring's W-1),
+// then copies every other chunk from the rank that reduced it.  Every barrier is reached even after a
+// failed combine, so no rank is left waiting.
+ncclResult_t direct_all_reduce_host(dcclComm* c, const void* send, void* recv, size_t count, int dtype, int op) {
+    const uint32_t W = c->world, r = c->rank;
+    const size_t esz = size_of_dtype(dtype), slot_elems = count / W, slot = slot_elems * esz;
+    Group& g = *c->group;
+    g.pub_in[r] = send;
+    g.pub_out[r] = recv;
+    g.barrier();  // every rank's buffers are published and its inputs are final
+    const uint32_t mine = (r + 1) % W;
+    const void* sends[kDirectMaxWorld];
+    for (uint32_t j = 0; j + 1 < W; ++j)
+        sends[j] = static_cast<const unsigned char*>(g.pub_in[(mine + j) % W]) + mine * slot;
+    const ncclResult_t rc = static_cast<ncclResult_t>(dccl_local_reduce_chain_host(
+        sends, int(W - 1), static_cast<const unsigned char*>(send) + mine * slot,
+        static_cast<unsigned char*>(recv) + mine * slot, dtype, slot_elems, op));
+    g.barrier();  // every chunk reduced by its owner
+    if (rc == dccl::ncclSuccess)
+        for (uint32_t k = 0; k < W; ++k)
+            if (k != mine)  // chunk k lives on rank k-1
+                std::memcpy(static_cast<unsigned char*>(recv) + k * slot,
+                            static_cast<const unsigned char*>(g.pub_out[(k + W - 1) % W]) + k * slot, slot);
+    g.barrier();  // peers are done reading our buffers
+    return rc;
 }
 
 // ncclReduceScatter: the ring with rank maps (o+W-1)%W / (n+1)%W (dccl.cpp:551-698) leaves slot o on

@@ -149,6 +149,7 @@ public:
     int run(const unsigned char* send, unsigned char* recv, int dtype, size_t count, int op);
     int run_zero_copy(const unsigned char* send, unsigned char* recv, void* dsend, void* drecv, int dtype,
                       size_t count, int op);
+    int run_chain(const void* const* sends, int nsend, const void* own, void* dst, int dtype, size_t count, int op);
 
 private:
     int fail() { release(); return DCCL_UNHANDLED_DEVICE_ERROR; }
@@ -162,6 +163,9 @@ private:
                 if (e) (void)hipEventDestroy(e);
             sl = Slot{};
         }
+        if (chain_h_) (void)hipHostFree(chain_h_);
+        chain_h_ = nullptr;
+        chain_cap_ = 0;
         for (hipStream_t s : {in_, comp_, out_})
             if (s) (void)hipStreamDestroy(s);
         in_ = comp_ = out_ = nullptr;
@@ -185,6 +189,8 @@ private:
     hipStream_t in_ = nullptr, comp_ = nullptr, out_ = nullptr;
     Slot slots_[kSlots];
     std::unique_ptr<CopyPool> pool_;  // created at the first pageable bounce
+    void* chain_h_ = nullptr;         // pinned staging of the host chain combine, grown on demand
+    size_t chain_cap_ = 0;
 };
 
 // Page-locked host memory: returns the device-side alias the GPU can load/store through
@@ -294,6 +300,51 @@ int Stager::run(const unsigned char* send, unsigned char* recv, int dtype, size_
     return rc;
 }
 
+// Host chain combine, the host twin of dccl_local_reduce_chain: operands that are not page-locked are
+// bounced into one pinned staging area, one zero-copy chain kernel reads them all over PCIe in the
+// ring's order, and the result is copied back.  At most kChainMaxBytes of staging.
+constexpr size_t kChainMaxBytes = size_t(64) << 20;
+
+int Stager::run_chain(const void* const* sends, int nsend, const void* own, void* dst, int dtype, size_t count,
+                      int op) {
+    const size_t bytes = count * size_of_dtype(dtype), stride = (bytes + 255) / 256 * 256;
+    const size_t need = stride * size_t(nsend + 1);
+    if (need > kChainMaxBytes) return DCCL_INVALID_USAGE;
+    if (chain_cap_ < need) {
+        if (chain_h_) (void)hipHostFree(chain_h_);
+        chain_h_ = nullptr;
+        chain_cap_ = 0;
+        const size_t cap = need < (size_t(1) << 20) ? size_t(1) << 20 : need;
+        if (hipHostMalloc(&chain_h_, cap, hipHostMallocDefault) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
+        chain_cap_ = cap;
+    }
+    void* dbase = nullptr;
+    if (hipHostGetDevicePointer(&dbase, chain_h_, 0) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
+    auto* h = static_cast<unsigned char*>(chain_h_);
+    auto* d = static_cast<unsigned char*>(dbase);
+    const void* dsends[8];
+    for (int j = 0; j < nsend; ++j) {
+        if (const void* alias = pinned_device_alias(sends[j])) {
+            dsends[j] = alias;
+            continue;
+        }
+        bounce(h + size_t(j) * stride, sends[j], bytes);
+        dsends[j] = d + size_t(j) * stride;
+    }
+    void* down = pinned_device_alias(own);
+    void* ddst = pinned_device_alias(dst);
+    const bool staged = down == nullptr || ddst == nullptr;
+    unsigned char* hown = h + size_t(nsend) * stride;
+    if (staged) {  // own is staged and the kernel writes the result over it (own may alias dst)
+        bounce(hown, own, bytes);
+        down = ddst = d + size_t(nsend) * stride;
+    }
+    int rc = dccl_local_reduce_chain(dsends, nsend, down, ddst, dtype, count, op, comp_);
+    if (hipStreamSynchronize(comp_) != hipSuccess && rc == DCCL_SUCCESS) rc = DCCL_UNHANDLED_DEVICE_ERROR;
+    if (rc == DCCL_SUCCESS && staged) bounce(dst, hown, bytes);
+    return rc;
+}
+
 struct ThreadStagers {
     std::vector<std::unique_ptr<Stager>> per_device;
     Stager* get(int dev) {
@@ -323,6 +374,26 @@ extern "C" int dccl_local_reduce_host(const void* send, void* recv, int dtype, s
     int rc = st->init();
     if (rc != DCCL_SUCCESS) return rc;
     rc = st->run(static_cast<const unsigned char*>(send), static_cast<unsigned char*>(recv), dtype, count, op);
+    (void)hipSetDevice(dev);
+    return rc;
+}
+
+extern "C" int dccl_local_reduce_chain_host(const void* const* sends, int nsend, const void* own, void* dst,
+                                            int dtype, size_t count, int op) {
+    const int v = validate(dtype, op);
+    if (v != DCCL_SUCCESS) return v;
+    if (nsend < 1 || nsend > 8 || sends == nullptr) return DCCL_INVALID_ARGUMENT;
+    if (count == 0) return DCCL_SUCCESS;
+    if (own == nullptr || dst == nullptr) return DCCL_INVALID_ARGUMENT;
+    for (int k = 0; k < nsend; ++k)
+        if (sends[k] == nullptr) return DCCL_INVALID_ARGUMENT;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
+    Stager* st = t_stagers.get(dev);
+    if (st == nullptr) return DCCL_UNHANDLED_DEVICE_ERROR;
+    int rc = st->init();
+    if (rc != DCCL_SUCCESS) return rc;
+    rc = st->run_chain(sends, nsend, own, dst, dtype, count, op);
     (void)hipSetDevice(dev);
     return rc;
 }

@@ -93,6 +93,15 @@ int dccl_copy_multi(const void* const* srcs, void* const* dsts, int npairs, size
  */
 int dccl_local_reduce_host(const void* send, void* recv, int dtype, size_t count, int op);
 
+/*
+ * Host chain combine, synchronous: dccl_local_reduce_chain on host pointers (the direct all_reduce of
+ * in-process ranks on host buffers).  Operands are staged through pinned memory and
+ * combined by one zero-copy kernel on the calling thread's current HIP device; registered operands
+ * are read in place.  ncclInvalidUsage when (nsend + 1) operands exceed 64 MiB of staging.
+ */
+int dccl_local_reduce_chain_host(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
+                                 size_t count, int op);
+
 /* Page-lock a host range for direct DMA by dccl_local_reduce_host
  * (the role of dcclRegisterCacheMemory, /root/reference/src/core/dccl.cpp:503-549). */
 int dccl_register_host_memory(void* buffer, size_t size);

@@ -66,6 +66,11 @@ def test_validation_without_gpu():
     assert d.local_reduce_host(0, 0, 9, 0, 3) == 0
     assert d.local_reduce_multi([0] * 9, 0, 7, 16, 0) == 4
     assert d.local_reduce_multi([0], 0, 7, 16, 4) == 5
+    assert d.local_reduce_chain_host([], 8, 8, 7, 16, 0) == 4        # nsend 0
+    assert d.local_reduce_chain_host([8] * 9, 8, 8, 7, 16, 0) == 4   # nsend 9
+    assert d.local_reduce_chain_host([8], 8, 8, 7, 16, 4) == 5       # Avg
+    assert d.local_reduce_chain_host([8], 8, 8, 7, 0, 0) == 0        # count 0
+    assert d.local_reduce_chain_host([0], 8, 8, 7, 16, 0) == 4       # NULL send
 
 
 def test_enum_values_match_reference_header():

@@ -175,7 +175,7 @@ def test_rabenseifner_simulation_cpu():
 
 # ------------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("gpu_flag,algo", [(-1, "ring"), (0, "ring"), (0, "direct"), (0, "auto")])
+@pytest.mark.parametrize("gpu_flag,algo", [(-1, "ring"), (-1, "auto"), (0, "ring"), (0, "direct"), (0, "auto")])
 @pytest.mark.parametrize("kind", ["float32", "uint32"])
 def test_c1_known_answers(gpu_flag, algo, kind):
     """BASELINE C1: dccl_cli -a all_reduce -c 1024, 4 ranks; the reference's bit patterns, through the

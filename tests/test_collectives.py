@@ -82,11 +82,10 @@ def _expected_allreduce(inputs, dt, op):
 @pytest.mark.parametrize("device", [True, False])
 @pytest.mark.parametrize("W,dt,op", [(4, 7, 0), (3, 9, 1), (2, 2, 3), (5, 8, 2)])
 def test_all_reduce_threads(W, dt, op, device, algo, monkeypatch):
-    """Thread ranks, bit-exact against the ring simulation + oracle.  algo "" is the default (device
-    buffers take the direct collectives, host buffers the ring); "ring" forces the ring."""
+    """Thread ranks, bit-exact against the ring simulation + oracle.  algo "" is the default (the direct
+    collectives: peer reads on device buffers, one staged chain combine per rank on host buffers);
+    "ring" forces the ring."""
     import torch
-    if algo == "ring" and not device:
-        pytest.skip("host buffers always take the ring")
     monkeypatch.setenv("DCCL_ALLREDUCE_ALGORITHM", algo)
     rng = np.random.default_rng(W * 10 + dt)
     n = W * 40961

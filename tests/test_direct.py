@@ -50,6 +50,39 @@ def test_ipc_comm_rejects_bad_rank_cpu():
 
 # ----------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
+@pytest.mark.parametrize("dt", [0, 2, 6, 7, 8, 9])
+def test_chain_host_against_oracle(gpu, dt):
+    """dccl_local_reduce_chain_host: pageable and registered operands, own == dst and own != dst,
+    odd sizes and byte offsets; the staging limit answers ncclInvalidUsage."""
+    import dccl_amd
+    from tests.test_gpu_parity import rand_inputs
+    from tests.test_oracle import fp_equal
+    rng = np.random.default_rng(50 + dt)
+    for op in (0, 1, 2, 3):
+        for k, n, pinned, same in ((1, 1, False, True), (3, 4099, False, True), (7, 65537, False, False),
+                                   (2, 1000, True, True), (4, 30001, True, False)):
+            arrs = [rand_inputs(rng, dt, n)[0] for _ in range(k + 1)]
+            sends, own = arrs[:k], arrs[k].copy()
+            want = chain_expected(sends, arrs[k], dt, op)
+            dst = own if same else np.zeros_like(own)
+            regs = (sends + [own] + ([] if same else [dst])) if pinned else []
+            for x in regs:
+                assert dccl_amd.register_host_memory(x.ctypes.data, x.nbytes) == 0
+            try:
+                assert dccl_amd.local_reduce_chain_host([s.ctypes.data for s in sends], own.ctypes.data,
+                                                        dst.ctypes.data, dt, n, op) == 0
+            finally:
+                for x in regs:
+                    dccl_amd.deregister_host_memory(x.ctypes.data)
+            assert fp_equal(dst, want, dt), (op, k, n, pinned, same)
+            if not same:
+                assert own.tobytes() == arrs[k].tobytes()
+    big = np.zeros((9 << 20) // 4, np.float32)  # 8 sends + own of 9 MiB > 64 MiB of staging
+    assert dccl_amd.local_reduce_chain_host([big.ctypes.data] * 8, big.ctypes.data, big.ctypes.data, 7,
+                                            big.size, 0) == 5
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dt", list(range(10)))
 def test_chain_against_oracle(gpu, dt):
     import torch

@@ -42,6 +42,7 @@ static void cpu_checks(void) {
     const void* sends[1] = {a};
     CHECK(dccl_local_reduce_multi(sends, 0, b, 7, 4, 0, NULL) == DCCL_INVALID_ARGUMENT);
     CHECK(dccl_local_reduce_chain(sends, 9, a, b, 7, 4, 0, NULL) == DCCL_INVALID_ARGUMENT);
+    CHECK(dccl_local_reduce_chain_host(sends, 0, a, b, 7, 4, 0) == DCCL_INVALID_ARGUMENT);
     CHECK(dccl_synth_fill(NULL, 7, 16, 0, 1, 0, NULL) == DCCL_INVALID_ARGUMENT);
     CHECK(dccl_copy_multi(NULL, NULL, 0, 16, NULL) == DCCL_SUCCESS);
     CHECK(dccl_all_reduce(a, b, 4, 7, 0, NULL, NULL) == DCCL_INVALID_ARGUMENT); /* null communicator */
