@@ -399,6 +399,8 @@ ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recv
     const size_t slot = recvcount * size_of_dtype(datatype), total = slot * W;
     if (W > 1 && dev && direct_selected(comm))
         return direct_reduce_scatter(comm, sendbuff, recvbuff, recvcount, datatype, op, stream);
+    if (W > 1 && !dev && host_direct_selected(comm, slot))
+        return direct_reduce_scatter_host(comm, sendbuff, recvbuff, recvcount, datatype, op);
     if ((rc = ensure_work(comm, total, dev)) != ncclSuccess) return rc;
     void* work = dev ? comm->dev_work : comm->host_work;
     if ((rc = copy_bytes(work, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:585-609

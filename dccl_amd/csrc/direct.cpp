@@ -389,6 +389,25 @@ ncclResult_t direct_all_reduce_host(dcclComm* c, const void* send, void* recv, s
     return rc;
 }
 
+// ncclReduceScatter on host memory: slot r reduced from every rank's input in the order of the ring with
+// ncclReduceScatter's maps (as direct_reduce_scatter), one staged chain combine.
+ncclResult_t direct_reduce_scatter_host(dcclComm* c, const void* send, void* recv, size_t recvcount, int dtype,
+                                        int op) {
+    const uint32_t W = c->world, r = c->rank;
+    const size_t slot = recvcount * size_of_dtype(dtype);
+    Group& g = *c->group;
+    g.pub_in[r] = send;
+    g.pub_out[r] = recv;
+    g.barrier();
+    const void* sends[kDirectMaxWorld];
+    for (uint32_t j = 0; j + 1 < W; ++j)
+        sends[j] = static_cast<const unsigned char*>(g.pub_in[(r + 1 + j) % W]) + r * slot;
+    const ncclResult_t rc = static_cast<ncclResult_t>(dccl_local_reduce_chain_host(
+        sends, int(W - 1), static_cast<const unsigned char*>(send) + r * slot, recv, dtype, recvcount, op));
+    g.barrier();  // peers are done reading our input
+    return rc;
+}
+
 // ncclReduceScatter: the ring with rank maps (o+W-1)%W / (n+1)%W (dccl.cpp:551-698) leaves slot o on
 // rank o, combined in the order o+1, o+2, ..., o-1, o.
 ncclResult_t direct_reduce_scatter(dcclComm* c, const void* send, void* recv, size_t recvcount, int dtype, int op,

@@ -48,6 +48,8 @@ ncclResult_t direct_all_reduce(dccl::dcclComm* c, const void* send, void* recv, 
 bool host_direct_selected(const dccl::dcclComm* c, size_t slot_bytes);
 ncclResult_t direct_all_reduce_host(dccl::dcclComm* c, const void* send, void* recv, size_t count, int dtype,
                                     int op);
+ncclResult_t direct_reduce_scatter_host(dccl::dcclComm* c, const void* send, void* recv, size_t recvcount,
+                                        int dtype, int op);
 ncclResult_t direct_reduce_scatter(dccl::dcclComm* c, const void* send, void* recv, size_t recvcount, int dtype,
                                    int op, hipStream_t st);
 ncclResult_t direct_reduce(dccl::dcclComm* c, const void* send, void* recv, size_t count, int dtype, int op,

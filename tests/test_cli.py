@@ -217,8 +217,8 @@ def test_cli_unknown_algorithm_rejected_cpu():
 def test_cli_apis_against_oracle(api, gpu_flag, device, algo):
     if api in ("all_gather", "broadcast") and algo == "ring-scratch":
         pytest.skip("no combine in this api")
-    if algo == "direct" and not device:
-        pytest.skip("the direct collectives read peers' device memory")
+    if algo == "direct" and not device and api not in ("all_reduce", "reduce_scatter"):
+        pytest.skip("host buffers take the direct choreography for all_reduce and reduce_scatter only")
     env = {"DCCL_RS_SCRATCH": "1" if algo == "ring-scratch" else "0",
            "DCCL_ALLREDUCE_ALGORITHM": "direct" if algo == "direct" else "ring"}
     for W, n, dtype, op in [(4, 1024, "float32", 0), (3, 3 * 1001, "float64", 1), (2, 4096, "int8", 2),
