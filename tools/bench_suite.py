@@ -203,7 +203,8 @@ def host(results):
             rows.append({"bytes_per_operand": nbytes, "pinned": pinned, "ms": round(t * 1e3, 3),
                          "payload_gib_s": round(nbytes / t / 2**30, 2)})
             print("host", rows[-1], flush=True)
-    results["host_staged"] = {"zero_copy_max": os.environ.get("DCCL_HOST_ZEROCOPY_MAX", "default (256 KiB)"),
+    results["host_staged"] = {"zero_copy_max": os.environ.get("DCCL_HOST_ZEROCOPY_MAX", "default (unlimited)"),
+                              "copy_threads": os.environ.get("DCCL_HOST_COPY_THREADS", "default (4)"),
                               "rows": rows}
 
 
