@@ -116,6 +116,27 @@ def test_all_reduce_threads(W, dt, op, device, algo, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.slow
+def test_all_reduce_threads_host_large():
+    """Host buffers beyond one staging area: the direct all_reduce stages each rank's chain in pieces
+    (W = 4, 18 MiB chunks, W copies > 64 MiB); bit-exact against the ring simulation + oracle."""
+    W, dt, op = 4, 7, 0
+    n = W * ((18 << 20) // 4 + 37)
+    rng = np.random.default_rng(77)
+    inputs = [rng.standard_normal(n).astype(np.float32) for _ in range(W)]
+    want = _expected_allreduce(inputs, dt, op)
+
+    def body(comm, r):
+        buf = inputs[r].copy()
+        assert comm.all_reduce(buf.ctypes.data, buf.ctypes.data, n, dt, op) == 0
+        return buf
+
+    out = run_ranks(W, body)
+    for r in range(W):
+        assert out[r].tobytes() == want[r].tobytes(), r
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("algo", ["", "ring"])
 def test_reduce_scatter_threads_device(algo, monkeypatch):
     import torch
