@@ -30,7 +30,6 @@ constexpr uint64_t kMagic = 0x3143504943434344ull;  // "DCCIPC1"
 constexpr uint32_t kMaxRanks = 64;
 constexpr size_t kHandleBytes = sizeof(hipIpcMemHandle_t);
 constexpr size_t kMaxOpenPerXport = 256;  // mappings kept open; the oldest is closed beyond this
-constexpr size_t kHostChainMaxBytes = size_t(64) << 20;  // staging limit of dccl_local_reduce_chain_host
 
 struct ShmSlot {
     unsigned char h_in[kHandleBytes];
@@ -352,25 +351,8 @@ ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t
     return arrive(c, st);  // peers are done reading our buffers
 }
 
-// Host chain combine of W sources of `elems` elements at byte offset `off`, in pieces whose W staged
-// copies fit dccl_local_reduce_chain_host's staging.
-static ncclResult_t host_chain_pieces(const void* const* srcs, int nsrc, const unsigned char* own, unsigned char* dst,
-                                      size_t elems, int dtype, int op) {
-    const size_t esz = size_of_dtype(dtype);
-    const size_t piece = (kHostChainMaxBytes / size_t(nsrc + 1) - 256) / esz / 64 * 64;  // elements
-    const void* s[kDirectMaxWorld];
-    ncclResult_t rc = dccl::ncclSuccess;
-    for (size_t o = 0; o < elems && rc == dccl::ncclSuccess; o += piece) {
-        const size_t n = elems - o < piece ? elems - o : piece;
-        for (int j = 0; j < nsrc; ++j) s[j] = static_cast<const unsigned char*>(srcs[j]) + o * esz;
-        rc = static_cast<ncclResult_t>(
-            dccl_local_reduce_chain_host(s, nsrc, own + o * esz, dst + o * esz, dtype, n, op));
-    }
-    return rc;
-}
-
 bool host_direct_selected(const dcclComm* c, size_t slot_bytes) {
-    (void)slot_bytes;  // any size: the chain is staged in pieces
+    (void)slot_bytes;  // any size: dccl_local_reduce_chain_host stages in pieces
     if (c->ipc != nullptr || c->rccl != nullptr || c->group == nullptr || c->world > kDirectMaxWorld) return false;
     const char* a = std::getenv("DCCL_ALLREDUCE_ALGORITHM");
     if (a == nullptr || *a == 0) return true;
@@ -393,8 +375,9 @@ ncclResult_t direct_all_reduce_host(dcclComm* c, const void* send, void* recv, s
     const void* sends[kDirectMaxWorld];
     for (uint32_t j = 0; j + 1 < W; ++j)
         sends[j] = static_cast<const unsigned char*>(g.pub_in[(mine + j) % W]) + mine * slot;
-    const ncclResult_t rc = host_chain_pieces(sends, int(W - 1), static_cast<const unsigned char*>(send) + mine * slot,
-                                              static_cast<unsigned char*>(recv) + mine * slot, slot_elems, dtype, op);
+    const ncclResult_t rc = static_cast<ncclResult_t>(dccl_local_reduce_chain_host(
+        sends, int(W - 1), static_cast<const unsigned char*>(send) + mine * slot,
+        static_cast<unsigned char*>(recv) + mine * slot, dtype, slot_elems, op));
     g.barrier();  // every chunk reduced by its owner
     if (rc == dccl::ncclSuccess)
         for (uint32_t k = 0; k < W; ++k)
@@ -418,8 +401,8 @@ ncclResult_t direct_reduce_scatter_host(dcclComm* c, const void* send, void* rec
     const void* sends[kDirectMaxWorld];
     for (uint32_t j = 0; j + 1 < W; ++j)
         sends[j] = static_cast<const unsigned char*>(g.pub_in[(r + 1 + j) % W]) + r * slot;
-    const ncclResult_t rc = host_chain_pieces(sends, int(W - 1), static_cast<const unsigned char*>(send) + r * slot,
-                                              static_cast<unsigned char*>(recv), recvcount, dtype, op);
+    const ncclResult_t rc = static_cast<ncclResult_t>(dccl_local_reduce_chain_host(
+        sends, int(W - 1), static_cast<const unsigned char*>(send) + r * slot, recv, dtype, recvcount, op));
     g.barrier();  // peers are done reading our input
     return rc;
 }

@@ -43,8 +43,8 @@ ncclResult_t direct_all_reduce(dccl::dcclComm* c, const void* send, void* recv, 
                                hipStream_t st);
 
 // Host buffers of an in-process group: the direct all_reduce with the chain combine staged through the
-// GPU (dccl_local_reduce_chain_host, in pieces whose W staged copies fit its 64 MiB staging) and the
-// all-gather by memcpy from the owners' buffers.  Selected like direct_selected().
+// GPU (dccl_local_reduce_chain_host, staged in double-buffered pieces) and the all-gather by memcpy from
+// the owners' buffers.  Selected like direct_selected().
 bool host_direct_selected(const dccl::dcclComm* c, size_t slot_bytes);
 ncclResult_t direct_all_reduce_host(dccl::dcclComm* c, const void* send, void* recv, size_t count, int dtype,
                                     int op);

@@ -142,6 +142,8 @@ public:
             for (hipEvent_t* e : {&sl.in_done, &sl.comp_done, &sl.out_done})
                 if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return fail();
         }
+        for (hipEvent_t& e : chain_ev_)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail();
         ready_ = true;
         return DCCL_SUCCESS;
     }
@@ -166,6 +168,10 @@ private:
         if (chain_h_) (void)hipHostFree(chain_h_);
         chain_h_ = nullptr;
         chain_cap_ = 0;
+        for (hipEvent_t& e : chain_ev_) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
         for (hipStream_t s : {in_, comp_, out_})
             if (s) (void)hipStreamDestroy(s);
         in_ = comp_ = out_ = nullptr;
@@ -189,8 +195,9 @@ private:
     hipStream_t in_ = nullptr, comp_ = nullptr, out_ = nullptr;
     Slot slots_[kSlots];
     std::unique_ptr<CopyPool> pool_;  // created at the first pageable bounce
-    void* chain_h_ = nullptr;         // pinned staging of the host chain combine, grown on demand
+    void* chain_h_ = nullptr;         // pinned staging of the host chain combine (two halves), grown on demand
     size_t chain_cap_ = 0;
+    hipEvent_t chain_ev_[2] = {};     // last kernel reading each half
 };
 
 // Page-locked host memory: returns the device-side alias the GPU can load/store through
@@ -300,16 +307,33 @@ int Stager::run(const unsigned char* send, unsigned char* recv, int dtype, size_
     return rc;
 }
 
-// Host chain combine, the host twin of dccl_local_reduce_chain: operands that are not page-locked are
-// bounced into one pinned staging area, one zero-copy chain kernel reads them all over PCIe in the
-// ring's order, and the result is copied back.  At most kChainMaxBytes of staging.
-constexpr size_t kChainMaxBytes = size_t(64) << 20;
+// Host chain combine, the host twin of dccl_local_reduce_chain.  Operands that are not page-locked are
+// bounced into pinned staging and one zero-copy chain kernel per piece reads them over PCIe in the
+// ring's order; the result is copied back.  Pieces alternate between two halves of the staging area, so
+// the bounce of piece j overlaps the kernel of piece j-1.  Page-locked operands are read in place.
+constexpr size_t kChainHalfBytes = size_t(32) << 20;
 
 int Stager::run_chain(const void* const* sends, int nsend, const void* own, void* dst, int dtype, size_t count,
                       int op) {
-    const size_t bytes = count * size_of_dtype(dtype), stride = (bytes + 255) / 256 * 256;
-    const size_t need = stride * size_t(nsend + 1);
-    if (need > kChainMaxBytes) return DCCL_INVALID_USAGE;
+    const size_t esz = size_of_dtype(dtype);
+    const void* as[8];
+    bool all_pinned = true;
+    for (int k = 0; k < nsend; ++k)
+        if ((as[k] = pinned_device_alias(sends[k])) == nullptr) all_pinned = false;
+    void* a_own = pinned_device_alias(own);
+    void* a_dst = pinned_device_alias(dst);
+    const bool stage_own = a_own == nullptr || a_dst == nullptr;
+    int rc = DCCL_SUCCESS;
+    if (all_pinned && !stage_own) {  // everything page-locked: one kernel, nothing staged
+        rc = dccl_local_reduce_chain(as, nsend, a_own, a_dst, dtype, count, op, comp_);
+        if (hipStreamSynchronize(comp_) != hipSuccess && rc == DCCL_SUCCESS) rc = DCCL_UNHANDLED_DEVICE_ERROR;
+        return rc;
+    }
+    const size_t slot_max = kChainHalfBytes / size_t(nsend + 1) / 256 * 256;  // bytes per operand per half
+    const size_t piece = count * esz <= slot_max ? count : slot_max / esz;    // elements
+    const size_t npieces = (count + piece - 1) / piece;
+    const size_t ps = (piece * esz + 255) / 256 * 256, half = ps * size_t(nsend + 1);
+    const size_t need = npieces > 1 ? 2 * half : half;
     if (chain_cap_ < need) {
         if (chain_h_) (void)hipHostFree(chain_h_);
         chain_h_ = nullptr;
@@ -322,26 +346,45 @@ int Stager::run_chain(const void* const* sends, int nsend, const void* own, void
     if (hipHostGetDevicePointer(&dbase, chain_h_, 0) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
     auto* h = static_cast<unsigned char*>(chain_h_);
     auto* d = static_cast<unsigned char*>(dbase);
-    const void* dsends[8];
-    for (int j = 0; j < nsend; ++j) {
-        if (const void* alias = pinned_device_alias(sends[j])) {
-            dsends[j] = alias;
-            continue;
+    auto elems = [&](size_t j) { return j + 1 == npieces ? count - j * piece : piece; };
+    // wait for piece j's kernel, then copy its result back to dst
+    auto finish = [&](size_t j) {
+        if (hipEventSynchronize(chain_ev_[j % 2]) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
+        if (stage_own)
+            bounce(static_cast<unsigned char*>(dst) + j * piece * esz, h + (j % 2) * half + size_t(nsend) * ps,
+                   elems(j) * esz);
+        return DCCL_SUCCESS;
+    };
+    size_t launched = 0, returned = 0;
+    for (size_t j = 0; j < npieces && rc == DCCL_SUCCESS; ++j) {
+        if (j >= 2 && (rc = finish(returned++)) != DCCL_SUCCESS) break;  // frees this half
+        const size_t o = j * piece * esz, n = elems(j), hb = (j % 2) * half;
+        const void* ds[8];
+        for (int k = 0; k < nsend; ++k) {
+            if (as[k] != nullptr) {
+                ds[k] = static_cast<const unsigned char*>(as[k]) + o;
+                continue;
+            }
+            bounce(h + hb + size_t(k) * ps, static_cast<const unsigned char*>(sends[k]) + o, n * esz);
+            ds[k] = d + hb + size_t(k) * ps;
         }
-        bounce(h + size_t(j) * stride, sends[j], bytes);
-        dsends[j] = d + size_t(j) * stride;
+        const void* down;
+        void* ddst;
+        if (stage_own) {  // own is staged and the kernel writes the result over it (own may alias dst)
+            bounce(h + hb + size_t(nsend) * ps, static_cast<const unsigned char*>(own) + o, n * esz);
+            down = ddst = d + hb + size_t(nsend) * ps;
+        } else {
+            down = static_cast<const unsigned char*>(a_own) + o;
+            ddst = static_cast<unsigned char*>(a_dst) + o;
+        }
+        rc = dccl_local_reduce_chain(ds, nsend, down, ddst, dtype, n, op, comp_);
+        if (rc == DCCL_SUCCESS && hipEventRecord(chain_ev_[j % 2], comp_) != hipSuccess)
+            rc = DCCL_UNHANDLED_DEVICE_ERROR;
+        if (rc == DCCL_SUCCESS) launched = j + 1;
     }
-    void* down = pinned_device_alias(own);
-    void* ddst = pinned_device_alias(dst);
-    const bool staged = down == nullptr || ddst == nullptr;
-    unsigned char* hown = h + size_t(nsend) * stride;
-    if (staged) {  // own is staged and the kernel writes the result over it (own may alias dst)
-        bounce(hown, own, bytes);
-        down = ddst = d + size_t(nsend) * stride;
-    }
-    int rc = dccl_local_reduce_chain(dsends, nsend, down, ddst, dtype, count, op, comp_);
+    // no kernel may still read the staging area after return, even after an error
     if (hipStreamSynchronize(comp_) != hipSuccess && rc == DCCL_SUCCESS) rc = DCCL_UNHANDLED_DEVICE_ERROR;
-    if (rc == DCCL_SUCCESS && staged) bounce(dst, hown, bytes);
+    while (rc == DCCL_SUCCESS && returned < launched) rc = finish(returned++);
     return rc;
 }
 

@@ -96,8 +96,8 @@ int dccl_local_reduce_host(const void* send, void* recv, int dtype, size_t count
 /*
  * Host chain combine, synchronous: dccl_local_reduce_chain on host pointers (the direct all_reduce of
  * in-process ranks on host buffers).  Operands are staged through pinned memory and
- * combined by one zero-copy kernel on the calling thread's current HIP device; registered operands
- * are read in place.  ncclInvalidUsage when (nsend + 1) operands exceed 64 MiB of staging.
+ * combined by zero-copy kernels on the calling thread's current HIP device, in pieces whose staging
+ * overlaps the previous piece's kernel; registered operands are read in place.
  */
 int dccl_local_reduce_chain_host(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
                                  size_t count, int op);

@@ -52,8 +52,8 @@ def test_ipc_comm_rejects_bad_rank_cpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt", [0, 2, 6, 7, 8, 9])
 def test_chain_host_against_oracle(gpu, dt):
-    """dccl_local_reduce_chain_host: pageable and registered operands, own == dst and own != dst,
-    odd sizes and byte offsets; the staging limit answers ncclInvalidUsage."""
+    """dccl_local_reduce_chain_host: pageable and registered operands, own == dst and own != dst, odd
+    sizes, and operands larger than one staging half (several double-buffered pieces)."""
     import dccl_amd
     from tests.test_gpu_parity import rand_inputs
     from tests.test_oracle import fp_equal
@@ -77,9 +77,18 @@ def test_chain_host_against_oracle(gpu, dt):
             assert fp_equal(dst, want, dt), (op, k, n, pinned, same)
             if not same:
                 assert own.tobytes() == arrs[k].tobytes()
-    big = np.zeros((9 << 20) // 4, np.float32)  # 8 sends + own of 9 MiB > 64 MiB of staging
-    assert dccl_amd.local_reduce_chain_host([big.ctypes.data] * 8, big.ctypes.data, big.ctypes.data, 7,
-                                            big.size, 0) == 5
+    # 3 sends + own of 21 MiB + 5 elements: 8 MiB staging slots per half, 3 pieces; one send registered
+    n = (21 << 20) // 4 + 5
+    arrs = [rng.standard_normal(n).astype(np.float32) for _ in range(4)]
+    want = chain_expected(arrs[:3], arrs[3], 7, 0)
+    own = arrs[3].copy()
+    assert dccl_amd.register_host_memory(arrs[1].ctypes.data, arrs[1].nbytes) == 0
+    try:
+        assert dccl_amd.local_reduce_chain_host([a.ctypes.data for a in arrs[:3]], own.ctypes.data, own.ctypes.data,
+                                                7, n, 0) == 0
+    finally:
+        dccl_amd.deregister_host_memory(arrs[1].ctypes.data)
+    assert own.tobytes() == want.tobytes()
 
 
 @pytest.mark.gpu
