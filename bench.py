@@ -349,12 +349,15 @@ def allgather_compare(comms: dict, world: int, rank: int, dev, st, count: int, i
         torch.cuda.synchronize(dev)
         ok = bool(torch.equal(y, want))
         dist.barrier()
+        each = []
         t0 = time.perf_counter()
         for _ in range(iters):
+            t1 = time.perf_counter()
             dccl_amd.check(comm.all_gather(mine.data_ptr(), y.data_ptr(), per, 2, st.cuda_stream), name)
-        torch.cuda.synchronize(dev)
+            torch.cuda.synchronize(dev)
+            each.append((time.perf_counter() - t1) * 1e3)
         t = (time.perf_counter() - t0) / iters
-        res[name] = {"bit_exact": ok, "ms": round(t * 1e3, 3),
+        res[name] = {"bit_exact": ok, "ms": round(t * 1e3, 3), "ms_each": [round(x, 3) for x in each],
                      "busbw_gb_s": round((world - 1) * per * 4 / t / 1e9, 1)}
     if dist.get_backend() == "nccl":
         dist.all_gather_into_tensor(y, mine)

@@ -36,7 +36,10 @@ void Group::barrier() {
     lk.unlock();
     const auto start = std::chrono::steady_clock::now();
     for (uint32_t i = 1; barrier_gen_.load(std::memory_order_acquire) == gen; ++i) {
-        if ((i & 1023) == 0 && std::chrono::steady_clock::now() - start > std::chrono::milliseconds(2)) break;
+        if ((i & 1023) == 0) {
+            if (std::chrono::steady_clock::now() - start > std::chrono::milliseconds(2)) break;
+            std::this_thread::yield();  // a rank without a core of its own gets one
+        }
         __builtin_ia32_pause();
     }
     lk.lock();

@@ -98,6 +98,7 @@ ncclResult_t shm_barrier(IpcXport* x) {
             return dccl::ncclSystemError;
         }
         if (now - start > kSpin) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        else std::this_thread::yield();  // a peer without a core of its own gets one
     }
     return dccl::ncclSuccess;
 }
