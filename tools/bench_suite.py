@@ -101,16 +101,24 @@ def c4(results):
         sets = max(1, min(64, (512 << 20) // (2 * nbytes)))  # rotate so launches read cold lines
         if nbytes >= 1 << 32:
             sets = 1
-        bufs = [(fill(nbytes, 7, 0, 2 * i), fill(nbytes, 7, 0, 2 * i + 1)) for i in range(sets)]
-        fns = [lambda s=s, r=r: dccl_amd.local_reduce(s.data_ptr(), r.data_ptr(), 7, n, 0, st) for s, r in bufs]
-        med, mn = time_launches(fns)
-        gbs = 3 * nbytes / (med * 1e-3) / 1e9
-        rows.append({"bytes_per_operand": nbytes, "ms": round(med, 5), "gb_s": round(gbs, 1),
-                     "gib_s_traffic": round(3 * nbytes / (med * 1e-3) / 2**30, 1), "frac": round(gbs / PEAK, 4),
-                     "buffer_sets": sets, "regime": "mall" if 2 * nbytes * sets <= MALL else "hbm"})
-        print("c4", nbytes, rows[-1]["gb_s"], rows[-1]["regime"], flush=True)
-        del bufs, fns
-        torch.cuda.empty_cache()
+        row = {"bytes_per_operand": nbytes, "buffer_sets": sets, "regime": "mall" if 2 * nbytes * sets <= MALL else "hbm"}
+        # bench.py's pooled pair first (the headline layout), then separately allocated operands
+        for layout in ("pooled", "separate"):
+            if layout == "pooled":
+                bufs = [pooled(nbytes, 7, 0, 2 * i) for i in range(sets)]
+            else:
+                bufs = [(fill(nbytes, 7, 0, 2 * i), fill(nbytes, 7, 0, 2 * i + 1)) for i in range(sets)]
+            fns = [lambda s=s, r=r: dccl_amd.local_reduce(s.data_ptr(), r.data_ptr(), 7, n, 0, st) for s, r in bufs]
+            med, mn = time_launches(fns)
+            gbs = 3 * nbytes / (med * 1e-3) / 1e9
+            key = "" if layout == "pooled" else "separate_"
+            row.update({f"{key}ms": round(med, 5), f"{key}gb_s": round(gbs, 1), f"{key}frac": round(gbs / PEAK, 4)})
+            if layout == "pooled":
+                row["gib_s_traffic"] = round(3 * nbytes / (med * 1e-3) / 2**30, 1)
+            del bufs, fns
+            torch.cuda.empty_cache()
+        rows.append(row)
+        print("c4", nbytes, row["gb_s"], row["separate_gb_s"], row["regime"], flush=True)
     results["c4"] = rows
 
 
@@ -149,14 +157,20 @@ def c2(results):
     st = torch.cuda.current_stream().cuda_stream
     nbytes = 256 << 20
     n = nbytes // 4
-    s, r = fill(nbytes, 7, 0, 1), fill(nbytes, 7, 0, 2)
-    s2, r2 = fill(nbytes, 7, 0, 3), fill(nbytes, 7, 0, 4)
-    fns = [lambda: dccl_amd.local_reduce(s.data_ptr(), r.data_ptr(), 7, n, 0, st),
-           lambda: dccl_amd.local_reduce(s2.data_ptr(), r2.data_ptr(), 7, n, 0, st)]
-    med, mn = time_launches(fns)
-    gbs = 3 * nbytes / (med * 1e-3) / 1e9
-    results["c2"] = {"bytes_per_operand": nbytes, "ms": round(med, 4), "gb_s": round(gbs, 1),
-                     "frac": round(gbs / PEAK, 4), "note": "2 buffer sets rotated (1 GiB working set)"}
+    res = {"bytes_per_operand": nbytes, "note": "2 buffer sets rotated (1 GiB working set); pooled = bench.py's "
+                                                 "layout, separate = separately allocated operands"}
+    for layout in ("pooled", "separate"):
+        sets = [pooled(nbytes, 7, 0, 2 * i) if layout == "pooled" else (fill(nbytes, 7, 0, 2 * i + 1),
+                                                                        fill(nbytes, 7, 0, 2 * i + 2))
+                for i in range(2)]
+        fns = [lambda s=s, r=r: dccl_amd.local_reduce(s.data_ptr(), r.data_ptr(), 7, n, 0, st) for s, r in sets]
+        med, mn = time_launches(fns)
+        gbs = 3 * nbytes / (med * 1e-3) / 1e9
+        key = "" if layout == "pooled" else "separate_"
+        res.update({f"{key}ms": round(med, 4), f"{key}gb_s": round(gbs, 1), f"{key}frac": round(gbs / PEAK, 4)})
+        del sets, fns
+        torch.cuda.empty_cache()
+    results["c2"] = res
     print("c2", results["c2"], flush=True)
 
 
