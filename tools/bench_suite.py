@@ -175,23 +175,40 @@ def c2(results):
 
 
 def kway(results, mib=256):
+    """k-way combine, k = 1..8: separately allocated operands, and the nine operands carved from one
+    allocation with a 4 KiB x (j+1) stagger between operand j and j+1 (bench.py's pooled layout
+    generalised, as tools/tune_multi.py's "staggered")."""
     st = torch.cuda.current_stream().cuda_stream
     nbytes = mib << 20
     n = nbytes // 4
-    sends = [fill(nbytes, 7, 0, 10 + k) for k in range(8)]
-    r = fill(nbytes, 7, 0, 99)
-    rows = []
-    for k in range(1, 9):
-        ptrs = [x.data_ptr() for x in sends[:k]]
-        fn = lambda ptrs=ptrs: dccl_amd.local_reduce_multi(ptrs, r.data_ptr(), 7, n, 0, st)
-        med, _ = time_launches([fn])
-        seq = lambda ptrs=ptrs: [dccl_amd.local_reduce(p, r.data_ptr(), 7, n, 0, st) for p in ptrs]
-        med_seq, _ = time_launches([seq])
-        gbs = (k + 2) * nbytes / (med * 1e-3) / 1e9
-        rows.append({"k": k, "ms": round(med, 4), "gb_s": round(gbs, 1), "frac": round(gbs / PEAK, 4),
-                     "ms_k_single_launches": round(med_seq, 4), "speedup": round(med_seq / med, 2)})
-        print("kway", rows[-1], flush=True)
-    results["kway"] = {"bytes_per_operand": nbytes, "rows": rows}
+    out = {"bytes_per_operand": nbytes}
+    for layout in ("separate", "staggered"):
+        if layout == "separate":
+            keep = [fill(nbytes, 7, 0, 10 + k) for k in range(8)] + [fill(nbytes, 7, 0, 99)]
+            ptrs_all = [x.data_ptr() for x in keep]
+        else:
+            pool = torch.empty(9 * nbytes + 4096 * 45, dtype=torch.uint8, device="cuda")
+            keep, ptrs_all, off = [pool], [], 0
+            for j in range(9):
+                ptrs_all.append(pool.data_ptr() + off)
+                dccl_amd.check(dccl_amd.synth_fill(ptrs_all[-1], 7, n, 0, 0xDCC1, 10 + j, st), "synth")
+                off += nbytes + 4096 * (j + 1)
+        sends, r = ptrs_all[:8], ptrs_all[8]
+        rows = []
+        for k in range(1, 9):
+            ptrs = sends[:k]
+            fn = lambda ptrs=ptrs: dccl_amd.local_reduce_multi(ptrs, r, 7, n, 0, st)
+            med, _ = time_launches([fn])
+            seq = lambda ptrs=ptrs: [dccl_amd.local_reduce(p, r, 7, n, 0, st) for p in ptrs]
+            med_seq, _ = time_launches([seq])
+            gbs = (k + 2) * nbytes / (med * 1e-3) / 1e9
+            rows.append({"k": k, "ms": round(med, 4), "gb_s": round(gbs, 1), "frac": round(gbs / PEAK, 4),
+                         "ms_k_single_launches": round(med_seq, 4), "speedup": round(med_seq / med, 2)})
+            print("kway", layout, rows[-1], flush=True)
+        out["rows" if layout == "separate" else "staggered_rows"] = rows
+        del keep
+        torch.cuda.empty_cache()
+    results["kway"] = out
 
 
 def host(results):
