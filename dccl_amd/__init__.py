@@ -118,6 +118,7 @@ def _load():
         "dccl_tune_ceiling": (c_int, [c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
         "dccl_tune_write_num_variants": (c_int, []),
         "dccl_tune_shift_num_variants": (c_int, []),
+        "dccl_tune_pipelined_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_size_t, c_void_p]),
         "dccl_tune_shift_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_void_p, c_void_p]),
         "dccl_tune_write_probe": (c_int, [c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
     })
@@ -141,7 +142,7 @@ EXPORTED_SYMBOLS = [
     "dccl_synth_fill", "dccl_tune_multi_f32_sum", "dccl_local_reduce_chain", "dccl_copy_multi",
     "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_tune_ceiling",
     "dccl_tune_write_num_variants", "dccl_tune_write_probe", "dccl_tune_shift_num_variants",
-    "dccl_tune_shift_f32_sum", "dccl_local_reduce_chain_host",
+    "dccl_tune_shift_f32_sum", "dccl_local_reduce_chain_host", "dccl_tune_pipelined_f32_sum",
 ]
 
 

@@ -390,3 +390,54 @@ extern "C" int dccl_tune_shift_f32_sum(const void* send, void* recv, size_t coun
     return kShift[variant].fn(static_cast<const unsigned char*>(send), static_cast<unsigned char*>(recv), count,
                               static_cast<hipStream_t>(stream), tune_align());
 }
+
+// ---------------------------------------------------------------------------------
+// Tuning only: persistent one-wave blocks with a software pipeline, fp32 Sum, 16-B aligned operands.
+// Each wave walks tiles t, t+G, t+2G, ... (G = grid) and issues the loads of its next tile before it
+// combines and stores the current one, so two tiles' loads are in flight per wave without relaunching
+// waves; DEPTH tiles ahead (1 or 2).
+// ---------------------------------------------------------------------------------
+namespace {
+template <int DEPTH>
+__global__ __launch_bounds__(64) void tune_pipelined_kernel(const u32x4* __restrict__ vs, u32x4* __restrict__ vr,
+                                                            size_t nvec) {
+    const size_t G = gridDim.x;
+    const size_t ntiles = nvec / 64;  // full tiles only (the probe passes a multiple of 64 vectors)
+    size_t t = blockIdx.x;
+    u32x4 s[DEPTH + 1], r[DEPTH + 1];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+        const size_t td = t + size_t(d) * G;
+        if (td < ntiles) {
+            s[d] = __builtin_nontemporal_load(vs + td * 64 + threadIdx.x);
+            r[d] = __builtin_nontemporal_load(vr + td * 64 + threadIdx.x);
+        }
+    }
+    for (; t < ntiles; t += G) {
+        const size_t tn = t + size_t(DEPTH) * G;
+        if (tn < ntiles) {
+            s[DEPTH] = __builtin_nontemporal_load(vs + tn * 64 + threadIdx.x);
+            r[DEPTH] = __builtin_nontemporal_load(vr + tn * 64 + threadIdx.x);
+        }
+        __builtin_nontemporal_store(combine16<float, kSum>(r[0], s[0]), vr + t * 64 + threadIdx.x);
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            s[d] = s[d + 1];
+            r[d] = r[d + 1];
+        }
+    }
+}
+}  // namespace
+
+extern "C" int dccl_tune_pipelined_f32_sum(const void* send, void* recv, size_t count, int depth, size_t grid,
+                                           void* stream) {
+    const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
+    if (((as | ar) & 15) || count % 256 || grid == 0 || (depth != 1 && depth != 2)) return DCCL_INVALID_ARGUMENT;
+    size_t nvec = count / 4;
+    const void* fn = depth == 1 ? reinterpret_cast<const void*>(&tune_pipelined_kernel<1>)
+                                : reinterpret_cast<const void*>(&tune_pipelined_kernel<2>);
+    void* args[] = {&send, &recv, &nvec};
+    return hipLaunchKernel(fn, dim3(unsigned(grid)), dim3(64), args, 0, static_cast<hipStream_t>(stream)) == hipSuccess
+               ? DCCL_SUCCESS
+               : DCCL_UNHANDLED_DEVICE_ERROR;
+}

@@ -43,6 +43,9 @@ int dccl_tune_ceiling(int kind, const void* send, void* recv, size_t count_f32, 
 int dccl_tune_shift_num_variants(void);
 int dccl_tune_shift_f32_sum(const void* send, void* recv, size_t count, int variant, int* policy, int* xcd,
                             void* stream);
+/* Persistent one-wave blocks with a software pipeline (loads of `depth` tiles ahead in flight), fp32 Sum,
+ * 16-B aligned operands, count a multiple of 256, `grid` blocks. */
+int dccl_tune_pipelined_f32_sum(const void* send, void* recv, size_t count, int depth, size_t grid, void* stream);
 int dccl_tune_write_num_variants(void);
 int dccl_tune_write_probe(int variant, void* recv, size_t count_f32, int* block, int* unroll, int* policy,
                           void* stream);
