@@ -151,17 +151,23 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
 // ---------------------------------------------------------------------------------
 struct CopyList { const unsigned char* src[8]; unsigned char* dst[8]; };
 
-__global__ __launch_bounds__(64) void copy_multi_kernel(CopyList cl, size_t bytes) {
-    const unsigned char* s = cl.src[blockIdx.y];
-    unsigned char* d = cl.dst[blockIdx.y];
+// Pairs are interleaved block by block (block b copies for pair b % npairs), so the blocks the
+// dispatcher issues together read from every source at once: with a peer per pair, every xGMI link is
+// busy for the whole launch instead of one peer after another (a y-row per pair would be dispatched
+// row by row).
+__global__ __launch_bounds__(64) void copy_multi_kernel(CopyList cl, int npairs, size_t bytes) {
+    const unsigned y = blockIdx.x % unsigned(npairs);
+    const size_t x = blockIdx.x / unsigned(npairs), gx = gridDim.x / unsigned(npairs);
+    const unsigned char* s = cl.src[y];
+    unsigned char* d = cl.dst[y];
     size_t head = (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15;
     if (head > bytes) head = bytes;
     const size_t nvec = (bytes - head) / 16;
     const u32x4* vs = reinterpret_cast<const u32x4*>(s + head);
     u32x4* vd = reinterpret_cast<u32x4*>(d + head);
-    for (size_t i = size_t(blockIdx.x) * 64 + threadIdx.x; i < nvec; i += size_t(gridDim.x) * 64)
+    for (size_t i = x * 64 + threadIdx.x; i < nvec; i += gx * 64)
         __builtin_nontemporal_store(__builtin_nontemporal_load(vs + i), vd + i);
-    if (blockIdx.x == 0) {
+    if (x == 0) {
         for (size_t b = threadIdx.x; b < head; b += 64) d[b] = s[b];
         for (size_t b = head + nvec * 16 + threadIdx.x; b < bytes; b += 64) d[b] = s[b];
     }
@@ -290,8 +296,8 @@ extern "C" int dccl_copy_multi(const void* const* srcs, void* const* dsts, int n
     }
     size_t gx = ceil_div(bytes / 16 + 1, 64);
     if (gx > (size_t(1) << 20)) gx = size_t(1) << 20;
-    void* args[] = {&cl, &bytes};
-    return hipLaunchKernel(reinterpret_cast<const void*>(&copy_multi_kernel), dim3(unsigned(gx), unsigned(npairs)),
+    void* args[] = {&cl, &npairs, &bytes};
+    return hipLaunchKernel(reinterpret_cast<const void*>(&copy_multi_kernel), dim3(unsigned(gx * size_t(npairs))),
                            dim3(64), args, 0, st) == hipSuccess
                ? DCCL_SUCCESS
                : DCCL_UNHANDLED_DEVICE_ERROR;
