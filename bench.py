@@ -25,7 +25,8 @@ c5 (BASELINE config C5 on every run: --c5-gib GiB per operand sharded over the N
 combine time and, N>1, the RCCL all-gather of the reduced shards),
 dccl_allreduce (N>1: the namespace-dccl ncclAllReduce over the RCCL p2p ring and over the direct
 IPC peer-read transport, checked against each other and RCCL's own all_reduce, timed beside it, plus
-the namespace-dccl all_gather of each transport against RCCL's all_gather (`dccl_allgather`);
+the namespace-dccl all_gather of each transport against RCCL's all_gather (`dccl_allgather`), and the
+direct all_gather at C5's size beside RCCL's (`c5_allgather`);
 in a child process per rank, so a fault or hang there cannot take the bench line with it).
 Progress goes to stderr, one line per phase.
 """
@@ -324,6 +325,13 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
                                  "busbw_gb_s": round(2 * (world - 1) / world * count * 4 / t / 1e9, 1),
                                  "note": "RCCL's own all_reduce, informational: its combine is RCCL's"}
         out["dccl_allgather"] = allgather_compare(comms, world, rank, dev, st, count, iters)
+        # BASELINE C5's exchange step at its own size (the reduced shards of DCCL_BENCH_C5_GIB GiB of fp32,
+        # moved as int32): the direct IPC all-gather beside RCCL's (the single-link ring is left out here)
+        c5_gib = float(os.environ.get("DCCL_BENCH_C5_GIB", "0") or 0)
+        if c5_gib > 0 and "direct" in comms:
+            c5_count = int(c5_gib * GIB) // 4 // world * world
+            torch.cuda.empty_cache()
+            out["c5_allgather"] = allgather_compare({"direct": comms["direct"]}, world, rank, dev, st, c5_count, 3)
     finally:
         for comm in comms.values():
             comm.finalize()
@@ -336,10 +344,12 @@ def allgather_compare(comms: dict, world: int, rank: int, dev, st, count: int, i
     the concatenation of every rank's slice (each rank regenerates all slices from their seeds), timed,
     and beside RCCL's all_gather_into_tensor when torch.distributed runs on RCCL."""
     per = count // world
-    slices = [torch.randint(-2**31, 2**31 - 1, (per,), device=dev, dtype=torch.int32,
-                            generator=torch.Generator(device=dev).manual_seed(777 + p)) for p in range(world)]
-    want = torch.cat(slices)
-    mine = slices[rank]
+
+    def slice_of(p):  # rank p's input, regenerated anywhere from its seed
+        return torch.randint(-2**31, 2**31 - 1, (per,), device=dev, dtype=torch.int32,
+                             generator=torch.Generator(device=dev).manual_seed(777 + p))
+
+    mine = slice_of(rank)
     res = {"bytes_per_rank": per * 4}
     y = torch.empty(per * world, dtype=torch.int32, device=dev)
     for name, comm in comms.items():
@@ -347,7 +357,7 @@ def allgather_compare(comms: dict, world: int, rank: int, dev, st, count: int, i
         torch.cuda.synchronize(dev)
         dccl_amd.check(comm.all_gather(mine.data_ptr(), y.data_ptr(), per, 2, st.cuda_stream), name)
         torch.cuda.synchronize(dev)
-        ok = bool(torch.equal(y, want))
+        ok = all(bool(torch.equal(y[p * per:(p + 1) * per], slice_of(p))) for p in range(world))
         dist.barrier()
         each = []
         t0 = time.perf_counter()
@@ -441,7 +451,7 @@ def progress(msg: str) -> None:
 CHILD_TIMEOUT_S = 150.0
 
 
-def collective_in_child(world: int, rank: int, local: int, backend: str) -> dict:
+def collective_in_child(world: int, rank: int, local: int, backend: str, c5_gib: float = 0.0) -> dict:
     """Run dccl_allreduce_multi in a child process per rank, with its own process group on a fresh port.
     The namespace-dccl collectives (RCCL p2p ring, IPC peer reads) are reported extras, never `value`: a
     fault or hang inside them ends the child, which is killed after CHILD_TIMEOUT_S, while this process,
@@ -460,7 +470,7 @@ def collective_in_child(world: int, rank: int, local: int, backend: str) -> dict
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
     env = {**env, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port[0]), "RANK": str(rank),
            "WORLD_SIZE": str(world), "LOCAL_RANK": str(local), "DCCL_BENCH_BACKEND": backend,
-           "DCCL_BOOTSTRAP_TAG": f"bench_child_{port[0]}"}
+           "DCCL_BOOTSTRAP_TAG": f"bench_child_{port[0]}", "DCCL_BENCH_C5_GIB": str(c5_gib)}
     torch.cuda.synchronize()
     progress(f"namespace-dccl all_reduce extras in a child process (port {port[0]})")
     t0 = time.perf_counter()
@@ -620,7 +630,8 @@ def main():
         if (backend == "nccl" or rehearse) and os.environ.get("DCCL_BENCH_NO_COLLECTIVE", "0") != "1":
             send = recv = None
             torch.cuda.empty_cache()
-            extra["dccl_allreduce"] = collective_in_child(world, rank, local, backend)
+            extra["dccl_allreduce"] = collective_in_child(world, rank, local, backend,
+                                                          a.c5_gib if backend == "nccl" else min(a.c5_gib, 1.0))
 
     if rank == 0:
         traffic = None

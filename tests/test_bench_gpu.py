@@ -69,6 +69,7 @@ def test_bench_direct_allreduce_two_processes_one_gpu():
     assert "error" not in ar, ar
     assert ar["direct"]["int32_sum_bit_exact_vs_rccl"] and ar["direct"]["fp32_within_bound"], ar
     assert ar["dccl_allgather"]["direct"]["bit_exact"], ar["dccl_allgather"]
+    assert ar["c5_allgather"]["direct"]["bit_exact"], ar["c5_allgather"]
 
 
 def test_bench_single_gpu_line():
