@@ -95,12 +95,6 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
 // per CU are capped (through unused dynamic LDS, 160 KiB per CU) to keep roughly 50-80 KiB of reads
 // outstanding per CU.  Measured optimum per k at 1 GiB per operand on MI355X, fp32 Sum
 // (tools/tune_multi.py, profiles/r1_tune_multi_waves.json): 4-7 % faster than 32 waves for k >= 2.
-constexpr int kMultiWaves[9] = {32, 32, 18, 13, 13, 11, 11, 10, 9};
-constexpr size_t kLdsPerCu = 160u << 10;
-constexpr size_t multi_lds(int k) {
-    return kMultiWaves[k] >= 32 ? 0 : (kLdsPerCu / kMultiWaves[k] + 255) / 256 * 256;
-}
-
 template <typename T, int OP, int K>
 int launch_multi_vec(SendList sl, unsigned char* r, Split sp, hipStream_t stream) {
     using C = DefaultCfg;
@@ -123,6 +117,12 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
         if ((a ^ ar) & 15) vec_ok = false;
     }
     auto r = static_cast<unsigned char*>(recv);
+    if (elem_ok && !vec_ok) {  // element-aligned sources at other 16-B phases: the phased kernel
+        const Split sp = split_for_vectors<T>(ar, count, recv_align());
+        PhaseList ph{};
+        for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(T));
+        return multi_phased_typed<T, OP>(sl, ph, nsend, r, sp, stream);
+    }
     if (!vec_ok) {
         const size_t grid = ceil_div(count, size_t(kBlock));
         void* args[] = {&sl, &nsend, &r, &count};
@@ -197,6 +197,13 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
     }
     const auto o = static_cast<const unsigned char*>(own);
     auto d = static_cast<unsigned char*>(dst);
+    if (elem_ok && !vec_ok) {  // element-aligned operands at other 16-B phases than dst's: the phased kernel
+        const Split sp = split_for_vectors<T>(ad, count, recv_align());
+        PhaseList ph{};
+        for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(T));
+        ph.p[nsend] = phase_word(o, sp.head * sizeof(T));
+        return chain_phased_typed<T, OP>(sl, ph, nsend, o, d, sp, stream);
+    }
     if (!vec_ok) {
         const size_t grid = ceil_div(count, size_t(kBlock));
         void* args[] = {&sl, &nsend, const_cast<const unsigned char**>(&o), &d, &count};

@@ -1,0 +1,57 @@
+// dccl_amd/csrc/phased_chain.hip — the chain combine dst = op(own, op(s{K-1}, ... op(s1, s0))) (the ring order) for element-aligned
+// operands whose 16-B phases differ from the destination's (reduce_chain_phased_kernel in
+// reduce_kernels.hpp).  Instantiated for every (T, OP) here, in a translation unit of its own, so the
+// build compiles it beside local_reduce.hip.
+#include <hip/hip_runtime.h>
+
+
+#include "dispatch.hpp"
+#include "reduce_kernels.hpp"
+
+namespace dccl_amd {
+namespace {
+
+template <typename T, int OP, int K>
+int launch_phased(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream) {
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    void* args[] = {&sl, &ph, &own, &d, &sp.head, &sp.nvec, &sp.tail};
+    // No occupancy cap, unlike the k-way kernel (reduce_kernels.hpp, "Phased k-way and chain kernels").
+    return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K>), grid, args, stream, 64);
+}
+
+}  // namespace
+
+template <typename T, int OP>
+int chain_phased_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream) {
+    switch (nsend) {
+    case 1: return launch_phased<T, OP, 1>(sl, ph, own, d, sp, stream);
+    case 2: return launch_phased<T, OP, 2>(sl, ph, own, d, sp, stream);
+    case 3: return launch_phased<T, OP, 3>(sl, ph, own, d, sp, stream);
+    case 4: return launch_phased<T, OP, 4>(sl, ph, own, d, sp, stream);
+    case 5: return launch_phased<T, OP, 5>(sl, ph, own, d, sp, stream);
+    case 6: return launch_phased<T, OP, 6>(sl, ph, own, d, sp, stream);
+    case 7: return launch_phased<T, OP, 7>(sl, ph, own, d, sp, stream);
+    case 8: return launch_phased<T, OP, 8>(sl, ph, own, d, sp, stream);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+
+#define DCCL_PHASED_INST(T)                                                       \
+    template int chain_phased_typed<T, kSum>(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream);  \
+    template int chain_phased_typed<T, kProd>(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream); \
+    template int chain_phased_typed<T, kMax>(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream);  \
+    template int chain_phased_typed<T, kMin>(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream);
+DCCL_PHASED_INST(int8_t)
+DCCL_PHASED_INST(uint8_t)
+DCCL_PHASED_INST(int32_t)
+DCCL_PHASED_INST(uint32_t)
+DCCL_PHASED_INST(int64_t)
+DCCL_PHASED_INST(uint64_t)
+DCCL_PHASED_INST(f16_bits)
+DCCL_PHASED_INST(float)
+DCCL_PHASED_INST(double)
+DCCL_PHASED_INST(bf16_bits)
+#undef DCCL_PHASED_INST
+
+}  // namespace dccl_amd

@@ -331,8 +331,117 @@ __global__ __launch_bounds__(kBlock) void reduce_chain_scalar_kernel(SendList se
 }
 
 // ---------------------------------------------------------------------------------
+// Phased k-way and chain kernels: element-aligned sources whose 16-B phases differ from the
+// destination's (DCCL chunks of sizes that are not a multiple of 16 B, read from peers or
+// scratchpads at other phases).  Operand j's body starts p_j bytes (ph.p[j], 0 <= p_j < 16) past
+// a 16-B boundary A_j.  An operand with p_j != 0 is read the shifted kernel's way: every lane
+// loads the ALIGNED vector A_j[v] (non-temporal), lane 63 also loads A_j[v+1] (through the
+// caches), the other lanes take it from their right-hand neighbour (ds_bpermute), and the 32
+// bytes are funnel-shifted by p_j.  An operand with p_j == 0 is a plain vector load.
+// Measured on MI355X (tools/bench_suite.py --parts phased, profiles/r1_s5_phased_probe.json): one
+// operand at a time with a uniform branch on its phase, and no occupancy cap, beat issuing every
+// operand's loads before the first shift (branch-free selects) and the k-way kernel's wave caps:
+// 74-79 % of HBM peak for k = 1..7 against 45-61 %.  The per-operand load -> bpermute -> shift
+// chain needs the full 32 waves per CU to hide its latency.
+// One-wave blocks and a per-tile loop uniform per wave: every lane reaches the bpermutes.
+// ---------------------------------------------------------------------------------
+struct PhaseList { unsigned p[9]; };
+
+// The 16 body bytes of vector v (zero for v >= nvec) of an operand whose body starts at `body`,
+// phase p.  All 64 lanes must call it (p is uniform).
+__device__ __forceinline__ u32x4 ld_phased(const unsigned char* body, unsigned p, size_t v, size_t nvec) {
+    u32x4 lo = {0u, 0u, 0u, 0u};
+    if (p == 0) {
+        if (v < nvec) lo = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(body) + v);
+        return lo;
+    }
+    const u32x4* va = reinterpret_cast<const u32x4*>(body - p);
+    const bool last_lane = (threadIdx.x & 63) == 63;
+    u32x4 ex = {0u, 0u, 0u, 0u};
+    if (v <= nvec) lo = __builtin_nontemporal_load(va + v);  // A[nvec] holds the last p body bytes
+    if (last_lane && v < nvec) ex = va[v + 1];
+    u32x4 hi = from_next_lane(lo);
+    if (last_lane) hi = ex;
+    const unsigned b = p & 3;
+    switch (p >> 2) {  // uniform
+    case 0: return funnel16<0>(lo, hi, b);
+    case 1: return funnel16<1>(lo, hi, b);
+    case 2: return funnel16<2>(lo, hi, b);
+    default: return funnel16<3>(lo, hi, b);
+    }
+}
+
+template <typename T, int OP, int K>
+__global__ __launch_bounds__(64) void reduce_multi_phased_kernel(SendList sends, PhaseList ph,
+                                                                 unsigned char* __restrict__ recv, size_t head,
+                                                                 size_t nvec, size_t tail) {
+    const size_t off = head * sizeof(T);
+    u32x4* vr = reinterpret_cast<u32x4*>(recv + off);
+    const size_t ntiles = (nvec + 63) / 64;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t v = t * 64 + threadIdx.x;
+        u32x4 s[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k] + off, ph.p[k], v, nvec);
+        if (v < nvec) {
+            u32x4 acc = ld16<true>(vr + v);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, s[k]);
+            __builtin_nontemporal_store(acc, vr + v);
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (size_t j = threadIdx.x; j < head + tail; j += blockDim.x) {
+            const size_t i = j < head ? j : head + nvec * Pack<T>::N + (j - head);
+            T acc = ld_elem<T, true>(recv, i);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, true>(sends.p[k], i));
+            st_elem<T, true>(recv, i, acc);
+        }
+    }
+}
+
+// Chain order as reduce_chain_vec_kernel; ph.p[K] is own's phase.
+template <typename T, int OP, int K>
+__global__ __launch_bounds__(64) void reduce_chain_phased_kernel(SendList sends, PhaseList ph,
+                                                                 const unsigned char* own, unsigned char* dst,
+                                                                 size_t head, size_t nvec, size_t tail) {
+    const size_t off = head * sizeof(T);
+    u32x4* vd = reinterpret_cast<u32x4*>(dst + off);
+    const size_t ntiles = (nvec + 63) / 64;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t v = t * 64 + threadIdx.x;
+        u32x4 s[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k] + off, ph.p[k], v, nvec);
+        const u32x4 o = ld_phased(own + off, ph.p[K], v, nvec);
+        if (v < nvec) {
+            u32x4 acc = s[0];
+#pragma unroll
+            for (int k = 1; k < K; ++k) acc = combine16<T, OP>(s[k], acc);
+            __builtin_nontemporal_store(combine16<T, OP>(o, acc), vd + v);
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (size_t j = threadIdx.x; j < head + tail; j += blockDim.x) {
+            const size_t i = j < head ? j : head + nvec * Pack<T>::N + (j - head);
+            T acc = ld_elem<T, true>(sends.p[0], i);
+#pragma unroll
+            for (int k = 1; k < K; ++k) acc = Combine<T, OP>::apply(ld_elem<T, true>(sends.p[k], i), acc);
+            st_elem<T, true>(dst, i, Combine<T, OP>::apply(ld_elem<T, true>(own, i), acc));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // Host-side launch helpers
 // ---------------------------------------------------------------------------------
+inline constexpr int kMultiWaves[9] = {32, 32, 18, 13, 13, 11, 11, 10, 9};
+inline constexpr size_t kLdsPerCu = 160u << 10;
+constexpr size_t multi_lds(int k) {
+    return kMultiWaves[k] >= 32 ? 0 : (kLdsPerCu / kMultiWaves[k] + 255) / 256 * 256;
+}
+
 constexpr size_t kMaxGrid = size_t(1) << 24;  // grid-stride beyond this (2^24 x 64 threads)
 
 inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream, int block = kBlock,
@@ -385,5 +494,18 @@ int launch_shift(const unsigned char* s, unsigned char* r, size_t count, hipStre
     return launch(reinterpret_cast<const void*>(&reduce_shift_kernel<T, OP, POLICY, XCD, TAG>), grid, args, stream,
                   64);
 }
+
+// 16-B phase of an operand whose body starts `off` bytes in (see PhaseList).
+inline unsigned phase_word(const unsigned char* base, size_t off) {
+    return unsigned((reinterpret_cast<uintptr_t>(base) + off) & 15);
+}
+
+// The phased k-way and chain launches, instantiated for every (T, OP) in phased_multi.hip and
+// phased_chain.hip (their own translation units, so they compile beside local_reduce.hip).
+template <typename T, int OP>
+int multi_phased_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, Split sp, hipStream_t stream);
+template <typename T, int OP>
+int chain_phased_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp,
+                       hipStream_t stream);
 
 }  // namespace dccl_amd

@@ -129,6 +129,37 @@ def test_chain_against_oracle(gpu, dt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dt", list(range(10)))
+def test_chain_mixed_phases(gpu, dt):
+    """Sends, own and dst each at their own element-aligned 16-B / 128-B phase (the phased chain kernel)."""
+    import dccl_amd
+    from tests.test_gpu_parity import rand_inputs, dev_bytes, host_of
+    from tests.test_oracle import fp_equal
+    rng = np.random.default_rng(500 + dt)
+    esz = dccl_amd.size_of_type(dt)
+    for k, n in ((1, 3), (2, 63), (3, 4099), (5, 65539), (7, 1000), (8, 20001)):
+        op = int(rng.integers(0, 4))
+        arrs = [rand_inputs(rng, dt, n)[0] for _ in range(k + 1)]
+        sends, own = arrs[:k], arrs[k]
+        want = chain_expected(sends, own, dt, op)
+        offs = [int(rng.integers(0, 256 // esz)) * esz for _ in range(k + 2)]
+        offs[0] = (offs[0] // 16) * 16 + (esz if esz < 16 else 0)
+        dev = [dev_bytes(a, o) for a, o in zip(sends, offs)]
+        t_own, p_own = dev_bytes(own, offs[k])
+        t_dst, p_dst = dev_bytes(np.zeros_like(own), offs[k + 1])
+        assert dccl_amd.local_reduce_chain([d[1] for d in dev], p_own, p_dst, dt, n, op) == 0
+        import torch
+        torch.cuda.synchronize()
+        got = host_of(t_dst, offs[k + 1], own)
+        assert fp_equal(got, want, dt), (op, k, n, offs)
+        assert host_of(t_own, offs[k], own).tobytes() == own.tobytes()
+        # in place: own == dst at its own phase, the sends at theirs
+        assert dccl_amd.local_reduce_chain([d[1] for d in dev], p_own, p_own, dt, n, op) == 0
+        torch.cuda.synchronize()
+        assert fp_equal(host_of(t_own, offs[k], own), want, dt), (op, k, n, offs, "in place")
+
+
+@pytest.mark.gpu
 def test_copy_multi(gpu):
     import torch
     import dccl_amd

@@ -225,6 +225,29 @@ def test_multi_matches_sequential(dccl, k):
     assert dccl.local_reduce_multi([], 0, 7, 4, 0, 0) == 4
 
 
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 7, 8])
+def test_multi_mixed_phases(dccl, k):
+    """Element-aligned sources at their own 16-B and 128-B phases (the phased k-way kernel)."""
+    rng = np.random.default_rng(400 + k)
+    for dt in ALL_DTYPES:
+        esz = int(oracle.NP_DTYPES[dt]().itemsize)
+        for n in (1, 5, 63, 4099, 65539):
+            op = int(rng.integers(0, 4))
+            sends = [rand_inputs(rng, dt, n)[0] for _ in range(k)]
+            _, r = rand_inputs(rng, dt, n)
+            offs = [int(rng.integers(0, 256 // esz)) * esz for _ in range(k)]
+            offs[0] = (offs[0] // 16) * 16 + (esz if esz < 16 else 0)  # at least one source off 16-B phase
+            roff = int(rng.integers(0, 256 // esz)) * esz
+            holders = [dev_bytes(x, o) for x, o in zip(sends, offs)]
+            tr, pr = dev_bytes(r, roff)
+            assert dccl.local_reduce_multi([h[1] for h in holders], pr, dt, n, op, 0) == 0
+            torch.cuda.synchronize()
+            want = r
+            for x in sends:
+                want = expected(x, want, dt, op)
+            assert fp_equal(host_of(tr, roff, r), want, dt), (k, dt, n, op, offs, roff)
+
+
 # ----------------------------------------------------------------------------- host path
 @pytest.mark.parametrize("zero_copy", ["default", "0"])
 @pytest.mark.parametrize("pinned", ["none", "both", "send"])

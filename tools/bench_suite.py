@@ -283,6 +283,35 @@ def misaligned(results, mib=1024):
     results["misaligned"] = rows
 
 
+def phased(results, mib=256):
+    """k-way and chain combines with sources off the destination's 16-B phase (phased kernels) beside
+    the same launch with every operand in phase, fp32 Sum, separately allocated operands."""
+    st = torch.cuda.current_stream().cuda_stream
+    nbytes = mib << 20
+    n = nbytes // 4 - 64
+    keep = [fill(nbytes, 7, 0, 20 + k) for k in range(9)]
+    base = [x.data_ptr() for x in keep]
+    rows = []
+    for k in (1, 2, 4, 7):
+        for what, offs in (("in phase", [0] * k), ("all sources +4 B", [4] * k),
+                           ("alternate sources +8 B", [8 * (j % 2) for j in range(k)]),
+                           ("sources +16 B (cached loads)", [16] * k)):
+            ptrs = [base[j] + offs[j] for j in range(k)]
+            r = base[8]
+            fm = lambda ptrs=ptrs: dccl_amd.local_reduce_multi(ptrs, r, 7, n, 0, st)
+            fc = lambda ptrs=ptrs: dccl_amd.local_reduce_chain(ptrs, r, r, 7, n, 0, st)
+            row = {"k": k, "sources": what}
+            for name, fn in (("multi", fm), ("chain", fc)):
+                med, _ = time_launches([fn], rounds=5)
+                gbs = (k + 2) * n * 4 / (med * 1e-3) / 1e9
+                row[name] = {"ms": round(med, 4), "gb_s": round(gbs, 1), "frac": round(gbs / PEAK, 4)}
+            rows.append(row)
+            print("phased", row, flush=True)
+    results["phased"] = {"bytes_per_operand": n * 4, "rows": rows}
+    del keep
+    torch.cuda.empty_cache()
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--parts", default="c3,c4,c2,kway,host,c1,misaligned")
@@ -291,7 +320,7 @@ def main():
     results = {"device": torch.cuda.get_device_name(0), "peak_gb_s": PEAK}
     for part in a.parts.split(","):
         {"c3": c3, "c4": c4, "c2": c2, "kway": kway, "host": host, "c1": c1, "misaligned": misaligned,
-         "c4_graph": c4_graph}[part](results)
+         "c4_graph": c4_graph, "phased": phased}[part](results)
         if a.out:
             with open(a.out, "w") as f:
                 json.dump(results, f, indent=1)
