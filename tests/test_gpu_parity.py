@@ -165,6 +165,31 @@ def test_shifted_kernel_every_phase(dccl, dt):
                 assert not tr[:roff].any() and not tr[roff + nb:].any(), (dt, n, soff, roff)
 
 
+@pytest.mark.parametrize("dt", [2, 3, 4, 5, 6, 7, 8, 9])
+def test_element_misaligned_every_offset(dccl, dt):
+    """Element-misaligned operands (recv not a multiple of sizeof(T); the byte-gather kernel): every
+    recv byte offset in a 16-B vector, send at several byte phases, sizes around a 64-vector tile,
+    partial tiles; nothing outside recv's bytes is written."""
+    rng = np.random.default_rng(700 + dt)
+    esz = np.dtype(oracle.NP_DTYPES[dt]).itemsize
+    per_tile = 64 * (16 // esz)
+    sizes = [1, 2, 16 // esz + 1, per_tile - 1, per_tile, per_tile + 1, 2 * per_tile + 16 // esz + 3, 40001]
+    for roff in range(1, 16):
+        if roff % esz == 0:
+            continue
+        for soff in sorted({0, roff, (roff + 3) % 16, 16 - roff, 1 + 16 * (roff % 3)}):
+            for n in sizes:
+                s, r = rand_inputs(rng, dt, n)
+                op = int(rng.integers(0, 4))
+                ts, ps = dev_bytes(s, soff)
+                tr, pr = dev_bytes(r, roff)
+                assert dccl.local_reduce(ps, pr, dt, n, op, 0) == 0
+                torch.cuda.synchronize()
+                assert fp_equal(host_of(tr, roff, r), expected(s, r, dt, op), dt), (dt, op, n, soff, roff)
+                nb = n * esz
+                assert not tr[:roff].any() and not tr[roff + nb:].any(), (dt, n, soff, roff)
+
+
 @pytest.mark.parametrize("dt", [6, 9])
 def test_all_16bit_patterns(dccl, dt):
     """Every fp16 / bf16 bit pattern as recv against a fixed set of partners."""

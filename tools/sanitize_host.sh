@@ -16,11 +16,11 @@ for f in comm algorithms dccl_api direct host_staged rccl_transport; do
   "$HIPCC" "${flags[@]}" -c "$root/dccl_amd/csrc/$f.cpp" -o "$out/$f.o"
   objs+=("$out/$f.o")
 done
-# the kernel translation unit is reused from the normal build (its host side is a launcher only)
-lr="$root/build/obj/local_reduce.hip.o"
-[[ -f "$lr" ]] || python "$root/dccl_amd/build.py" > /dev/null
+# the kernel translation units are reused from the normal build (their host side is launchers only)
+lr=("$root/build/obj/local_reduce.hip.o" "$root/build/obj/phased_multi.hip.o" "$root/build/obj/phased_chain.hip.o")
+for o in "${lr[@]}"; do [[ -f "$o" ]] || python "$root/dccl_amd/build.py" > /dev/null; done
 "$HIPCC" "${flags[@]}" -c "$root/tools/dccl_cli.cpp" -o "$out/cli.o"
-"$HIPCC" --offload-arch=gfx950 -Xarch_host "-fsanitize=$kind" "$out/cli.o" "${objs[@]}" "$lr" -o "$out/dccl_cli" -pthread -ldl
+"$HIPCC" --offload-arch=gfx950 -Xarch_host "-fsanitize=$kind" "$out/cli.o" "${objs[@]}" "${lr[@]}" -o "$out/dccl_cli" -pthread -ldl
 export TSAN_OPTIONS="halt_on_error=1 exitcode=66" ASAN_OPTIONS="halt_on_error=1 exitcode=66 detect_leaks=1" \
        UBSAN_OPTIONS="halt_on_error=1 exitcode=66 print_stacktrace=1"
 run() { echo "+ dccl_cli $*"; "$out/dccl_cli" "$@" > "$out/last.log" 2>&1 || { cat "$out/last.log"; exit 1; }; }
