@@ -147,14 +147,15 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
 // ---------------------------------------------------------------------------------
 // Multi-source copy (the all-gather half of the direct collectives): pair y copies `bytes`
 // from src[y] to dst[y]; every pair in one launch, so reads from up to 8 peers (8 xGMI links)
-// are in flight together.  Requires src[y] and dst[y] to share a 16-B phase.
+// are in flight together.  Any byte alignment of src[y] and dst[y].
 // ---------------------------------------------------------------------------------
 struct CopyList { const unsigned char* src[8]; unsigned char* dst[8]; };
 
 // Pairs are interleaved block by block (block b copies for pair b % npairs), so the blocks the
 // dispatcher issues together read from every source at once: with a peer per pair, every xGMI link is
 // busy for the whole launch instead of one peer after another (a y-row per pair would be dispatched
-// row by row).
+// row by row).  dst is walked in aligned 16-B vectors; a source at another 16-B phase is read with
+// the phased kernels' cross-lane funnel shift (ld_phased), so every access stays a 16-B vector.
 __global__ __launch_bounds__(64) void copy_multi_kernel(CopyList cl, int npairs, size_t bytes) {
     const unsigned y = blockIdx.x % unsigned(npairs);
     const size_t x = blockIdx.x / unsigned(npairs), gx = gridDim.x / unsigned(npairs);
@@ -163,10 +164,13 @@ __global__ __launch_bounds__(64) void copy_multi_kernel(CopyList cl, int npairs,
     size_t head = (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15;
     if (head > bytes) head = bytes;
     const size_t nvec = (bytes - head) / 16;
-    const u32x4* vs = reinterpret_cast<const u32x4*>(s + head);
+    const unsigned p = unsigned((reinterpret_cast<uintptr_t>(s) + head) & 15);  // uniform per block
     u32x4* vd = reinterpret_cast<u32x4*>(d + head);
-    for (size_t i = x * 64 + threadIdx.x; i < nvec; i += gx * 64)
-        __builtin_nontemporal_store(__builtin_nontemporal_load(vs + i), vd + i);
+    for (size_t t = x; t * 64 < nvec; t += gx) {  // uniform per wave: every lane reaches the bpermutes
+        const size_t v = t * 64 + threadIdx.x;
+        const u32x4 val = ld_phased(s + head, p, v, nvec);
+        if (v < nvec) __builtin_nontemporal_store(val, vd + v);
+    }
     if (x == 0) {
         for (size_t b = threadIdx.x; b < head; b += 64) d[b] = s[b];
         for (size_t b = head + nvec * 16 + threadIdx.x; b < bytes; b += 64) d[b] = s[b];
@@ -287,20 +291,12 @@ extern "C" int dccl_copy_multi(const void* const* srcs, void* const* dsts, int n
     if (npairs < 0 || npairs > 8 || (npairs > 0 && (srcs == nullptr || dsts == nullptr))) return DCCL_INVALID_ARGUMENT;
     if (npairs == 0 || bytes == 0) return DCCL_SUCCESS;
     CopyList cl{};
-    bool vec_ok = true;
     for (int y = 0; y < npairs; ++y) {
         if (srcs[y] == nullptr || dsts[y] == nullptr) return DCCL_INVALID_ARGUMENT;
         cl.src[y] = static_cast<const unsigned char*>(srcs[y]);
         cl.dst[y] = static_cast<unsigned char*>(dsts[y]);
-        if ((reinterpret_cast<uintptr_t>(srcs[y]) ^ reinterpret_cast<uintptr_t>(dsts[y])) & 15) vec_ok = false;
     }
     const auto st = static_cast<hipStream_t>(stream);
-    if (!vec_ok) {  // rare: differing 16-B phases; the runtime's copy handles any alignment
-        for (int y = 0; y < npairs; ++y)
-            if (hipMemcpyAsync(dsts[y], srcs[y], bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
-                return DCCL_UNHANDLED_DEVICE_ERROR;
-        return DCCL_SUCCESS;
-    }
     size_t gx = ceil_div(bytes / 16 + 1, 64);
     if (gx > (size_t(1) << 20)) gx = size_t(1) << 20;
     void* args[] = {&cl, &npairs, &bytes};

@@ -163,7 +163,9 @@ def test_chain_mixed_phases(gpu, dt):
 def test_copy_multi(gpu):
     import torch
     import dccl_amd
-    for nbytes, soff, doff in ((1, 0, 0), (15, 3, 3), (4096, 0, 0), ((1 << 20) + 7, 5, 5), (1000, 1, 2)):
+    for nbytes, soff, doff in ((1, 0, 0), (15, 3, 3), (4096, 0, 0), ((1 << 20) + 7, 5, 5), (1000, 1, 2),
+                               (1023, 4, 0), (1024 * 64 + 17, 0, 12), ((1 << 20) + 3, 13, 6), (17, 15, 1),
+                               (64 * 16 + 5, 8, 9), (999999, 7, 3)):
         srcs = [torch.randint(0, 255, (nbytes + 64,), dtype=torch.uint8, device="cuda") for _ in range(8)]
         dsts = [torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda") for _ in range(8)]
         assert dccl_amd.copy_multi([s.data_ptr() + soff for s in srcs], [d.data_ptr() + doff for d in dsts],
