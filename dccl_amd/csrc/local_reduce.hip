@@ -95,6 +95,16 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
 // per CU are capped (through unused dynamic LDS, 160 KiB per CU) to keep roughly 50-80 KiB of reads
 // outstanding per CU.  Measured optimum per k at 1 GiB per operand on MI355X, fp32 Sum
 // (tools/tune_multi.py, profiles/r1_tune_multi_waves.json): 4-7 % faster than 32 waves for k >= 2.
+// In-phase sources off recv's 128-B line grid (recv is line-aligned past the head): their loads go
+// through the caches, so the line two neighbouring tiles share is fetched once (StraddleCfg's rule).
+// 1 GiB-class A/B on one MI355X (profiles/r1_s5_kway_straddle_ab.json): k = 1 76.7 -> 85.6 %,
+// k = 2 75.5 -> 78.0 %, k = 4 74.4 -> 78.4 %, k = 7 72.3 -> 77.5 % of HBM peak.
+inline bool any_straddles(const SendList& sl, int nsend, size_t off) {
+    for (int k = 0; k < nsend; ++k)
+        if ((reinterpret_cast<uintptr_t>(sl.p[k]) + off) & 127) return true;
+    return false;
+}
+
 template <typename T, int OP, int K>
 int launch_multi_vec(SendList sl, unsigned char* r, Split sp, hipStream_t stream) {
     using C = DefaultCfg;
@@ -131,6 +141,8 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
         return launch(fn, grid, args, stream);
     }
     const Split sp = split_for_vectors<T>(ar, count, recv_align());
+    if (any_straddles(sl, nsend, sp.head * sizeof(T)))
+        return multi_straddle_typed<T, OP>(sl, nsend, r, sp, stream);
     switch (nsend) {
     case 1: return launch_multi_vec<T, OP, 1>(sl, r, sp, stream);
     case 2: return launch_multi_vec<T, OP, 2>(sl, r, sp, stream);
@@ -216,6 +228,8 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
         return launch(fn, grid, args, stream);
     }
     const Split sp = split_for_vectors<T>(ad, count, recv_align());
+    if (any_straddles(sl, nsend, sp.head * sizeof(T)))
+        return chain_straddle_typed<T, OP>(sl, nsend, o, d, sp, stream);
     switch (nsend) {
     case 1: return launch_chain_vec<T, OP, 1>(sl, o, d, sp, stream);
     case 2: return launch_chain_vec<T, OP, 2>(sl, o, d, sp, stream);

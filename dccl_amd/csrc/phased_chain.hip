@@ -20,6 +20,17 @@ int launch_phased(SendList sl, PhaseList ph, const unsigned char* own, unsigned 
     return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K>), grid, args, stream, 64);
 }
 
+using StraddleKwayCfg = VecCfg<64, 1, kNtRecv | kNtStore, false>;
+
+template <typename T, int OP, int K>
+int launch_straddle(SendList sl, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream) {
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    void* args[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&reduce_chain_vec_kernel<T, OP, K, StraddleKwayCfg>), grid, args, stream, 64,
+                  multi_lds(K));
+}
+
 }  // namespace
 
 template <typename T, int OP>
@@ -37,7 +48,26 @@ int chain_phased_typed(SendList sl, PhaseList ph, int nsend, const unsigned char
     }
 }
 
+template <typename T, int OP>
+int chain_straddle_typed(SendList sl, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream) {
+    switch (nsend) {
+    case 1: return launch_straddle<T, OP, 1>(sl, own, d, sp, stream);
+    case 2: return launch_straddle<T, OP, 2>(sl, own, d, sp, stream);
+    case 3: return launch_straddle<T, OP, 3>(sl, own, d, sp, stream);
+    case 4: return launch_straddle<T, OP, 4>(sl, own, d, sp, stream);
+    case 5: return launch_straddle<T, OP, 5>(sl, own, d, sp, stream);
+    case 6: return launch_straddle<T, OP, 6>(sl, own, d, sp, stream);
+    case 7: return launch_straddle<T, OP, 7>(sl, own, d, sp, stream);
+    case 8: return launch_straddle<T, OP, 8>(sl, own, d, sp, stream);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+
 #define DCCL_PHASED_INST(T)                                                       \
+    template int chain_straddle_typed<T, kSum>(SendList sl, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream); \
+    template int chain_straddle_typed<T, kProd>(SendList sl, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream); \
+    template int chain_straddle_typed<T, kMax>(SendList sl, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream); \
+    template int chain_straddle_typed<T, kMin>(SendList sl, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream); \
     template int chain_phased_typed<T, kSum>(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream);  \
     template int chain_phased_typed<T, kProd>(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream); \
     template int chain_phased_typed<T, kMax>(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream);  \

@@ -20,6 +20,17 @@ int launch_phased(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStre
     return launch(reinterpret_cast<const void*>(&reduce_multi_phased_kernel<T, OP, K>), grid, args, stream, 64);
 }
 
+using StraddleKwayCfg = VecCfg<64, 1, kNtRecv | kNtStore, false>;
+
+template <typename T, int OP, int K>
+int launch_straddle(SendList sl, unsigned char* r, Split sp, hipStream_t stream) {
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, StraddleKwayCfg>), grid, args, stream, 64,
+                  multi_lds(K));
+}
+
 }  // namespace
 
 template <typename T, int OP>
@@ -37,7 +48,26 @@ int multi_phased_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, S
     }
 }
 
+template <typename T, int OP>
+int multi_straddle_typed(SendList sl, int nsend, unsigned char* r, Split sp, hipStream_t stream) {
+    switch (nsend) {
+    case 1: return launch_straddle<T, OP, 1>(sl, r, sp, stream);
+    case 2: return launch_straddle<T, OP, 2>(sl, r, sp, stream);
+    case 3: return launch_straddle<T, OP, 3>(sl, r, sp, stream);
+    case 4: return launch_straddle<T, OP, 4>(sl, r, sp, stream);
+    case 5: return launch_straddle<T, OP, 5>(sl, r, sp, stream);
+    case 6: return launch_straddle<T, OP, 6>(sl, r, sp, stream);
+    case 7: return launch_straddle<T, OP, 7>(sl, r, sp, stream);
+    case 8: return launch_straddle<T, OP, 8>(sl, r, sp, stream);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+
 #define DCCL_PHASED_INST(T)                                                       \
+    template int multi_straddle_typed<T, kSum>(SendList sl, int nsend, unsigned char* r, Split sp, hipStream_t stream); \
+    template int multi_straddle_typed<T, kProd>(SendList sl, int nsend, unsigned char* r, Split sp, hipStream_t stream); \
+    template int multi_straddle_typed<T, kMax>(SendList sl, int nsend, unsigned char* r, Split sp, hipStream_t stream); \
+    template int multi_straddle_typed<T, kMin>(SendList sl, int nsend, unsigned char* r, Split sp, hipStream_t stream); \
     template int multi_phased_typed<T, kSum>(SendList sl, PhaseList ph, int nsend, unsigned char* r, Split sp, hipStream_t stream);  \
     template int multi_phased_typed<T, kProd>(SendList sl, PhaseList ph, int nsend, unsigned char* r, Split sp, hipStream_t stream); \
     template int multi_phased_typed<T, kMax>(SendList sl, PhaseList ph, int nsend, unsigned char* r, Split sp, hipStream_t stream);  \

@@ -299,7 +299,8 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sen
         if (i < nvec) {
             u32x4 s[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k) s[k] = ld16<true>(reinterpret_cast<const u32x4*>(sends.p[k] + off) + i);
+            for (int k = 0; k < K; ++k)
+                s[k] = ld16<(C::POLICY & kNtSend) != 0>(reinterpret_cast<const u32x4*>(sends.p[k] + off) + i);
             const u32x4 o = ld16<true>(vo + i);
             u32x4 acc = s[0];
 #pragma unroll
@@ -504,6 +505,13 @@ inline unsigned phase_word(const unsigned char* base, size_t off) {
 // phased_chain.hip (their own translation units, so they compile beside local_reduce.hip).
 template <typename T, int OP>
 int multi_phased_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, Split sp, hipStream_t stream);
+// In-phase k-way and chain launches whose sources straddle recv's 128-B lines: sources loaded
+// through the caches (the pairwise StraddleCfg rule), instantiated in the same translation units.
+template <typename T, int OP>
+int multi_straddle_typed(SendList sl, int nsend, unsigned char* r, Split sp, hipStream_t stream);
+template <typename T, int OP>
+int chain_straddle_typed(SendList sl, int nsend, const unsigned char* own, unsigned char* d, Split sp,
+                         hipStream_t stream);
 template <typename T, int OP>
 int chain_phased_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp,
                        hipStream_t stream);
