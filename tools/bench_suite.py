@@ -295,7 +295,7 @@ def phased(results, mib=256):
     for k in (1, 2, 4, 7):
         for what, offs in (("in phase", [0] * k), ("all sources +4 B", [4] * k),
                            ("alternate sources +8 B", [8 * (j % 2) for j in range(k)]),
-                           ("sources +16 B (cached loads)", [16] * k)):
+                           ("sources +16 B (cached loads)", [16] * k), ("sources +20 B", [20] * k)):
             ptrs = [base[j] + offs[j] for j in range(k)]
             r = base[8]
             fm = lambda ptrs=ptrs: dccl_amd.local_reduce_multi(ptrs, r, 7, n, 0, st)
