@@ -196,7 +196,7 @@ int launch_chain_vec(SendList sl, const unsigned char* own, unsigned char* d, Sp
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_chain_vec_kernel<T, OP, K, C>), grid, args, stream, C::BLOCK,
-                  multi_lds(K));
+                  chain_lds(K));
 }
 
 template <typename T, int OP>

@@ -442,6 +442,14 @@ inline constexpr size_t kLdsPerCu = 160u << 10;
 constexpr size_t multi_lds(int k) {
     return kMultiWaves[k] >= 32 ? 0 : (kLdsPerCu / kMultiWaves[k] + 255) / 256 * 256;
 }
+// The in-phase chain kernel's own caps (K sources + own, one store): swept on MI355X at 256 MiB per
+// operand, fp32 Sum (profiles/r1_s5_chain_waves_sweep.json; k = 1, 2, 4, 7 measured, 3, 5, 6
+// interpolated): k = 2 79.5 -> 82.2 % with 24 waves instead of 18, k = 4 81.8 -> 82.9 % with 16
+// instead of 13, k = 1 and 7 unchanged.
+inline constexpr int kChainWaves[9] = {32, 32, 24, 20, 16, 13, 11, 10, 9};
+constexpr size_t chain_lds(int k) {
+    return kChainWaves[k] >= 32 ? 0 : (kLdsPerCu / kChainWaves[k] + 255) / 256 * 256;
+}
 
 constexpr size_t kMaxGrid = size_t(1) << 24;  // grid-stride beyond this (2^24 x 64 threads)
 
