@@ -93,11 +93,6 @@ def _load():
         "dccl_size_of_type": (c_size_t, [c_int]),
         "dccl_result_string": (ctypes.c_char_p, [c_int]),
         "dccl_version": (c_int, []),
-        "dccl_tune_reduce_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_size_t, c_void_p]),
-        "dccl_tune_num_variants": (c_int, []),
-        "dccl_tune_reduce_f32_sum_lds": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_size_t, c_size_t, c_void_p]),
-        "dccl_tune_asm_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
-        "dccl_tune_variant_info": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     }
     sig.update({
         "dccl_comm_init_rank": (c_int, [ctypes.POINTER(c_void_p), ctypes.c_uint32, ctypes.c_uint32]),
@@ -111,16 +106,8 @@ def _load():
         "dccl_reduce_scatter": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
         "dccl_all_gather": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_void_p]),
         "dccl_rccl_available": (c_int, []),
-        "dccl_tune_skew_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p]),
-        "dccl_tune_multi_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_size_t,
-                                            c_void_p]),
+        "dccl_bootstrap_unique_id": (c_int, [ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
         "dccl_synth_fill": (c_int, [c_void_p, c_int, c_size_t, c_int, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),
-        "dccl_tune_ceiling": (c_int, [c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
-        "dccl_tune_write_num_variants": (c_int, []),
-        "dccl_tune_shift_num_variants": (c_int, []),
-        "dccl_tune_pipelined_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_size_t, c_void_p]),
-        "dccl_tune_shift_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_void_p, c_void_p]),
-        "dccl_tune_write_probe": (c_int, [c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
     })
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -135,24 +122,12 @@ lib = _load()
 EXPORTED_SYMBOLS = [
     "dccl_local_reduce", "dccl_local_reduce_multi", "dccl_local_reduce_host",
     "dccl_register_host_memory", "dccl_deregister_host_memory", "dccl_size_of_type",
-    "dccl_result_string", "dccl_version", "dccl_tune_reduce_f32_sum", "dccl_tune_num_variants",
-    "dccl_tune_variant_info", "dccl_tune_asm_f32_sum", "dccl_tune_reduce_f32_sum_lds",
+    "dccl_result_string", "dccl_version",
     "dccl_comm_init_rank", "dccl_get_unique_id", "dccl_comm_init_rccl", "dccl_comm_finalize", "dccl_all_reduce",
-    "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available", "dccl_tune_skew_f32_sum",
-    "dccl_synth_fill", "dccl_tune_multi_f32_sum", "dccl_local_reduce_chain", "dccl_copy_multi",
-    "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_tune_ceiling",
-    "dccl_tune_write_num_variants", "dccl_tune_write_probe", "dccl_tune_shift_num_variants",
-    "dccl_tune_shift_f32_sum", "dccl_local_reduce_chain_host", "dccl_tune_pipelined_f32_sum",
+    "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available", "dccl_bootstrap_unique_id",
+    "dccl_synth_fill", "dccl_local_reduce_chain", "dccl_copy_multi",
+    "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_local_reduce_chain_host",
 ]
-
-
-def tune_variants() -> list[dict]:
-    out = []
-    for v in range(lib.dccl_tune_num_variants()):
-        vals = [ctypes.c_int() for _ in range(4)]
-        lib.dccl_tune_variant_info(v, *[ctypes.byref(x) for x in vals])
-        out.append(dict(zip(("block", "unroll", "policy", "xcd"), (x.value for x in vals))))
-    return out
 
 
 def result_string(code: int) -> str:

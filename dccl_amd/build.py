@@ -5,6 +5,10 @@ C++ ``namespace dccl`` API (include/dccl/dccl.hpp).  Sources compile in parallel
 link is a plain ``hipcc -shared``.  No fast-math / FTZ flags: the combine must keep
 fp32/fp16 denormals (SURVEY.md §7 "Bit-exact semantics").
 
+Tools-only artefacts, never linked into the product library: the tuning variants
+(tools/tune/tune_kernels.hip -> tools/lib/libdccl_amd_tune.so), the dccl_cli harness and the
+plain-C ABI check (dccl_amd/bin/).
+
     python dccl_amd/build.py [--force]      (by path: importing the package loads the library)
 """
 from __future__ import annotations
@@ -25,6 +29,9 @@ CLI_SRC = os.path.join(ROOT, "tools", "dccl_cli.cpp")
 CLI = os.path.join(BIN_DIR, "dccl_cli")
 C_CHECK_SRC = os.path.join(ROOT, "tools", "c_abi_check.c")
 C_CHECK = os.path.join(BIN_DIR, "c_abi_check")
+TUNE_DIR = os.path.join(ROOT, "tools", "tune")
+TUNE_SRC = os.path.join(TUNE_DIR, "tune_kernels.hip")
+TUNE_LIB = os.path.join(ROOT, "tools", "lib", "libdccl_amd_tune.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DCCL_OFFLOAD_ARCH", "gfx950")
 
@@ -43,12 +50,14 @@ def _headers() -> list[str]:
     return hs
 
 
-def _compile(src: str) -> str:
+def _compile(src: str, extra_inc: tuple = ()) -> str:
     obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
-    newest_dep = max(os.path.getmtime(p) for p in _headers() + [src, __file__])
+    deps = _headers() + [src, __file__] + [os.path.join(d, f) for d in extra_inc for f in os.listdir(d)
+                                          if f.endswith(".h")]
+    newest_dep = max(os.path.getmtime(p) for p in deps)
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj
-    cmd = [HIPCC, *COMMON, f"--offload-arch={ARCH}", "-c", src, "-o", obj]
+    cmd = [HIPCC, *COMMON, *[f"-I{d}" for d in extra_inc], f"--offload-arch={ARCH}", "-c", src, "-o", obj]
     if src.endswith(".hip"):
         cmd[1:1] = ["-x", "hip"]
     subprocess.run(cmd, check=True)
@@ -62,13 +71,21 @@ def build(force: bool = False) -> str:
     if force:
         for f in os.listdir(OBJ_DIR):
             os.remove(os.path.join(OBJ_DIR, f))
-    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs) + 1)) as ex:
+        tune_obj = ex.submit(_compile, TUNE_SRC, (TUNE_DIR,))
         objs = list(ex.map(_compile, srcs))
+        tune_obj = tune_obj.result()
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
         tmp = LIB + ".tmp"
         subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp,
                         "-Wl,-soname,libdccl_amd.so"], check=True)
         os.replace(tmp, LIB)
+    # the tuning variants: a tools library of their own, never part of the product library
+    os.makedirs(os.path.dirname(TUNE_LIB), exist_ok=True)
+    if force or not os.path.exists(TUNE_LIB) or os.path.getmtime(TUNE_LIB) < os.path.getmtime(tune_obj):
+        subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", tune_obj, "-o", TUNE_LIB + ".tmp",
+                        "-Wl,-soname,libdccl_amd_tune.so"], check=True)
+        os.replace(TUNE_LIB + ".tmp", TUNE_LIB)
     # the dccl_cli harness (C++ on the namespace-dccl API), rpath'd to the in-tree library
     os.makedirs(BIN_DIR, exist_ok=True)
     if force or not os.path.exists(CLI) or os.path.getmtime(CLI) < max(os.path.getmtime(LIB),

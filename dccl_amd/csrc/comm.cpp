@@ -24,14 +24,20 @@ Group::Group(uint32_t world)
 // Ranks of a collective arrive within microseconds of each other: poll the generation for up to 2 ms
 // (with the pause hint) before blocking on the condition variable, whose wake-up costs tens of
 // microseconds on the critical path of every direct collective (tools/ipc_latency.py).
-void Group::barrier() {
+bool Group::barrier(bool ok) {
     std::unique_lock<std::mutex> lk(bmu_);
     const uint64_t gen = barrier_gen_.load(std::memory_order_relaxed);
+    if (!ok) barrier_bad_ = true;
     if (++barrier_count_ == world_) {
+        // Generation gen+2 cannot complete before every rank of gen has read this slot: each of them must
+        // arrive at gen+1 first, so indexing the outcome by parity is safe.
+        const bool all = !barrier_bad_;
+        barrier_ok_[gen & 1] = all;
         barrier_count_ = 0;
+        barrier_bad_ = false;
         barrier_gen_.store(gen + 1, std::memory_order_release);
         bcv_.notify_all();
-        return;
+        return all;
     }
     lk.unlock();
     const auto start = std::chrono::steady_clock::now();
@@ -44,6 +50,7 @@ void Group::barrier() {
     }
     lk.lock();
     bcv_.wait(lk, [&] { return barrier_gen_.load(std::memory_order_acquire) != gen; });
+    return barrier_ok_[gen & 1];
 }
 
 namespace {
@@ -195,6 +202,13 @@ ncclResult_t ensure_scratch(dccl::dcclComm* c, size_t bytes, bool device) {
 ncclResult_t ensure_work(dccl::dcclComm* c, size_t bytes, bool device) {
     return device ? grow(&c->dev_work, &c->dev_work_bytes, bytes, true)
                   : grow(&c->host_work, &c->host_work_bytes, bytes, false);
+}
+
+bool fault_injected(const char* site, uint32_t rank) {
+    const char* f = std::getenv("DCCL_FAULT_INJECT");
+    if (f == nullptr) return false;
+    const size_t n = std::strlen(site);
+    return std::strncmp(f, site, n) == 0 && f[n] == ':' && std::strtoul(f + n + 1, nullptr, 10) == rank;
 }
 
 ncclResult_t combine(const void* send, void* recv, int dtype, size_t count, int op, bool device,

@@ -55,8 +55,10 @@ public:
     explicit Group(uint32_t world);
     uint32_t world() const { return world_; }
     Channel& channel(uint32_t src, uint32_t dst) { return *chan_[src * world_ + dst]; }
-    // Rendezvous: blocks until every rank arrived (used by init / finalize).
-    void barrier();
+    // Rendezvous: blocks until every rank arrived (init / finalize / the direct collectives' phase
+    // points).  It also agrees on success: returns true iff every rank arrived with ok == true, so a rank
+    // whose step failed still meets the others and they all learn of it at the same point.
+    bool barrier(bool ok = true);
     // HIP device of each rank (-1: none), filled at join; used to enable peer access.
     std::vector<int> devices;
     // Buffer addresses each rank publishes for the direct (peer-read) collectives, direct.cpp.
@@ -74,6 +76,8 @@ private:
     std::mutex bmu_;
     std::condition_variable bcv_;
     uint32_t barrier_count_ = 0;
+    bool barrier_bad_ = false;           // some rank of the open generation arrived with ok == false
+    bool barrier_ok_[2] = {true, true};  // outcome of each generation, indexed by its parity
     std::atomic<uint64_t> barrier_gen_{0};  // written under bmu_, polled without it
 };
 
@@ -131,6 +135,12 @@ ncclResult_t xport_recv_combine(dccl::dcclComm* c, uint32_t peer, void* dst, siz
 // Scratch management (grown on demand, page/line rounded; never shrinks until finalize).
 ncclResult_t ensure_scratch(dccl::dcclComm* c, size_t bytes, bool device);
 ncclResult_t ensure_work(dccl::dcclComm* c, size_t bytes, bool device);
+
+// Test-only fault injection: DCCL_FAULT_INJECT=<site>:<rank> makes `site` fail on that rank, so the
+// tests can check that one rank's failure reaches every member of the group (as an error) instead of
+// leaving peers blocked in a barrier.  Sites: join_events (group formation, dccl_api.cpp),
+// direct_combine (the combine step of the direct collectives, direct.cpp).
+bool fault_injected(const char* site, uint32_t rank);
 
 // Local combine on either side of the host/device boundary.
 ncclResult_t combine(const void* send, void* recv, int dtype, size_t count, int op, bool device,

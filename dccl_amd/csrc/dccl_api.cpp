@@ -24,11 +24,9 @@
 #include <stdexcept>
 #include <string>
 
-#include <chrono>
-#include <fstream>
-#include <thread>
 
 #include "algorithms.hpp"
+#include "bootstrap.hpp"
 #include "comm.hpp"
 #include "direct.hpp"
 #include "rccl_transport.hpp"
@@ -101,6 +99,16 @@ ncclResult_t ring_scratch(dcclComm* c, size_t bytes, bool dev, void** out) {
     return rc;
 }
 
+void destroy_events(dcclComm* c) {
+    for (hipEvent_t& e : c->ready_events)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+    for (hipEvent_t& e : c->done_events)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+}
+
+// In-process group formation.  Once a rank is counted into the group it always reaches both of the
+// group's agreeing barriers, so a failure on any rank (event creation, peer access) comes back as an
+// error on every rank instead of a peer blocked forever; a failed group is discarded by all.
 ncclResult_t join(dcclComm** out, uint32_t world, int64_t want_rank) {
     if (world == 0) return dccl::ncclInvalidArgument;
     if (want_rank >= int64_t(world)) return dccl::ncclInvalidArgument;
@@ -137,26 +145,38 @@ ncclResult_t join(dcclComm** out, uint32_t world, int64_t want_rank) {
     c->done_events.assign(size_t(world) * c->event_ring, nullptr);
     c->sent.assign(world, 0);
     c->received.assign(world, 0);
+    ncclResult_t rc = dccl::ncclSuccess;
+    if (fault_injected("join_events", c->rank)) rc = dccl::ncclUnhandledCudaError;
     if (dev >= 0) {
-        for (size_t i = 0; i < c->ready_events.size(); ++i) {
+        for (size_t i = 0; i < c->ready_events.size() && rc == dccl::ncclSuccess; ++i) {
             if (hipEventCreateWithFlags(&c->ready_events[i], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&c->done_events[i], hipEventDisableTiming) != hipSuccess)
-                return dccl::ncclUnhandledCudaError;
+                hipEventCreateWithFlags(&c->done_events[i], hipEventDisableTiming) != hipSuccess) {
+                (void)hipGetLastError();
+                rc = dccl::ncclUnhandledCudaError;
+            }
         }
     }
-    g->barrier();  // like Derecho's group formation: returns once every member joined
+    // like Derecho's group formation: returns once every member joined (and agrees on success)
+    if (!g->barrier(rc == dccl::ncclSuccess)) {
+        destroy_events(c.get());
+        return rc != dccl::ncclSuccess ? rc : dccl::ncclRemoteError;
+    }
     // Ranks on other GPUs: let this device's kernels and copies read their memory over xGMI.
     if (dev >= 0) {
-        for (uint32_t p = 0; p < world; ++p) {
+        for (uint32_t p = 0; p < world && rc == dccl::ncclSuccess; ++p) {
             const int pd = g->devices[p];
             if (pd < 0 || pd == dev) continue;
             int can = 0;
             if (hipDeviceCanAccessPeer(&can, dev, pd) == hipSuccess && can) {
                 const hipError_t e = hipDeviceEnablePeerAccess(pd, 0);
-                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return dccl::ncclUnhandledCudaError;
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) rc = dccl::ncclUnhandledCudaError;
                 (void)hipGetLastError();
             }
         }
+    }
+    if (!g->barrier(rc == dccl::ncclSuccess)) {
+        destroy_events(c.get());
+        return rc != dccl::ncclSuccess ? rc : dccl::ncclRemoteError;
     }
     *out = c.release();
     return dccl::ncclSuccess;
@@ -175,33 +195,22 @@ ncclResult_t join_rccl(dcclComm** out, uint32_t world, uint32_t rank, const void
     return dccl::ncclSuccess;
 }
 
-// Single-node bootstrap of the RCCL unique id through a file: rank 0 writes it (atomically, by
-// rename), the others poll for it.  Directory: DCCL_BOOTSTRAP_DIR (default /tmp); name tag:
-// DCCL_BOOTSTRAP_TAG, else MASTER_PORT (set by torchrun).
-ncclResult_t bootstrap_unique_id(uint32_t rank, unsigned char* id) {
-    const char* dir = std::getenv("DCCL_BOOTSTRAP_DIR");
-    const char* tag = std::getenv("DCCL_BOOTSTRAP_TAG");
-    if (!tag) tag = std::getenv("MASTER_PORT");
-    const std::string path = std::string(dir ? dir : "/tmp") + "/dccl_rccl_uid_" + (tag ? tag : "default");
+// Single-node bootstrap of the RCCL unique id through a rendezvous file (bootstrap.hpp): rank 0
+// publishes it stamped with its pid, start time and the world size; the others take it only from a live
+// publisher, so a file an earlier job left behind with the same tag is never used.
+ncclResult_t bootstrap_unique_id(uint32_t rank, uint32_t world, unsigned char* id) {
+    const std::string path = rdv_path("dccl_rccl_uid_");
     if (rank == 0) {
         const int rc = rccl_get_unique_id(id);
         if (rc != 0) return static_cast<ncclResult_t>(rc);
-        const std::string tmp = path + ".tmp";
-        {
-            std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
-            f.write(reinterpret_cast<const char*>(id), kRcclUniqueIdBytes);
-            if (!f) return dccl::ncclSystemError;
-        }
-        if (std::rename(tmp.c_str(), path.c_str()) != 0) return dccl::ncclSystemError;
-        return dccl::ncclSuccess;
+        return rdv_publish(path, world, std::string(reinterpret_cast<const char*>(id), kRcclUniqueIdBytes));
     }
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
-    while (std::chrono::steady_clock::now() < deadline) {
-        std::ifstream f(path, std::ios::binary);
-        if (f.read(reinterpret_cast<char*>(id), kRcclUniqueIdBytes)) return dccl::ncclSuccess;
-        std::this_thread::sleep_for(std::chrono::milliseconds(10));
-    }
-    return dccl::ncclSystemError;
+    std::string payload;
+    const ncclResult_t rc = rdv_read(path, world, rdv_timeout_s(), &payload);
+    if (rc != dccl::ncclSuccess) return rc;
+    if (payload.size() != kRcclUniqueIdBytes) return dccl::ncclSystemError;
+    std::memcpy(id, payload.data(), kRcclUniqueIdBytes);
+    return dccl::ncclSuccess;
 }
 
 long env_long(const char* a, const char* b, long dflt) {
@@ -261,9 +270,12 @@ ncclResult_t ncclCommInit(ncclComm_t* comm) {
         const long r = env_long("DCCL_RANK", "RANK", 0);
         if (r < 0 || r >= w) return ncclInvalidArgument;
         unsigned char id[kRcclUniqueIdBytes];
-        const ncclResult_t rc = bootstrap_unique_id(static_cast<uint32_t>(r), id);
+        ncclResult_t rc = bootstrap_unique_id(static_cast<uint32_t>(r), static_cast<uint32_t>(w), id);
         if (rc != ncclSuccess) return rc;
-        return join_rccl(comm, static_cast<uint32_t>(w), static_cast<uint32_t>(r), id);
+        rc = join_rccl(comm, static_cast<uint32_t>(w), static_cast<uint32_t>(r), id);
+        // ncclCommInitRank returns on rank 0 once every rank connected, i.e. read the file
+        if (r == 0) rdv_remove(rdv_path("dccl_rccl_uid_"));
+        return rc;
     }
     return join(comm, static_cast<uint32_t>(w), -1);
 }
@@ -629,3 +641,8 @@ extern "C" int dccl_broadcast(const void* send, void* recv, size_t count, int dt
 }
 
 extern "C" int dccl_rccl_available(void) { return rccl_available(); }
+
+extern "C" int dccl_bootstrap_unique_id(uint32_t rank, uint32_t world, void* id128) {
+    if (id128 == nullptr || world == 0 || rank >= world) return DCCL_INVALID_ARGUMENT;
+    return guarded([&] { return bootstrap_unique_id(rank, world, static_cast<unsigned char*>(id128)); });
+}

@@ -11,13 +11,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
-#include <fstream>
 #include <map>
 #include <random>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "bootstrap.hpp"
 #include "dccl/dccl_reduce.h"
 #include "dispatch.hpp"
 
@@ -63,22 +63,19 @@ struct IpcXport {
 
 IpcXport* xport(const dcclComm* c) { return static_cast<IpcXport*>(c->ipc); }
 
-std::string bootstrap_path() {
-    const char* dir = std::getenv("DCCL_BOOTSTRAP_DIR");
-    const char* tag = std::getenv("DCCL_BOOTSTRAP_TAG");
-    if (!tag) tag = std::getenv("MASTER_PORT");
-    return std::string(dir ? dir : "/tmp") + "/dccl_ipc_name_" + (tag ? tag : "default");
-}
-
-// Sense-reversing barrier on the shared counters; every waiter gives up (and tells the others)
-// after timeout_s, so a dead peer turns into an error instead of a hang.
-ncclResult_t shm_barrier(IpcXport* x) {
+// Sense-reversing barrier on the shared counters that also agrees on success: a rank arriving with
+// ok == false raises the segment's abort flag, and every rank returns ncclRemoteError from a barrier that
+// completes with the flag up.  The flag is sticky (the transport is unusable after a failed collective,
+// like an aborted NCCL communicator).  Every waiter gives up (and tells the others) after timeout_s, so
+// a dead peer turns into an error instead of a hang.
+ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
     ShmCtl* s = x->ctl;
+    if (!ok) s->abort.store(1, std::memory_order_relaxed);
     const uint32_t g = s->gen.load(std::memory_order_acquire);
     if (s->count.fetch_add(1, std::memory_order_acq_rel) + 1 == s->world) {
         s->count.store(0, std::memory_order_relaxed);
         s->gen.store(g + 1, std::memory_order_release);
-        return dccl::ncclSuccess;
+        return s->abort.load(std::memory_order_relaxed) ? dccl::ncclRemoteError : dccl::ncclSuccess;
     }
     // Spin (with the pause hint) for up to kSpin before sleeping: peers arrive within microseconds of
     // each other in a collective, and a 20 us sleep costs 50-80 us once the kernel's timer slack is
@@ -100,7 +97,7 @@ ncclResult_t shm_barrier(IpcXport* x) {
         if (now - start > kSpin) std::this_thread::sleep_for(std::chrono::microseconds(20));
         else std::this_thread::yield();  // a peer without a core of its own gets one
     }
-    return dccl::ncclSuccess;
+    return s->abort.load(std::memory_order_relaxed) ? dccl::ncclRemoteError : dccl::ncclSuccess;
 }
 
 ncclResult_t export_ptr(IpcXport* x, const void* p, unsigned char* handle_out, uint64_t* off_out) {
@@ -166,25 +163,25 @@ struct Peers {
     std::vector<unsigned char*> out;
 };
 
-// This rank's stream has drained (its inputs / outputs are complete) and every rank got here.
-ncclResult_t arrive(dcclComm* c, hipStream_t st) {
-    if (hipStreamSynchronize(st) != hipSuccess) {
+// A phase point of a direct collective: this rank's stream has drained (its inputs / outputs are
+// complete) and every rank got here.  It agrees on success: a rank whose step failed (rc) still comes
+// here, and every rank returns an error from the same phase point if any rank failed, so no rank is
+// left waiting at a later barrier and no rank goes on to read a peer's unfinished chunk.
+ncclResult_t arrive(dcclComm* c, hipStream_t st, ncclResult_t rc = dccl::ncclSuccess) {
+    if (hipStreamSynchronize(st) != hipSuccess) {  // drained even after a failed launch: peers' reads end
         (void)hipGetLastError();
-        if (c->ipc) xport(c)->ctl->abort.store(1);
-        return dccl::ncclUnhandledCudaError;
+        if (rc == dccl::ncclSuccess) rc = dccl::ncclUnhandledCudaError;
     }
-    if (c->ipc) return shm_barrier(xport(c));
-    c->group->barrier();
-    return dccl::ncclSuccess;
+    const bool ok = rc == dccl::ncclSuccess;
+    const ncclResult_t all = c->ipc ? shm_barrier(xport(c), ok)
+                                    : (c->group->barrier(ok) ? dccl::ncclSuccess : dccl::ncclRemoteError);
+    return ok ? all : rc;
 }
 
-ncclResult_t fail(dcclComm* c, ncclResult_t rc) {
-    if (c->ipc && rc != dccl::ncclSuccess) xport(c)->ctl->abort.store(1);
-    return rc;
-}
-
-// Publish (in, out), wait for every rank, then resolve every rank's (in, out) in this process.
-ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Peers* P) {
+// Publish (in, out), meet every rank, then resolve every rank's (in, out) in this process.  *met is
+// false when the meeting itself failed (every rank sees that and returns); when it is true, a non-success
+// return is this rank's own failure to map a peer, which the caller carries into its next phase point.
+ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Peers* P, bool* met) {
     const uint32_t W = c->world, r = c->rank;
     P->in.assign(W, nullptr);
     P->out.assign(W, nullptr);
@@ -193,12 +190,13 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
         ShmSlot& s = xport(c)->ctl->slot[r];
         rc = export_ptr(xport(c), in, s.h_in, &s.off_in);
         if (rc == dccl::ncclSuccess) rc = export_ptr(xport(c), out, s.h_out, &s.off_out);
-        if (rc != dccl::ncclSuccess) return fail(c, rc);
     } else {
         c->group->pub_in[r] = in;
         c->group->pub_out[r] = out;
     }
-    if ((rc = arrive(c, st)) != dccl::ncclSuccess) return rc;
+    rc = arrive(c, st, rc);
+    *met = rc == dccl::ncclSuccess;
+    if (!*met) return rc;
     if (c->ipc) trim_mappings(xport(c), 2 * size_t(W));
     for (uint32_t p = 0; p < W; ++p) {
         if (p == r) {
@@ -210,7 +208,7 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
             unsigned char* po = nullptr;
             rc = import_ptr(xport(c), s.h_in, s.off_in, &pi);
             if (rc == dccl::ncclSuccess) rc = import_ptr(xport(c), s.h_out, s.off_out, &po);
-            if (rc != dccl::ncclSuccess) return fail(c, rc);
+            if (rc != dccl::ncclSuccess) return rc;
             P->in[p] = pi;
             P->out[p] = po;
         } else {
@@ -224,7 +222,8 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
 // dst = the ring's combine chain for one chunk: contributions of ranks first, first+1, ...,
 // first+W-2 (their `in` buffers at byte offset `off`), then `own` last.
 ncclResult_t chain(const Peers& P, uint32_t W, uint32_t first, size_t off, const void* own, void* dst, size_t elems,
-                   int dtype, int op, hipStream_t st) {
+                   int dtype, int op, hipStream_t st, uint32_t rank) {
+    if (fault_injected("direct_combine", rank)) return dccl::ncclUnhandledCudaError;
     const void* sends[kDirectMaxWorld];
     for (uint32_t j = 0; j + 1 < W; ++j) sends[j] = P.in[(first + j) % W] + off;
     return static_cast<ncclResult_t>(
@@ -244,7 +243,9 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
         (void)hipGetLastError();
         return dccl::ncclUnhandledCudaError;
     }
-    const std::string path = bootstrap_path();
+    // rendezvous file stamped by a live rank 0 (bootstrap.hpp): a name an earlier job left behind is never
+    // taken, so no rank maps a stale segment
+    const std::string path = rdv_path("dccl_ipc_name_");
     std::string name;
     int fd = -1;
     if (rank == 0) {
@@ -252,40 +253,50 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
         name = "/dccl_ipc_" + std::to_string(::getpid()) + "_" + std::to_string(rd());
         fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
         if (fd < 0 || ftruncate(fd, sizeof(ShmCtl)) != 0) {
-            if (fd >= 0) ::close(fd);
+            if (fd >= 0) {
+                ::close(fd);
+                shm_unlink(name.c_str());
+            }
             return dccl::ncclSystemError;
         }
     } else {
-        const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
-        while (fd < 0 && std::chrono::steady_clock::now() < deadline) {
-            std::ifstream f(path);
-            if (std::getline(f, name) && !name.empty()) fd = shm_open(name.c_str(), O_RDWR, 0600);
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(rdv_timeout_s());
+        while (fd < 0) {
+            const double left = std::chrono::duration<double>(deadline - std::chrono::steady_clock::now()).count();
+            if (left <= 0 || rdv_read(path, world, left, &name) != dccl::ncclSuccess) return dccl::ncclSystemError;
+            fd = shm_open(name.c_str(), O_RDWR, 0600);
             if (fd < 0) std::this_thread::sleep_for(std::chrono::milliseconds(10));
         }
-        if (fd < 0) return dccl::ncclSystemError;
     }
     void* m = mmap(nullptr, sizeof(ShmCtl), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     ::close(fd);
-    if (m == MAP_FAILED) return dccl::ncclSystemError;
+    if (m == MAP_FAILED) {
+        if (rank == 0) shm_unlink(name.c_str());
+        return dccl::ncclSystemError;
+    }
     auto* ctl = static_cast<ShmCtl*>(m);
     if (rank == 0) {
         std::memset(m, 0, sizeof(ShmCtl));  // fresh segment; atomics are plain words here
         ctl->world = world;
         ctl->magic.store(kMagic, std::memory_order_release);
-        const std::string tmp = path + ".tmp";
-        {
-            std::ofstream f(tmp, std::ios::trunc);
-            f << name << "\n";
-            if (!f) return dccl::ncclSystemError;
+        if (rdv_publish(path, world, name) != dccl::ncclSuccess) {
+            munmap(m, sizeof(ShmCtl));
+            shm_unlink(name.c_str());
+            return dccl::ncclSystemError;
         }
-        if (std::rename(tmp.c_str(), path.c_str()) != 0) return dccl::ncclSystemError;
     } else {
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
         while (ctl->magic.load(std::memory_order_acquire) != kMagic) {
-            if (std::chrono::steady_clock::now() > deadline) return dccl::ncclSystemError;
+            if (std::chrono::steady_clock::now() > deadline) {
+                munmap(m, sizeof(ShmCtl));
+                return dccl::ncclSystemError;
+            }
             std::this_thread::sleep_for(std::chrono::milliseconds(1));
         }
-        if (ctl->world != world) return dccl::ncclInvalidUsage;
+        if (ctl->world != world) {
+            munmap(m, sizeof(ShmCtl));
+            return dccl::ncclInvalidUsage;
+        }
     }
     auto* x = new IpcXport;
     x->ctl = ctl;
@@ -297,7 +308,7 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
     const ncclResult_t rc = shm_barrier(x);  // everyone mapped the segment
     if (rc == dccl::ncclSuccess && rank == 0) {   // nothing left to find by name
         shm_unlink(name.c_str());
-        std::remove(path.c_str());
+        rdv_remove(path);
     }
     return rc;
 }
@@ -335,12 +346,13 @@ ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t
     if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
     const size_t esz = size_of_dtype(dtype), slot_elems = count / W, slot = slot_elems * esz;
     Peers P;
-    ncclResult_t rc = exchange(c, send, recv, st, &P);
-    if (rc != dccl::ncclSuccess) return rc;
+    bool met = false;
+    ncclResult_t rc = exchange(c, send, recv, st, &P, &met);
+    if (!met) return rc;
     const uint32_t mine = (r + 1) % W;
-    rc = chain(P, W, mine, mine * slot, P.in[r] + mine * slot, P.out[r] + mine * slot, slot_elems, dtype, op, st);
-    if (rc != dccl::ncclSuccess) return fail(c, rc);
-    if ((rc = arrive(c, st)) != dccl::ncclSuccess) return rc;  // every chunk reduced by its owner
+    if (rc == dccl::ncclSuccess)
+        rc = chain(P, W, mine, mine * slot, P.in[r] + mine * slot, P.out[r] + mine * slot, slot_elems, dtype, op, st, r);
+    if ((rc = arrive(c, st, rc)) != dccl::ncclSuccess) return rc;  // every chunk reduced by its owner
     std::vector<const void*> src;
     std::vector<void*> dst;
     for (uint32_t k = 0; k < W; ++k) {
@@ -348,8 +360,7 @@ ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t
         src.push_back(P.out[(k + W - 1) % W] + k * slot);  // chunk k lives on rank k-1
         dst.push_back(P.out[r] + k * slot);
     }
-    if ((rc = copy_pairs(src, dst, slot, st)) != dccl::ncclSuccess) return fail(c, rc);
-    return arrive(c, st);  // peers are done reading our buffers
+    return arrive(c, st, copy_pairs(src, dst, slot, st));  // peers are done reading our buffers
 }
 
 bool host_direct_selected(const dcclComm* c, size_t slot_bytes) {
@@ -364,7 +375,8 @@ bool host_direct_selected(const dcclComm* c, size_t slot_bytes) {
 // The same choreography as direct_all_reduce on host memory: rank r reduces chunk r+1 from every rank's
 // input in the ring's order with one staged chain kernel (one GPU round trip instead of the ring's W-1),
 // then copies every other chunk from the rank that reduced it.  Every barrier is reached even after a
-// failed combine, so no rank is left waiting.
+// failed combine, and the barrier after the combine agrees on success: if any rank failed, nobody copies
+// a chunk (it could be unreduced) and every rank returns an error.
 ncclResult_t direct_all_reduce_host(dcclComm* c, const void* send, void* recv, size_t count, int dtype, int op) {
     const uint32_t W = c->world, r = c->rank;
     const size_t esz = size_of_dtype(dtype), slot_elems = count / W, slot = slot_elems * esz;
@@ -376,17 +388,19 @@ ncclResult_t direct_all_reduce_host(dcclComm* c, const void* send, void* recv, s
     const void* sends[kDirectMaxWorld];
     for (uint32_t j = 0; j + 1 < W; ++j)
         sends[j] = static_cast<const unsigned char*>(g.pub_in[(mine + j) % W]) + mine * slot;
-    const ncclResult_t rc = static_cast<ncclResult_t>(dccl_local_reduce_chain_host(
-        sends, int(W - 1), static_cast<const unsigned char*>(send) + mine * slot,
-        static_cast<unsigned char*>(recv) + mine * slot, dtype, slot_elems, op));
-    g.barrier();  // every chunk reduced by its owner
-    if (rc == dccl::ncclSuccess)
+    const ncclResult_t rc = fault_injected("direct_combine", r)
+                                ? dccl::ncclUnhandledCudaError
+                                : static_cast<ncclResult_t>(dccl_local_reduce_chain_host(
+                                      sends, int(W - 1), static_cast<const unsigned char*>(send) + mine * slot,
+                                      static_cast<unsigned char*>(recv) + mine * slot, dtype, slot_elems, op));
+    const bool all = g.barrier(rc == dccl::ncclSuccess);  // every chunk reduced by its owner
+    if (all)
         for (uint32_t k = 0; k < W; ++k)
             if (k != mine)  // chunk k lives on rank k-1
                 std::memcpy(static_cast<unsigned char*>(recv) + k * slot,
                             static_cast<const unsigned char*>(g.pub_out[(k + W - 1) % W]) + k * slot, slot);
     g.barrier();  // peers are done reading our buffers
-    return rc;
+    return rc != dccl::ncclSuccess ? rc : (all ? dccl::ncclSuccess : dccl::ncclRemoteError);
 }
 
 // ncclReduceScatter on host memory: slot r reduced from every rank's input in the order of the ring with
@@ -402,10 +416,13 @@ ncclResult_t direct_reduce_scatter_host(dcclComm* c, const void* send, void* rec
     const void* sends[kDirectMaxWorld];
     for (uint32_t j = 0; j + 1 < W; ++j)
         sends[j] = static_cast<const unsigned char*>(g.pub_in[(r + 1 + j) % W]) + r * slot;
-    const ncclResult_t rc = static_cast<ncclResult_t>(dccl_local_reduce_chain_host(
-        sends, int(W - 1), static_cast<const unsigned char*>(send) + r * slot, recv, dtype, recvcount, op));
-    g.barrier();  // peers are done reading our input
-    return rc;
+    const ncclResult_t rc = fault_injected("direct_combine", r)
+                                ? dccl::ncclUnhandledCudaError
+                                : static_cast<ncclResult_t>(dccl_local_reduce_chain_host(
+                                      sends, int(W - 1), static_cast<const unsigned char*>(send) + r * slot, recv,
+                                      dtype, recvcount, op));
+    const bool all = g.barrier(rc == dccl::ncclSuccess);  // peers are done reading our input
+    return rc != dccl::ncclSuccess ? rc : (all ? dccl::ncclSuccess : dccl::ncclRemoteError);
 }
 
 // ncclReduceScatter: the ring with rank maps (o+W-1)%W / (n+1)%W (dccl.cpp:551-698) leaves slot o on
@@ -416,11 +433,11 @@ ncclResult_t direct_reduce_scatter(dcclComm* c, const void* send, void* recv, si
     if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
     const size_t slot = recvcount * size_of_dtype(dtype);
     Peers P;
-    ncclResult_t rc = exchange(c, send, recv, st, &P);
-    if (rc != dccl::ncclSuccess) return rc;
-    rc = chain(P, W, (r + 1) % W, r * slot, P.in[r] + r * slot, recv, recvcount, dtype, op, st);
-    if (rc != dccl::ncclSuccess) return fail(c, rc);
-    return arrive(c, st);
+    bool met = false;
+    ncclResult_t rc = exchange(c, send, recv, st, &P, &met);
+    if (!met) return rc;
+    if (rc == dccl::ncclSuccess) rc = chain(P, W, (r + 1) % W, r * slot, P.in[r] + r * slot, recv, recvcount, dtype, op, st, r);
+    return arrive(c, st, rc);
 }
 
 // ncclReduce: the reference runs the reduce-scatter ring with the same maps, then gathers the slots
@@ -431,15 +448,14 @@ ncclResult_t direct_reduce(dcclComm* c, const void* send, void* recv, size_t cou
     if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
     const size_t slot_elems = count / W, slot = slot_elems * size_of_dtype(dtype);
     Peers P;
-    ncclResult_t rc = exchange(c, send, r == root ? recv : const_cast<void*>(send), st, &P);
-    if (rc != dccl::ncclSuccess) return rc;
-    if (r == root) {
+    bool met = false;
+    ncclResult_t rc = exchange(c, send, r == root ? recv : const_cast<void*>(send), st, &P, &met);
+    if (!met) return rc;
+    if (r == root)
         for (uint32_t o = 0; o < W && rc == dccl::ncclSuccess; ++o)
             rc = chain(P, W, (o + 1) % W, o * slot, P.in[o] + o * slot, P.out[r] + o * slot, slot_elems, dtype, op,
-                       st);
-        if (rc != dccl::ncclSuccess) return fail(c, rc);
-    }
-    return arrive(c, st);
+                       st, r);
+    return arrive(c, st, rc);
 }
 
 ncclResult_t direct_all_gather(dcclComm* c, const void* send, void* recv, size_t sendcount, int dtype,
@@ -448,17 +464,20 @@ ncclResult_t direct_all_gather(dcclComm* c, const void* send, void* recv, size_t
     if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
     const size_t slot = sendcount * size_of_dtype(dtype);
     Peers P;
-    ncclResult_t rc = exchange(c, send, recv, st, &P);
-    if (rc != dccl::ncclSuccess) return rc;
-    std::vector<const void*> src;
-    std::vector<void*> dst;
-    for (uint32_t p = 0; p < W; ++p) {
-        if (p == r && P.in[r] == P.out[r] + r * slot) continue;  // already in place
-        src.push_back(P.in[p]);
-        dst.push_back(P.out[r] + p * slot);
+    bool met = false;
+    ncclResult_t rc = exchange(c, send, recv, st, &P, &met);
+    if (!met) return rc;
+    if (rc == dccl::ncclSuccess) {
+        std::vector<const void*> src;
+        std::vector<void*> dst;
+        for (uint32_t p = 0; p < W; ++p) {
+            if (p == r && P.in[r] == P.out[r] + r * slot) continue;  // already in place
+            src.push_back(P.in[p]);
+            dst.push_back(P.out[r] + p * slot);
+        }
+        rc = copy_pairs(src, dst, slot, st);
     }
-    if ((rc = copy_pairs(src, dst, slot, st)) != dccl::ncclSuccess) return fail(c, rc);
-    return arrive(c, st);
+    return arrive(c, st, rc);
 }
 
 ncclResult_t direct_broadcast(dcclComm* c, const void* send, void* recv, size_t count, int dtype, uint32_t root,
@@ -466,14 +485,15 @@ ncclResult_t direct_broadcast(dcclComm* c, const void* send, void* recv, size_t 
     const uint32_t r = c->rank;
     const size_t bytes = count * size_of_dtype(dtype);
     Peers P;
-    ncclResult_t rc = exchange(c, r == root ? send : recv, recv, st, &P);
-    if (rc != dccl::ncclSuccess) return rc;
-    if (P.in[root] != P.out[r]) {
+    bool met = false;
+    ncclResult_t rc = exchange(c, r == root ? send : recv, recv, st, &P, &met);
+    if (!met) return rc;
+    if (rc == dccl::ncclSuccess && P.in[root] != P.out[r]) {
         std::vector<const void*> src{P.in[root]};
         std::vector<void*> dst{P.out[r]};
-        if ((rc = copy_pairs(src, dst, bytes, st)) != dccl::ncclSuccess) return fail(c, rc);
+        rc = copy_pairs(src, dst, bytes, st);
     }
-    return arrive(c, st);
+    return arrive(c, st, rc);
 }
 
 }  // namespace dccl_amd

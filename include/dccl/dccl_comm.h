@@ -9,6 +9,11 @@
  *   dccl_comm_init_rccl   GPU; the 128-byte id travels out of band (dcclCommInitRccl)
  *   dccl_comm_init_ipc    cross-process group over the IPC peer-read transport (one process per GPU
  *                         on one node; rendezvous through DCCL_BOOTSTRAP_DIR, dcclCommInitIpc)
+ *   dccl_bootstrap_unique_id  single-node exchange of the RCCL id through DCCL_BOOTSTRAP_DIR: rank 0
+ *                         creates and publishes it, the others wait (DCCL_BOOTSTRAP_TIMEOUT_S, default
+ *                         120 s) for a file published by a LIVE rank 0 of the same world size, so a
+ *                         file an earlier job left behind is never taken (what ncclCommInit does
+ *                         with DCCL_TRANSPORT=rccl)
  *   dccl_all_reduce       ncclAllReduce       (/root/reference/include/dccl/dccl.hpp:206-207)
  *   dccl_reduce_scatter   ncclReduceScatter   (/root/reference/include/dccl/dccl.hpp:243-244)
  *   dccl_all_gather       ncclAllGather       (/root/reference/include/dccl/dccl.hpp:392-393)
@@ -27,6 +32,7 @@ int dccl_comm_init_rank(void** comm, uint32_t world, uint32_t rank);
 int dccl_get_unique_id(void* unique_id_128);
 int dccl_comm_init_rccl(void** comm, uint32_t world, uint32_t rank, const void* unique_id_128);
 int dccl_comm_init_ipc(void** comm, uint32_t world, uint32_t rank);
+int dccl_bootstrap_unique_id(uint32_t rank, uint32_t world, void* unique_id_128);
 int dccl_comm_finalize(void* comm);
 int dccl_all_reduce(const void* send, void* recv, size_t count, int dtype, int op, void* comm, void* stream);
 int dccl_reduce_scatter(const void* send, void* recv, size_t recvcount, int dtype, int op, void* comm,

@@ -1,0 +1,191 @@
+"""Failure paths of group formation, bootstrap and the direct collectives (advisor
+findings on direct.cpp): a failure on one rank must come back as an error on every rank, never as a
+peer blocked in a barrier, and a rendezvous file an earlier job left behind must never be taken.
+
+Every multi-rank case runs in a child process under a hard timeout, so a regression shows up as a
+failed test, not a hung suite.  Fault injection: DCCL_FAULT_INJECT=<site>:<rank> (comm.hpp).
+"""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_child(code: str, env: dict, timeout: float = 60.0) -> dict:
+    full = {**os.environ, **env, "PYTHONPATH": ROOT}
+    p = subprocess.run([sys.executable, "-c", textwrap.dedent(code)], env=full, capture_output=True, text=True,
+                       timeout=timeout)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+JOIN_CHILD = """
+import ctypes, json, threading
+import dccl_amd
+W = int(__import__("os").environ["W"])
+rcs, handles = [None] * W, [None] * W
+
+def rank(r):
+    h = ctypes.c_void_p()
+    rcs[r] = dccl_amd.lib.dccl_comm_init_rank(ctypes.byref(h), W, r)
+    handles[r] = h.value
+
+ts = [threading.Thread(target=rank, args=(r,)) for r in range(W)]
+[t.start() for t in ts]
+[t.join(30) for t in ts]
+hung = [r for r, t in enumerate(ts) if t.is_alive()]
+print(json.dumps({"rcs": rcs, "hung": hung, "handles": [h is not None for h in handles]}))
+"""
+
+
+@pytest.mark.parametrize("W,bad", [(2, 1), (3, 0), (4, 2)])
+def test_join_failure_reaches_every_rank_cpu(W, bad):
+    """One rank fails after it was counted into the group (event creation): every rank returns an error
+    (the failing one its own code, the others ncclRemoteError) and nobody waits forever."""
+    res = run_child(JOIN_CHILD, {"W": str(W), "DCCL_FAULT_INJECT": f"join_events:{bad}"})
+    assert res["hung"] == []
+    assert res["rcs"][bad] == 1
+    assert all(rc == 6 for r, rc in enumerate(res["rcs"]) if r != bad), res
+    assert not any(res["handles"])
+
+
+def test_join_without_fault_then_finalize_cpu():
+    code = JOIN_CHILD + """
+import dccl_amd as d
+fin = [None] * W
+def fin_rank(r):
+    h = handles[r]
+    fin[r] = d.lib.dccl_comm_finalize(ctypes.c_void_p(h)) if h else None
+ts = [threading.Thread(target=fin_rank, args=(r,)) for r in range(W)]
+[t.start() for t in ts]
+[t.join(30) for t in ts]
+print(json.dumps({"rcs": rcs, "fin": fin}))
+"""
+    res = run_child(code, {"W": "3", "DCCL_FAULT_INJECT": ""})
+    assert res["rcs"] == [0, 0, 0] and res["fin"] == [0, 0, 0]
+
+
+# ---------------------------------------------------------------------------------------------
+# bootstrap rendezvous files (bootstrap.cpp)
+# ---------------------------------------------------------------------------------------------
+def _start_time(pid: int) -> int:
+    line = open(f"/proc/{pid}/stat").read()
+    return int(line[line.rindex(")") + 2:].split()[19])
+
+
+def _stamp(pid: int, start: int, world: int, payload: bytes) -> str:
+    return f"DCCLRDV1 {pid} {start} {world} {payload.hex()}\n"
+
+
+@pytest.fixture()
+def rdv(tmp_path, monkeypatch):
+    monkeypatch.setenv("DCCL_BOOTSTRAP_DIR", str(tmp_path))
+    monkeypatch.setenv("DCCL_BOOTSTRAP_TAG", "t_stale")
+    monkeypatch.setenv("DCCL_BOOTSTRAP_TIMEOUT_S", "0.5")
+    return tmp_path / "dccl_rccl_uid_t_stale"
+
+
+def _read_id(world=2, rank=1):
+    import dccl_amd
+    buf = ctypes.create_string_buffer(128)
+    rc = dccl_amd.lib.dccl_bootstrap_unique_id(rank, world, buf)
+    return rc, buf.raw
+
+
+def test_bootstrap_rejects_stale_file_cpu(rdv):
+    """A file stamped by a process that is gone (an earlier job on the same tag) times out instead of
+    handing a dead RCCL id to ncclCommInitRank."""
+    child = subprocess.Popen(["true"])
+    child.wait()
+    dead_pid = child.pid
+    uid = bytes(range(128))
+    rdv.write_text(_stamp(dead_pid, 12345, 2, uid))
+    rc, _ = _read_id()
+    assert rc == 2
+    # a round-1 style file (the raw 128-byte id, no stamp) is not taken either
+    rdv.write_bytes(uid)
+    assert _read_id()[0] == 2
+
+
+def test_bootstrap_accepts_live_publisher_cpu(rdv):
+    uid = bytes((7 * i + 3) % 256 for i in range(128))
+    rdv.write_text(_stamp(os.getpid(), _start_time(os.getpid()), 2, uid))
+    rc, got = _read_id()
+    assert rc == 0 and got == uid
+    # right publisher, wrong world size: another job's file
+    rdv.write_text(_stamp(os.getpid(), _start_time(os.getpid()), 3, uid))
+    assert _read_id()[0] == 2
+    # the live pid but another start time: a recycled pid
+    rdv.write_text(_stamp(os.getpid(), _start_time(os.getpid()) + 1, 2, uid))
+    assert _read_id()[0] == 2
+
+
+def test_bootstrap_argument_checks_cpu():
+    import dccl_amd
+    buf = ctypes.create_string_buffer(128)
+    assert dccl_amd.lib.dccl_bootstrap_unique_id(2, 2, buf) == 4
+    assert dccl_amd.lib.dccl_bootstrap_unique_id(0, 0, buf) == 4
+    assert dccl_amd.lib.dccl_bootstrap_unique_id(0, 2, None) == 4
+
+
+# ---------------------------------------------------------------------------------------------
+# direct collectives: one rank's combine fails
+# ---------------------------------------------------------------------------------------------
+DIRECT_CHILD = """
+import json, os, threading
+import numpy as np
+import dccl_amd
+W, kind = int(os.environ["W"]), os.environ["KIND"]
+n = 1024 * W
+rcs, hung = [None] * W, []
+def body(r):
+    comm = dccl_amd.Comm.in_process(W, r)
+    try:
+        if kind == "device":
+            import torch
+            x = torch.full((n,), float(r + 1), device="cuda")
+            st = torch.cuda.current_stream().cuda_stream
+            rcs[r] = [comm.all_reduce(x.data_ptr(), x.data_ptr(), n, 7, 0, st),
+                      comm.reduce_scatter(x.data_ptr(), x.data_ptr(), n // W, 7, 0, st)]
+        else:
+            x = np.full(n, r + 1, np.float32)
+            y = np.zeros(n // W, np.float32)
+            rcs[r] = [comm.all_reduce(x.ctypes.data, x.ctypes.data, n, 7, 0),
+                      comm.reduce_scatter(x.ctypes.data, y.ctypes.data, n // W, 7, 0)]
+    finally:
+        comm.finalize()
+ts = [threading.Thread(target=body, args=(r,)) for r in range(W)]
+[t.start() for t in ts]
+[t.join(60) for t in ts]
+print(json.dumps({"rcs": rcs, "hung": [r for r, t in enumerate(ts) if t.is_alive()]}))
+"""
+
+
+@pytest.mark.parametrize("W,bad", [(2, 1), (3, 0)])
+def test_direct_host_combine_failure_no_hang_cpu(W, bad):
+    """Host buffers take the direct choreography; without a GPU every rank's staged combine fails, and with
+    the injected fault one rank fails first: no rank may wait forever, every rank reports an error."""
+    res = run_child(DIRECT_CHILD, {"W": str(W), "KIND": "host", "DCCL_FAULT_INJECT": f"direct_combine:{bad}"})
+    assert res["hung"] == []
+    for r in range(W):
+        assert all(rc != 0 for rc in res["rcs"][r]), res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,bad", [(2, 1), (3, 0), (4, 3)])
+@pytest.mark.parametrize("kind", ["device", "host"])
+def test_direct_combine_failure_reaches_every_rank(gpu, W, bad, kind):
+    """On the GPU only the injected rank fails: it returns its own code (1), every peer ncclRemoteError (6),
+    for all_reduce (three phase points) and reduce_scatter alike."""
+    res = run_child(DIRECT_CHILD, {"W": str(W), "KIND": kind, "DCCL_FAULT_INJECT": f"direct_combine:{bad}"},
+                    timeout=120)
+    assert res["hung"] == []
+    for r in range(W):
+        want = 1 if r == bad else 6
+        assert res["rcs"][r] == [want, want], res

@@ -13,7 +13,6 @@
 
 #include "dccl/dccl_comm.h"
 #include "dccl/dccl_reduce.h"
-#include "dccl/dccl_reduce_tuning.h"
 #include "dccl/dccl_synth.h"
 
 static int failures = 0;
@@ -46,7 +45,6 @@ static void cpu_checks(void) {
     CHECK(dccl_synth_fill(NULL, 7, 16, 0, 1, 0, NULL) == DCCL_INVALID_ARGUMENT);
     CHECK(dccl_copy_multi(NULL, NULL, 0, 16, NULL) == DCCL_SUCCESS);
     CHECK(dccl_all_reduce(a, b, 4, 7, 0, NULL, NULL) == DCCL_INVALID_ARGUMENT); /* null communicator */
-    CHECK(dccl_tune_num_variants() > 0);
 }
 
 static void gpu_checks(void) {

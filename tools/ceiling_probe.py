@@ -20,6 +20,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
+from tools import tune_lib  # noqa: E402
 
 KINDS = {0: ("read send", 1), 1: ("read send + recv", 2), 2: ("write recv", 1), 3: ("copy send -> recv", 2),
          4: ("combine recv += send", 3), 5: ("read send + recv, 256x4 blocks", 2),
@@ -42,9 +43,8 @@ def main():
     send.uniform_(-1, 1)
     recv.uniform_(-1, 1)
     st = torch.cuda.current_stream().cuda_stream
-    lib = dccl_amd.lib
     for k in KINDS:
-        assert lib.dccl_tune_ceiling(k, send.data_ptr(), recv.data_ptr(), n, st) == 0, k
+        assert tune_lib.lib.dccl_tune_ceiling(k, send.data_ptr(), recv.data_ptr(), n, st) == 0, k
     streams = [torch.cuda.Stream() for _ in range(max(SPLITS))]
 
     def split_combine(parts):
@@ -71,7 +71,7 @@ def main():
                 if isinstance(k, str):
                     split_combine(int(k[5:]))
                 else:
-                    lib.dccl_tune_ceiling(k, send.data_ptr(), recv.data_ptr(), n, st)
+                    tune_lib.lib.dccl_tune_ceiling(k, send.data_ptr(), recv.data_ptr(), n, st)
             e1.record()
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) / a.iters)
@@ -92,11 +92,11 @@ def main():
     # write-only ceiling over block shapes and store policies (dccl_tune_write_probe)
     import ctypes
     wrows = []
-    nw = lib.dccl_tune_write_num_variants()
+    nw = tune_lib.lib.dccl_tune_write_num_variants()
     shapes = []
     for v in range(nw):
         b, u, pol = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        assert lib.dccl_tune_write_probe(v, recv.data_ptr(), n, ctypes.byref(b), ctypes.byref(u), ctypes.byref(pol),
+        assert tune_lib.lib.dccl_tune_write_probe(v, recv.data_ptr(), n, ctypes.byref(b), ctypes.byref(u), ctypes.byref(pol),
                                          ctypes.c_void_p(~0 & ((1 << 64) - 1))) == 0
         shapes.append((b.value, u.value, ("plain", "nt", "sc1")[pol.value]))
     dummy = [ctypes.c_int() for _ in range(3)]
@@ -106,7 +106,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.iters):
-                lib.dccl_tune_write_probe(v, recv.data_ptr(), n, *[ctypes.byref(x) for x in dummy], st)
+                tune_lib.lib.dccl_tune_write_probe(v, recv.data_ptr(), n, *[ctypes.byref(x) for x in dummy], st)
             e1.record()
             e1.synchronize()
             wt[v].append(e0.elapsed_time(e1) / a.iters)

@@ -10,6 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
+from tools import tune_lib  # noqa: E402
 
 
 def main():
@@ -20,7 +21,7 @@ def main():
     r.uniform_(-1, 1)
     s.uniform_(-1, 1)
     st = torch.cuda.current_stream().cuda_stream
-    info = dccl_amd.tune_variants()
+    info = tune_lib.tune_variants()
     idx = {(v["block"], v["unroll"], v["policy"], v["xcd"]): i for i, v in enumerate(info)}
     cases = {}
     for lds in (0, 6656, 6912, 7168, 7424, 7680, 7936, 8192):
@@ -29,7 +30,7 @@ def main():
         cases[(128, 1, lds)] = idx[(128, 1, 7, 0)]
     for lds in (10240, 12288, 14336, 16384):
         cases[(64, 2, lds)] = idx[(64, 2, 7, 0)]
-    fn = lambda v, lds: dccl_amd.lib.dccl_tune_reduce_f32_sum_lds(s.data_ptr(), r.data_ptr(), n, v, 0, lds, st)
+    fn = lambda v, lds: tune_lib.lib.dccl_tune_reduce_f32_sum_lds(s.data_ptr(), r.data_ptr(), n, v, 0, lds, st)
     for (b, u, lds), v in cases.items():
         assert fn(v, lds) == 0
     torch.cuda.synchronize()

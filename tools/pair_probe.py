@@ -15,6 +15,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
+from tools import tune_lib  # noqa: E402
 from tools.bench_suite import PEAK, time_launches  # noqa: E402
 
 
@@ -34,7 +35,7 @@ def main():
         dccl_amd.check(dccl_amd.synth_fill(s.data_ptr(), 7, n, 0, 0xDCC1, 2 * i, st), "synth")
         dccl_amd.check(dccl_amd.synth_fill(r.data_ptr(), 7, n, 0, 0xDCC1, 2 * i + 1, st), "synth")
         pairs.append((s, r))
-    vinfo = dccl_amd.tune_variants()
+    vinfo = tune_lib.tune_variants()
     want = {(64, 1, 7, 0): "64x1 nt (shipped shape)", (64, 1, 6, 0): "64x1 send cached",
             (64, 1, 7, 1): "64x1 xcd", (128, 1, 7, 0): "128x1", (256, 1, 7, 0): "256x1"}
     variants = [(i, want[(v["block"], v["unroll"], v["policy"], v["xcd"])]) for i, v in enumerate(vinfo)
@@ -43,9 +44,9 @@ def main():
     for pi, (s, r) in enumerate(pairs):
         ps, pr = s.data_ptr(), r.data_ptr()
         cases = [("production", lambda: dccl_amd.local_reduce(ps, pr, 7, n, 0, st))]
-        cases += [(name, lambda i=i: dccl_amd.lib.dccl_tune_reduce_f32_sum(ps, pr, n, i, 0, st)) for i, name in variants]
+        cases += [(name, lambda i=i: tune_lib.lib.dccl_tune_reduce_f32_sum(ps, pr, n, i, 0, st)) for i, name in variants]
         cases.append(("64x1 nt, 22 waves/CU (LDS cap)",
-                      lambda: dccl_amd.lib.dccl_tune_reduce_f32_sum_lds(ps, pr, n, 0, 0, 7168, st)))
+                      lambda: tune_lib.lib.dccl_tune_reduce_f32_sum_lds(ps, pr, n, 0, 0, 7168, st)))
         t = {k: [] for k in range(len(cases))}
         for _ in range(a.rounds):
             for k, (_, fn) in enumerate(cases):

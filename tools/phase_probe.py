@@ -23,6 +23,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
+from tools import tune_lib  # noqa: E402
 from tools.bench_suite import PEAK, time_launches  # noqa: E402
 
 
@@ -32,7 +33,6 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--out", default="")
     a = p.parse_args()
-    lib = dccl_amd.lib
     st = torch.cuda.current_stream().cuda_stream
     nbytes = a.mib << 20
     n = nbytes // 4 - 64  # room for the displacements
@@ -47,18 +47,18 @@ def main():
     for soff, roff in ((4, 0), (8, 0), (12, 0), (0, 4), (20, 8)):
         s, r = send0 + soff, recv0 + roff
         cases.append(("shift", soff, roff, "production", lambda s=s, r=r: dccl_amd.local_reduce(s, r, 7, n, 0, st)))
-        for v in range(lib.dccl_tune_shift_num_variants()):
-            lib.dccl_tune_shift_f32_sum(s, r, 0, v, ctypes.byref(pol), ctypes.byref(xcd), st)
+        for v in range(tune_lib.lib.dccl_tune_shift_num_variants()):
+            tune_lib.lib.dccl_tune_shift_f32_sum(s, r, 0, v, ctypes.byref(pol), ctypes.byref(xcd), st)
             cases.append(("shift", soff, roff, f"policy {pol.value} xcd {xcd.value}",
-                          lambda s=s, r=r, v=v: lib.dccl_tune_shift_f32_sum(s, r, n, v, None, None, st)))
-    vec = dict(enumerate(dccl_amd.tune_variants()))
+                          lambda s=s, r=r, v=v: tune_lib.lib.dccl_tune_shift_f32_sum(s, r, n, v, None, None, st)))
+    vec = dict(enumerate(tune_lib.tune_variants()))
     pick = [i for i, v in vec.items() if v["block"] == 64 and v["unroll"] == 1]
     for soff, roff in ((0, 0), (16, 0), (64, 0), (0, 16), (48, 16)):
         s, r = send0 + soff, recv0 + roff
         cases.append(("line", soff, roff, "production", lambda s=s, r=r: dccl_amd.local_reduce(s, r, 7, n, 0, st)))
         for i in pick:
             cases.append(("line", soff, roff, f"policy {vec[i]['policy']} xcd {vec[i]['xcd']}",
-                          lambda s=s, r=r, i=i: lib.dccl_tune_reduce_f32_sum(s, r, n, i, 0, st)))
+                          lambda s=s, r=r, i=i: tune_lib.lib.dccl_tune_reduce_f32_sum(s, r, n, i, 0, st)))
     times = {k: [] for k in range(len(cases))}
     for _ in range(a.rounds):
         for k, c in enumerate(cases):

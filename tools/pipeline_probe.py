@@ -14,6 +14,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
+from tools import tune_lib  # noqa: E402
 from tools.bench_suite import PEAK, time_launches  # noqa: E402
 
 
@@ -29,7 +30,6 @@ def main():
     recv, send = pool[:nbytes], pool[nbytes + 4096:]
     dccl_amd.check(dccl_amd.synth_fill(send.data_ptr(), 7, n, 0, 0xDCC1, 0, st), "synth")
     dccl_amd.check(dccl_amd.synth_fill(recv.data_ptr(), 7, n, 0, 0xDCC1, 1, st), "synth")
-    lib = dccl_amd.lib
     variants = [(d, g) for d in (1, 2) for g in (256 * 1, 256 * 2, 256 * 4, 256 * 8, 256 * 16, 256 * 32)]
     # correctness: one launch of each variant from the same starting recv equals the shipped kernel's
     r0 = recv.clone()
@@ -37,7 +37,7 @@ def main():
     dccl_amd.check(dccl_amd.local_reduce(send.data_ptr(), want.data_ptr(), 7, n, 0, st), "ref")
     for d, g in variants:
         got = r0.clone()
-        assert lib.dccl_tune_pipelined_f32_sum(send.data_ptr(), got.data_ptr(), n, d, g, st) == 0
+        assert tune_lib.lib.dccl_tune_pipelined_f32_sum(send.data_ptr(), got.data_ptr(), n, d, g, st) == 0
         torch.cuda.synchronize()
         assert torch.equal(got, want), (d, g)
         del got
@@ -45,7 +45,7 @@ def main():
     torch.cuda.empty_cache()
     ps, pr = send.data_ptr(), recv.data_ptr()
     cases = [("shipped (one tile per one-wave block)", lambda: dccl_amd.local_reduce(ps, pr, 7, n, 0, st))]
-    cases += [(f"persistent depth {d} grid {g}", lambda d=d, g=g: lib.dccl_tune_pipelined_f32_sum(ps, pr, n, d, g, st))
+    cases += [(f"persistent depth {d} grid {g}", lambda d=d, g=g: tune_lib.lib.dccl_tune_pipelined_f32_sum(ps, pr, n, d, g, st))
               for d, g in variants]
     t = {k: [] for k in range(len(cases))}
     for _ in range(a.rounds):

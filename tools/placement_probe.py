@@ -17,6 +17,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
+from tools import tune_lib  # noqa: E402
 
 N = (1 << 30) // 4
 ST = 0
@@ -30,7 +31,7 @@ def timeit(sp, rp, rounds=10, iters=10, variant=None):
     if variant is None:
         call = lambda: dccl_amd.local_reduce(sp, rp, 7, N, 0, st)
     else:
-        call = lambda: dccl_amd.lib.dccl_tune_reduce_f32_sum_lds(sp, rp, N, variant, 0, 7 << 10, st)
+        call = lambda: tune_lib.lib.dccl_tune_reduce_f32_sum_lds(sp, rp, N, variant, 0, 7 << 10, st)
     for _ in range(3):
         call()
     torch.cuda.synchronize()
@@ -49,7 +50,7 @@ def timeit(sp, rp, rounds=10, iters=10, variant=None):
 
 def main():
     rows = []
-    info = dccl_amd.tune_variants()
+    info = tune_lib.tune_variants()
     v_plain = next(i for i, v in enumerate(info) if v == {"block": 64, "unroll": 1, "policy": 7, "xcd": 0})
     v_xcd = next(i for i, v in enumerate(info) if v == {"block": 64, "unroll": 1, "policy": 7, "xcd": 1})
     keep = []  # hold allocations so later pairs land elsewhere in physical memory

@@ -1,6 +1,6 @@
 /*
- * include/dccl/dccl_reduce_tuning.h — benchmark/tuning hook, NOT part of the drop-in
- * boundary.  Launches the fp32 Sum combine with an explicit kernel variant so the
+ * tools/tune/dccl_reduce_tuning.h — benchmark/tuning hook, NOT part of the drop-in boundary:
+ * built into tools/lib/libdccl_amd_tune.so, never into the product library libdccl_amd.so.  Launches the fp32 Sum combine with an explicit kernel variant so the
  * tuner (tools/tune_reduce.py) can A/B variants in one process on MI355X.
  *
  * A variant is (block threads, unroll = 16-B vectors per thread per operand in flight,

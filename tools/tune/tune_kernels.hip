@@ -1,12 +1,13 @@
-// dccl_amd/csrc/tune_kernels.hip — tuning-only variants of the fp32 Sum combine (not part of the
-// drop-in boundary; include/dccl/dccl_reduce_tuning.h).  Kept in their own translation unit so their
-// instantiations cannot perturb the production kernel's code generation.
+// tools/tune/tune_kernels.hip — tuning-only variants of the fp32 Sum combine (not part of the drop-in
+// boundary; tools/tune/dccl_reduce_tuning.h).  Built into its own library, tools/lib/libdccl_amd_tune.so
+// (dccl_amd/build.py), so the product library carries none of it, and kept in its own translation unit
+// so its instantiations cannot perturb the production kernel's code generation.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
 #include "dccl/dccl_reduce.h"
-#include "dccl/dccl_reduce_tuning.h"
+#include "dccl_reduce_tuning.h"
 #include "reduce_kernels.hpp"
 
 using namespace dccl_amd;

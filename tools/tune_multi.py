@@ -20,6 +20,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
+from tools import tune_lib  # noqa: E402
 
 PEAK = 8.0e12
 VARIANTS = {0: "64x1 nt-all (shipped)", 1: "64x2 nt-all", 2: "256x1 nt-all", 3: "64x1 nt-send", 4: "64x4 nt-all",
@@ -84,11 +85,11 @@ def main():
             row["shipped_ms"] = round(ms, 4)
             row["shipped_frac"] = round((k + 2) * nbytes / (ms * 1e-3) / PEAK, 4)
             for v in VARIANTS:
-                ms = median_ms(lambda: dccl_amd.lib.dccl_tune_multi_f32_sum(arr, k, recv, n, v, 0, st))
+                ms = median_ms(lambda: tune_lib.lib.dccl_tune_multi_f32_sum(arr, k, recv, n, v, 0, st))
                 row[f"v{v}_ms"] = round(ms, 4)
                 row[f"v{v}_frac"] = round((k + 2) * nbytes / (ms * 1e-3) / PEAK, 4)
             for w in ([] if a.no_waves else WAVES):
-                ms = median_ms(lambda: dccl_amd.lib.dccl_tune_multi_f32_sum(arr, k, recv, n, 0, lds_for(w), st))
+                ms = median_ms(lambda: tune_lib.lib.dccl_tune_multi_f32_sum(arr, k, recv, n, 0, lds_for(w), st))
                 row[f"w{w}_frac"] = round((k + 2) * nbytes / (ms * 1e-3) / PEAK, 4)
             rows.append(row)
             print(json.dumps(row), flush=True)

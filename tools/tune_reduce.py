@@ -21,6 +21,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
+from tools import tune_lib  # noqa: E402
 
 
 def main():
@@ -37,8 +38,7 @@ def main():
     r = torch.rand(n, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    info = dccl_amd.tune_variants()
-    lib = dccl_amd.lib
+    info = tune_lib.tune_variants()
 
     # placement experiment: one allocation, send at recv + n*4 + delta
     big = torch.empty(2 * n + (8 << 20) // 4, device="cuda")
@@ -46,29 +46,29 @@ def main():
 
     cases = {}
     for v, inf in enumerate(info):
-        cases[("tpl", v, 0)] = (lambda v=v: lib.dccl_tune_reduce_f32_sum(s.data_ptr(), r.data_ptr(), n, v, 0, st),
+        cases[("tpl", v, 0)] = (lambda v=v: tune_lib.lib.dccl_tune_reduce_f32_sum(s.data_ptr(), r.data_ptr(), n, v, 0, st),
                                 {**inf, "kind": "template", "grid_cap": 0})
         if inf["block"] == 256 and inf["unroll"] == 4 and inf["policy"] == 7:
             for k in (4, 16):
                 cap = cus * k
                 cases[("tpl", v, cap)] = (
-                    lambda v=v, cap=cap: lib.dccl_tune_reduce_f32_sum(s.data_ptr(), r.data_ptr(), n, v, cap, st),
+                    lambda v=v, cap=cap: tune_lib.lib.dccl_tune_reduce_f32_sum(s.data_ptr(), r.data_ptr(), n, v, cap, st),
                     {**inf, "kind": "template", "grid_cap": cap})
     for lds in [int(a.lds_kib * 1024)] if a.lds_kib else (5 << 10, 6 << 10, 7 << 10, 8 << 10, 9 << 10, 10 << 10, 20 << 10):
         cases[("lds", lds)] = (
-            lambda lds=lds: lib.dccl_tune_reduce_f32_sum_lds(s.data_ptr(), r.data_ptr(), n, 0, 0, lds, st),
+            lambda lds=lds: tune_lib.lib.dccl_tune_reduce_f32_sum_lds(s.data_ptr(), r.data_ptr(), n, 0, 0, lds, st),
             {"kind": "occupancy", "variant": info[0], "lds_bytes": lds, "max_waves_per_cu": (160 << 10) // lds})
     for waves, skew in ((8, 0), (8, 1), (8, 2), (8, 4), (4, 0), (4, 2), (16, 8), (16, 4)):
         cases[("skew", waves, skew)] = (
-            lambda waves=waves, skew=skew: lib.dccl_tune_skew_f32_sum(s.data_ptr(), r.data_ptr(), n, waves, skew, st),
+            lambda waves=waves, skew=skew: tune_lib.lib.dccl_tune_skew_f32_sum(s.data_ptr(), r.data_ptr(), n, waves, skew, st),
             {"kind": "skew", "waves": waves, "skew_kib": skew})
     for fl in range(7):
-        cases[("asm", fl)] = (lambda fl=fl: lib.dccl_tune_asm_f32_sum(s.data_ptr(), r.data_ptr(), n, fl, st),
+        cases[("asm", fl)] = (lambda fl=fl: tune_lib.lib.dccl_tune_asm_f32_sum(s.data_ptr(), r.data_ptr(), n, fl, st),
                               {"kind": "asm", "flavor": fl})
     for d in deltas:
         rp = big.data_ptr()
         sp = rp + n * 4 + d
-        cases[("place", d)] = (lambda sp=sp, rp=rp: lib.dccl_tune_reduce_f32_sum(sp, rp, n, 0, 0, st),
+        cases[("place", d)] = (lambda sp=sp, rp=rp: tune_lib.lib.dccl_tune_reduce_f32_sum(sp, rp, n, 0, 0, st),
                                {"kind": "placement", "variant": info[0], "send_minus_recv_end": d})
     if a.only:
         keep = set(a.only.split(","))

@@ -15,6 +15,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
+from tools import tune_lib  # noqa: E402
 from tools.bench_suite import time_launches  # noqa: E402
 
 
@@ -31,9 +32,9 @@ def main():
     r = torch.zeros(n, dtype=torch.float32).pin_memory()
     ps, pr = s.data_ptr(), r.data_ptr()  # ROCm maps page-locked memory at the same address on the device
     cases = [("production", lambda: dccl_amd.local_reduce(ps, pr, 7, n, 0, st))]
-    for i, v in enumerate(dccl_amd.tune_variants()):
+    for i, v in enumerate(tune_lib.tune_variants()):
         cases.append((f"{v['block']}x{v['unroll']} policy {v['policy']} xcd {v['xcd']}",
-                      lambda i=i: dccl_amd.lib.dccl_tune_reduce_f32_sum(ps, pr, n, i, 0, st)))
+                      lambda i=i: tune_lib.lib.dccl_tune_reduce_f32_sum(ps, pr, n, i, 0, st)))
     times = {k: [] for k in range(len(cases))}
     for _ in range(a.rounds):
         for k, (_, fn) in enumerate(cases):
