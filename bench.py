@@ -16,9 +16,11 @@ Rank 0 prints ONE JSON line:
   roofline         dominant kernel (the combine): algorithmic bytes per launch / average
                    launch duration (HIP events around the timed region on the launch stream,
                    divided by the steps), vs 8.0 TB/s HBM peak;
-                   `traffic` = PMC HBM bytes per launch from profiles/pmc_traffic.json when present
-  cpu_baseline     the reference's own CPU loop (oracle/_ref, Release flags) or the oracle
-                   restatement, single thread, timed on this host on a bounded sample (rank 0, N=1)
+                   `traffic` = HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+                   run during the bench (N=1) over the same kernel and layout (measured_traffic)
+  cpu_baseline     the build's C restatement of the reference loop (oracle/host_reduce.c, Release flags)
+                   on the headline's own 1 GiB operands in host memory: 1 core and every core this
+                   process may use (rank 0, N=1); nproc and the CPU model are stated
 Extra keys: payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
 rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately),
 c5 (BASELINE config C5 on every run: --c5-gib GiB per operand sharded over the N GPUs, strong scaling,
@@ -33,6 +35,7 @@ Progress goes to stderr, one line per phase.
 from __future__ import annotations
 
 import argparse
+import csv
 import json
 import os
 import sys
@@ -69,6 +72,8 @@ def parse():
     p.add_argument("--c5-gib", type=float, default=16.0,
                    help="BASELINE C5 extra on every run: one buffer of this many GiB per operand sharded over "
                         "the N GPUs, combine + RCCL all-gather, reported as `c5` (0 disables)")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip the rocprofv3 --pmc passes that measure roofline.traffic (N=1)")
     p.add_argument("--no-other-layout", action="store_true",
                    help="skip timing the other operand layout (profiling runs: one layout per kernel average)")
     p.add_argument("--layout", default="pooled", choices=["pooled", "separate"],
@@ -106,6 +111,37 @@ def operand_pair(n: int, dt: int, op: int, buffer_id: int, device, layout: str):
     return send, recv
 
 
+def verify_sample(recv: torch.Tensor, n: int, dt: int, op: int, send_id: int, recv_id: int, applications: int,
+                  width: int = 1 << 16) -> bool | None:
+    """Check sampled slices of a combined operand: the first and last `width` elements and four seeded
+    random slices.  Their inputs are regenerated on the device (dccl_synth_fill_range, the same counter-based
+    values at the same indices), the combine is applied `applications` times in order by plain torch ops
+    (IEEE arithmetic and compare-select, as the reference's do_host_reduce applies them,
+    internal_common.hpp:546-549), and the result must match the HIP kernel's bit for bit.
+    None when torch lacks the dtype's ops."""
+    import random
+    tdt = dccl_amd.TORCH_DTYPES.get(dt)
+    if tdt is None or dt in (3, 5):
+        return None
+    ops = {0: lambda r, s: r + s, 1: lambda r, s: r * s,
+           2: lambda r, s: torch.where(r < s, s, r), 3: lambda r, s: torch.where(r > s, s, r)}
+    width = min(width, n)
+    rnd = random.Random(0xDCC1 + recv_id)
+    starts = sorted({0, n - width, *(rnd.randrange(0, n - width + 1) for _ in range(4))})
+    st = torch.cuda.current_stream(recv.device).cuda_stream
+    for a0 in starts:
+        sv = torch.empty(width, dtype=tdt, device=recv.device)
+        want = torch.empty(width, dtype=tdt, device=recv.device)
+        dccl_amd.check(dccl_amd.synth_fill_range(sv.data_ptr(), dt, width, op, SEED, send_id, a0, st), "synth")
+        dccl_amd.check(dccl_amd.synth_fill_range(want.data_ptr(), dt, width, op, SEED, recv_id, a0, st), "synth")
+        for _ in range(applications):
+            want = ops[op](want, sv)
+        got = recv[a0:a0 + width]
+        if got.view(torch.uint8).cpu().numpy().tobytes() != want.view(torch.uint8).cpu().numpy().tobytes():
+            return False
+    return True
+
+
 def time_kernel(ps: int, pr: int, dt: int, n: int, op: int, stream, steps: int) -> float:
     """Average launch duration (ms) over `steps` back-to-back launches, HIP events on `stream`."""
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -124,21 +160,21 @@ import json, sys, time
 sys.path.insert(0, sys.argv[1])
 import oracle
 n, budget = int(sys.argv[2]), float(sys.argv[3])
-nat = oracle.reference_native()
+nat = oracle.restatement_native()
 if nat is None:
     print(json.dumps(None)); sys.exit(0)
 s = oracle.synth(n, 7, 0, 0xDCC1, 0); r = oracle.synth(n, 7, 0, 0xDCC1, 1)
-nat.ref_host_reduce(s.ctypes.data, r.ctypes.data, n, 7, 0)
+nat.oracle_host_reduce(s.ctypes.data, r.ctypes.data, n, 7, 0)
 reps, t0 = 0, time.perf_counter()
 while time.perf_counter() - t0 < budget:
-    nat.ref_host_reduce(s.ctypes.data, r.ctypes.data, n, 7, 0); reps += 1
+    nat.oracle_host_reduce(s.ctypes.data, r.ctypes.data, n, 7, 0); reps += 1
 print(json.dumps({"seconds_per_pass": (time.perf_counter() - t0) / reps, "passes": reps}))
 """
 
 
 def native_variant(budget_s: float, n: int) -> dict | None:
-    """The reference loop with its Benchmark flags (-Ofast -march=native, CMakeLists.txt:26), a labelled
-    variant.  It was compiled for the build container's CPU, so it runs in a child process: an
+    """The restatement with the reference's Benchmark flags (-Ofast -march=native, CMakeLists.txt:26), a
+    labelled variant.  It was compiled for the build container's CPU, so it runs in a child process: an
     instruction the box's CPU lacks ends the child, not the bench."""
     import subprocess
     try:
@@ -156,32 +192,40 @@ def native_variant(budget_s: float, n: int) -> dict | None:
             "passes": res["passes"], "flags": "-Ofast -march=native (reference Benchmark build, build-container CPU)"}
 
 
-def cpu_baseline(budget_s: float) -> dict | None:
-    """Reference CPU loop (oracle/_ref) single-threaded, plus all host threads, fp32 Sum."""
+def cpu_baseline(budget_s: float, nbytes: int) -> dict | None:
+    """the build's C restatement of the reference loop (oracle/host_reduce.c, the combine
+    of internal_common.hpp:496-586 with its head/pack/tail split) compiled with the reference's Release
+    flags (-O3 -mprefer-vector-width=512, CMakeLists.txt:25), on the headline's own operands: the same
+    counter-based fp32 values, 1 GiB per operand, in host memory.  Timed (i) on 1 core, as the reference
+    runs its combine (one thread per rank), and (ii) on every core this process may use, the buffer split
+    into 64-B aligned contiguous slices, one persistent thread each (ctypes drops the GIL)."""
     try:
         import oracle  # test infrastructure: the CPU baseline leg only
     except Exception:
         return None
-    ref = oracle.reference()
-    kind = "reference" if ref is not None else "port"
-    fn = (lambda s, r, n: ref.ref_host_reduce(s, r, n, 7, 0)) if ref is not None else \
-        (lambda s, r, n: oracle.restatement().oracle_host_reduce(s, r, n, 7, 0))
-    n = (256 << 20) // 4  # 256 MiB per operand sample (BASELINE config C2 size)
-    s = oracle.synth(n, 7, 0, SEED, 0)  # the same counter-based operands as the device run
-    r = oracle.synth(n, 7, 0, SEED, 1)
-    ps, pr = s.ctypes.data, r.ctypes.data
-    fn(ps, pr, n)  # page in
-    reps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s * 0.45:
-        fn(ps, pr, n)
-        reps += 1
-    t1 = (time.perf_counter() - t0) / reps
-    native = native_variant(budget_s * 0.2, n)
-    # the box's CPU share (OMP_NUM_THREADS; 16 per GPU on the pool): 64-B aligned contiguous
-    # slices, one persistent thread each (ctypes drops the GIL during the call)
+    lib = oracle.restatement()
+    fn = lambda s, r, n: lib.oracle_host_reduce(s, r, n, 7, 0)  # noqa: E731
+    n = nbytes // 4
     nthr = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
     per = (n // nthr) // 16 * 16
     bounds = [(i * per, n if i == nthr - 1 else (i + 1) * per) for i in range(nthr)]
+    s = oracle.aligned_empty(n, np.float32)
+    r = oracle.aligned_empty(n, np.float32)
+
+    def gen(b):  # the device generator's values, regenerated on the host in parallel slices
+        for arr, bid in ((s, 0), (r, 1)):
+            rc = lib.oracle_synth_fill(arr.ctypes.data + 4 * b[0], 7, b[1] - b[0], 0, SEED, bid, b[0])
+            assert rc == 0
+
+    with ThreadPoolExecutor(max_workers=nthr) as pool:
+        list(pool.map(gen, bounds))
+    ps, pr = s.ctypes.data, r.ctypes.data
+    fn(ps, pr, n)  # page in
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s * 0.4 or reps < 2:
+        fn(ps, pr, n)
+        reps += 1
+    t1 = (time.perf_counter() - t0) / reps
 
     def work(b):
         fn(ps + 4 * b[0], pr + 4 * b[0], b[1] - b[0])
@@ -190,11 +234,12 @@ def cpu_baseline(budget_s: float) -> dict | None:
     with ThreadPoolExecutor(max_workers=nthr) as pool:
         list(pool.map(work, bounds))  # warm the threads
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < budget_s * 0.35 or reps_mt == 0:
+        while time.perf_counter() - t0 < budget_s * 0.3 or reps_mt < 2:
             list(pool.map(work, bounds))
             reps_mt += 1
         tmt = (time.perf_counter() - t0) / reps_mt
-    nbytes = n * 4
+    del s, r
+    native = native_variant(budget_s * 0.3, n)
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -205,15 +250,65 @@ def cpu_baseline(budget_s: float) -> dict | None:
         pass
     return {
         "value": round(3 * nbytes / t1 / GIB, 2), "unit": "GiB/s (HBM-traffic basis 3*N*4 B, fp32 Sum)",
-        "cores": 1, "kind": kind,
-        "sample": f"fp32 Sum, 256 MiB per operand host buffers (64-B aligned, splitmix64 operands, seed 0xDCC1), "
-                  f"{reps} passes in {t1 * reps:.1f}s, Release flags -O3 -mprefer-vector-width=512",
+        "cores": 1, "kind": "port",
+        "sample": f"fp32 Sum, 1 GiB per operand in host memory (the headline's operands: splitmix64, seed 0xDCC1, "
+                  f"64-B aligned), {reps} passes in {t1 * reps:.1f}s; oracle/host_reduce.c (restatement of "
+                  f"internal_common.hpp:496-586) with the Release flags -O3 -mprefer-vector-width=512",
         "payload_gib_s": round(nbytes / t1 / GIB, 2),
+        "ms_per_pass": round(t1 * 1e3, 2),
         "all_cores": {"value": round(3 * nbytes / tmt / GIB, 2), "cores": nthr, "passes": reps_mt,
-                      "payload_gib_s": round(nbytes / tmt / GIB, 2)},
+                      "payload_gib_s": round(nbytes / tmt / GIB, 2), "ms_per_pass": round(tmt * 1e3, 2),
+                      "slices": "64-B aligned contiguous, one thread each"},
+        "nproc": len(os.sched_getaffinity(0)), "machine_cpus": os.cpu_count(),
         "native_flags_variant": native,
         "cpu_model": cpu_model,
     }
+
+
+def measured_traffic(nbytes: int, dt: int, op: int, launches: int = 5) -> dict:
+    """roofline.traffic, measured in this run: two rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE: they
+    do not fit one pass on gfx950) over dccl_amd/bin/pmc_combine, which runs the same kernel on operands of
+    the same size and layout.  Per launch, read = 2 x FETCH_SIZE (gfx950 reports half the bytes of 16-B-per-
+    lane streaming reads) and write = WRITE_SIZE (exact for 16-B stores), both in KiB
+    (MI355X_MICROARCH.md §HBM).  Any failure is reported, never fatal."""
+    import glob
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        return {"skipped": "bench.py itself runs under rocprofv3"}
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    binary = os.path.join(ROOT, "dccl_amd", "bin", "pmc_combine")
+    if not (os.path.exists(prof) and os.path.exists(binary)):
+        return {"error": "rocprofv3 or dccl_amd/bin/pmc_combine missing"}
+    vals = {}
+    with tempfile.TemporaryDirectory(prefix="dccl_pmc_") as d:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            cmd = ["timeout", "-s", "KILL", "90", prof, "--pmc", counter, "--output-format", "csv",
+                   "-d", os.path.join(d, counter), "-o", "p", "--", binary, str(nbytes), str(launches), str(dt),
+                   str(op)]
+            try:
+                p = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+            except subprocess.TimeoutExpired:
+                return {"error": f"{counter} pass timed out"}
+            if p.returncode != 0:
+                return {"error": f"{counter} pass exited with {p.returncode}", "stderr": p.stderr[-300:]}
+            rows = []
+            for path in glob.glob(os.path.join(d, counter, "**", "*counter_collection.csv"), recursive=True):
+                with open(path) as f:
+                    rows += [float(r["Counter_Value"]) for r in csv.DictReader(f)
+                             if "reduce_vec_kernel" in r.get("Kernel_Name", "") and r["Counter_Name"] == counter]
+            if len(rows) != launches:
+                return {"error": f"{counter}: {len(rows)} dispatches found, {launches} expected"}
+            vals[counter] = statistics.median(rows)
+    read_b, write_b = 2 * vals["FETCH_SIZE"] * 1024, vals["WRITE_SIZE"] * 1024
+    return {"hbm_bytes_per_launch": read_b + write_b, "read_bytes": read_b, "write_bytes": write_b,
+            "over_algorithmic": round((read_b + write_b) / (3 * nbytes), 6), "launches": launches,
+            "FETCH_SIZE_kb": vals["FETCH_SIZE"], "WRITE_SIZE_kb": vals["WRITE_SIZE"],
+            "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) during this run over "
+                   "dccl_amd/bin/pmc_combine (same kernel, operand size and pooled layout); "
+                   "read = 2 x FETCH_SIZE x 1024 (gfx950 halving), write = WRITE_SIZE x 1024"}
 
 
 def host_staged_rate(nbytes: int, dt: int, op: int) -> dict:
@@ -418,11 +513,19 @@ def c5_extra(a, world: int, rank: int, dev, backend: str, coll_dev) -> dict:
 
     tc = bracket(lambda: dccl_amd.check(dccl_amd.local_reduce(send.data_ptr(), recv.data_ptr(), dt, n, op,
                                                                stream.cuda_stream)), steps)
+    # every rank checks sampled slices of its combined shard (2 + steps applications), then all agree
+    ok = verify_sample(recv, n, dt, op, 2 * rank, 2 * rank + 1, 2 + steps)
+    if world > 1:
+        flag = torch.tensor([int(bool(ok))], dtype=torch.int32, device=coll_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = bool(flag[0])
     out = {"total_gib_per_operand": a.c5_gib, "shard_bytes_per_operand_max": max(b - a_ for a_, b in bounds) * esz,
            "steps": steps, "combine_ms": round(tc * 1e3, 4),
            "value": round(3 * total * esz / tc / GIB, 2), "unit": "GiB/s (3*N*4 B over all GPUs)",
            "frac_of_n_hbm_peaks": round(3 * total * esz / tc / 1e9 / (HBM_PEAK_GBS * world), 4),
-           "scaling": "strong"}
+           "scaling": "strong", "verified": ok,
+           "verification": "every rank: first, last and 4 random 64 Ki-element slices of its shard, inputs "
+                           "regenerated on the device, 12 sequential torch fp32 adds, bit-exact"}
     del send
     if world > 1:
         width = max(b - a_ for a_, b in bounds)
@@ -583,6 +686,12 @@ def main():
         kern_ms_max = kern_ms
     ms_per_step = elapsed / a.steps * 1e3
     progress(f"timed region done: {ms_per_step:.4f} ms per step, kernel {kern_ms:.4f} ms")
+    # the timed combines' result, sampled: warmup + steps applications of the op on this rank's operands
+    ok = verify_sample(recv, n, dt, op, 2 * rank, 2 * rank + 1, a.warmup + a.steps)
+    if world > 1:
+        flag = torch.tensor([-1 if ok is None else int(ok)], dtype=torch.int32, device=coll_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = None if int(flag[0]) < 0 else bool(flag[0])
 
     extra = {}
     # the other operand layout, timed briefly on every rank (reported, never in `value`)
@@ -634,13 +743,11 @@ def main():
                                                           a.c5_gib if backend == "nccl" else min(a.c5_gib, 1.0))
 
     if rank == 0:
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path) and dt == 7 and op == 0 and nbytes == 1 << 30:
-            try:
-                traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
+        traffic, traffic_detail = None, None
+        if world == 1 and not a.no_pmc:
+            progress("rocprofv3 --pmc passes for roofline.traffic")
+            traffic_detail = measured_traffic(nbytes, dt, op)
+            traffic = traffic_detail.get("hbm_bytes_per_launch")
         achieved = 3 * nbytes / (kern_ms * 1e-3) / 1e9
         res = {
             "metric": "device-resident reduce GiB/s (ncclSum fp32, 1 GiB) at 1/2/4/8 GPU vs HBM peak",
@@ -661,15 +768,17 @@ def main():
             "payload_gib_s": round(total_bytes / (ms_per_step * 1e-3) / GIB, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_measurement": traffic_detail,
                          "kernel": "reduce_vec_kernel (dccl_local_reduce)",
                          "kernel_ms_avg": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_ms_max, 4),
                          "bytes_per_launch": 3 * nbytes, "operand_layout": a.layout},
         }
+        res["verified"] = ok
         res.update(extra)
         if world == 1 and not a.no_host_staged:
             res["host_staged"] = host_staged_rate(nbytes, dt, op)
         if world == 1 and not a.no_cpu:
-            res["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(a.cpu_seconds, nbytes)
         print(json.dumps(res), flush=True)
     if world > 1:
         try:

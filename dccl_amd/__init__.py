@@ -108,6 +108,8 @@ def _load():
         "dccl_rccl_available": (c_int, []),
         "dccl_bootstrap_unique_id": (c_int, [ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
         "dccl_synth_fill": (c_int, [c_void_p, c_int, c_size_t, c_int, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),
+        "dccl_synth_fill_range": (c_int, [c_void_p, c_int, c_size_t, c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                          c_size_t, c_void_p]),
     })
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -125,7 +127,7 @@ EXPORTED_SYMBOLS = [
     "dccl_result_string", "dccl_version",
     "dccl_comm_init_rank", "dccl_get_unique_id", "dccl_comm_init_rccl", "dccl_comm_finalize", "dccl_all_reduce",
     "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available", "dccl_bootstrap_unique_id",
-    "dccl_synth_fill", "dccl_local_reduce_chain", "dccl_copy_multi",
+    "dccl_synth_fill", "dccl_synth_fill_range", "dccl_local_reduce_chain", "dccl_copy_multi",
     "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_local_reduce_chain_host",
 ]
 
@@ -182,6 +184,13 @@ def local_reduce_host(send_ptr: int, recv_ptr: int, dtype: int, count: int, op: 
 def synth_fill(ptr: int, dtype: int, count: int, op: int, seed: int, buffer_id: int, stream: int = 0) -> int:
     """Counter-based synthetic operand in device memory (include/dccl/dccl_synth.h)."""
     return int(lib.dccl_synth_fill(ptr, int(dtype), int(count), int(op), int(seed), int(buffer_id), stream or None))
+
+
+def synth_fill_range(ptr: int, dtype: int, count: int, op: int, seed: int, buffer_id: int, first: int,
+                     stream: int = 0) -> int:
+    """Elements [first, first + count) of the same synthetic operand."""
+    return int(lib.dccl_synth_fill_range(ptr, int(dtype), int(count), int(op), int(seed), int(buffer_id),
+                                         int(first), stream or None))
 
 
 def register_host_memory(ptr: int, size: int) -> int:

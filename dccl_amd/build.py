@@ -29,6 +29,8 @@ CLI_SRC = os.path.join(ROOT, "tools", "dccl_cli.cpp")
 CLI = os.path.join(BIN_DIR, "dccl_cli")
 C_CHECK_SRC = os.path.join(ROOT, "tools", "c_abi_check.c")
 C_CHECK = os.path.join(BIN_DIR, "c_abi_check")
+PMC_SRC = os.path.join(ROOT, "tools", "pmc_combine.cpp")
+PMC_BIN = os.path.join(BIN_DIR, "pmc_combine")
 TUNE_DIR = os.path.join(ROOT, "tools", "tune")
 TUNE_SRC = os.path.join(TUNE_DIR, "tune_kernels.hip")
 TUNE_LIB = os.path.join(ROOT, "tools", "lib", "libdccl_amd_tune.so")
@@ -92,6 +94,11 @@ def build(force: bool = False) -> str:
                                                                           os.path.getmtime(CLI_SRC)):
         subprocess.run([HIPCC, *COMMON, CLI_SRC, "-o", CLI, f"-L{OUT_DIR}", "-ldccl_amd",
                         "-Wl,-rpath,$ORIGIN/../lib", "-pthread"], check=True)
+    # the bench's combine as a bare process, for the rocprofv3 --pmc passes bench.py runs (roofline.traffic)
+    if force or not os.path.exists(PMC_BIN) or os.path.getmtime(PMC_BIN) < max(os.path.getmtime(LIB),
+                                                                                os.path.getmtime(PMC_SRC)):
+        subprocess.run([HIPCC, *COMMON, PMC_SRC, "-o", PMC_BIN, f"-L{OUT_DIR}", "-ldccl_amd",
+                        "-Wl,-rpath,$ORIGIN/../lib"], check=True)
     # a plain C11 consumer of the C-ABI headers (gcc, no C++ / HIP headers)
     if force or not os.path.exists(C_CHECK) or os.path.getmtime(C_CHECK) < max(
             [os.path.getmtime(LIB), os.path.getmtime(C_CHECK_SRC)] + [os.path.getmtime(h) for h in _headers()]):

@@ -117,6 +117,10 @@ int launch_multi_vec(SendList sl, unsigned char* r, Split sp, hipStream_t stream
 
 template <typename T, int OP>
 int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t count, hipStream_t stream) {
+    // One source is the pairwise combine itself: take its tuned dispatch (every alignment class).  The
+    // k-way kernel at k = 1 ran at 78.7 % of peak at 1 GiB against 85 % for the pairwise kernel
+    // (profiles/r2_kway_pmc.json, traffic exactly 3N in both).
+    if (nsend == 1) return reduce_typed<T, OP>(sends[0], recv, count, stream);
     SendList sl{};
     const uintptr_t ar = reinterpret_cast<uintptr_t>(recv);
     bool vec_ok = (ar % sizeof(T)) == 0, elem_ok = vec_ok;
@@ -144,7 +148,6 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
     if (any_straddles(sl, nsend, sp.head * sizeof(T)))
         return multi_straddle_typed<T, OP>(sl, nsend, r, sp, stream);
     switch (nsend) {
-    case 1: return launch_multi_vec<T, OP, 1>(sl, r, sp, stream);
     case 2: return launch_multi_vec<T, OP, 2>(sl, r, sp, stream);
     case 3: return launch_multi_vec<T, OP, 3>(sl, r, sp, stream);
     case 4: return launch_multi_vec<T, OP, 4>(sl, r, sp, stream);
@@ -202,6 +205,8 @@ int launch_chain_vec(SendList sl, const unsigned char* own, unsigned char* d, Sp
 template <typename T, int OP>
 int reduce_chain_typed(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
                        hipStream_t stream) {
+    // dst = op(own, s0) in place is the pairwise combine recv = op(recv, send) with recv = own = dst
+    if (nsend == 1 && own == dst) return reduce_typed<T, OP>(sends[0], dst, count, stream);
     SendList sl{};
     const uintptr_t ad = reinterpret_cast<uintptr_t>(dst), ao = reinterpret_cast<uintptr_t>(own);
     bool elem_ok = ((ad | ao) % sizeof(T)) == 0, vec_ok = elem_ok && ((ad ^ ao) & 15) == 0;

@@ -36,7 +36,6 @@ int launch_straddle(SendList sl, unsigned char* r, Split sp, hipStream_t stream)
 template <typename T, int OP>
 int multi_phased_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, Split sp, hipStream_t stream) {
     switch (nsend) {
-    case 1: return launch_phased<T, OP, 1>(sl, ph, r, sp, stream);
     case 2: return launch_phased<T, OP, 2>(sl, ph, r, sp, stream);
     case 3: return launch_phased<T, OP, 3>(sl, ph, r, sp, stream);
     case 4: return launch_phased<T, OP, 4>(sl, ph, r, sp, stream);
@@ -51,7 +50,6 @@ int multi_phased_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, S
 template <typename T, int OP>
 int multi_straddle_typed(SendList sl, int nsend, unsigned char* r, Split sp, hipStream_t stream) {
     switch (nsend) {
-    case 1: return launch_straddle<T, OP, 1>(sl, r, sp, stream);
     case 2: return launch_straddle<T, OP, 2>(sl, r, sp, stream);
     case 3: return launch_straddle<T, OP, 3>(sl, r, sp, stream);
     case 4: return launch_straddle<T, OP, 4>(sl, r, sp, stream);

@@ -42,7 +42,8 @@ template <typename T, bool PROD> __device__ __forceinline__ T value(uint64_t x) 
 }
 
 template <typename T, bool PROD>
-__global__ void __launch_bounds__(256) synth_kernel(T* dst, size_t count, uint64_t key, bool aligned16) {
+__global__ void __launch_bounds__(256) synth_kernel(T* dst, size_t count, uint64_t key, size_t first,
+                                                    bool aligned16) {
     constexpr size_t E = 16 / sizeof(T);
     const size_t nchunk = (count + E - 1) / E;
     const size_t stride = size_t(gridDim.x) * blockDim.x;
@@ -51,26 +52,26 @@ __global__ void __launch_bounds__(256) synth_kernel(T* dst, size_t count, uint64
         if (aligned16 && i0 + E <= count) {
             union { T e[E]; uint4 v; } u;
 #pragma unroll
-            for (size_t k = 0; k < E; ++k) u.e[k] = value<T, PROD>(splitmix64(key ^ (i0 + k)));
+            for (size_t k = 0; k < E; ++k) u.e[k] = value<T, PROD>(splitmix64(key ^ (first + i0 + k)));
             __builtin_nontemporal_store(u.v.x, reinterpret_cast<unsigned*>(dst + i0) + 0);
             __builtin_nontemporal_store(u.v.y, reinterpret_cast<unsigned*>(dst + i0) + 1);
             __builtin_nontemporal_store(u.v.z, reinterpret_cast<unsigned*>(dst + i0) + 2);
             __builtin_nontemporal_store(u.v.w, reinterpret_cast<unsigned*>(dst + i0) + 3);
         } else {
-            for (size_t i = i0; i < count && i < i0 + E; ++i) dst[i] = value<T, PROD>(splitmix64(key ^ i));
+            for (size_t i = i0; i < count && i < i0 + E; ++i) dst[i] = value<T, PROD>(splitmix64(key ^ (first + i)));
         }
     }
 }
 
 template <typename T>
-int fill(void* dst, size_t count, bool prod, uint64_t key, hipStream_t stream) {
+int fill(void* dst, size_t count, bool prod, uint64_t key, size_t first, hipStream_t stream) {
     constexpr size_t E = 16 / sizeof(T);
     const size_t nchunk = (count + E - 1) / E;
     size_t grid = (nchunk + 255) / 256;
     if (grid > 65536) grid = 65536;
     T* d = static_cast<T*>(dst);
     bool aligned16 = (reinterpret_cast<uintptr_t>(dst) & 15) == 0;
-    void* args[] = {&d, &count, &key, &aligned16};
+    void* args[] = {&d, &count, &key, &first, &aligned16};
     const void* fn = prod ? reinterpret_cast<const void*>(&synth_kernel<T, true>)
                           : reinterpret_cast<const void*>(&synth_kernel<T, false>);
     return hipLaunchKernel(fn, dim3(static_cast<unsigned>(grid)), dim3(256), args, 0, stream) == hipSuccess
@@ -83,8 +84,8 @@ int fill(void* dst, size_t count, bool prod, uint64_t key, hipStream_t stream) {
 
 using namespace dccl_amd;
 
-extern "C" int dccl_synth_fill(void* dst, int dtype, size_t count, int op, uint64_t seed, uint64_t buffer_id,
-                               void* hip_stream) {
+extern "C" int dccl_synth_fill_range(void* dst, int dtype, size_t count, int op, uint64_t seed, uint64_t buffer_id,
+                                     size_t first, void* hip_stream) {
     if (size_of_dtype(dtype) == 0 || op < 0 || op > kAvg) return DCCL_INVALID_ARGUMENT;
     if (count == 0) return DCCL_SUCCESS;
     if (dst == nullptr) return DCCL_INVALID_ARGUMENT;
@@ -92,16 +93,21 @@ extern "C" int dccl_synth_fill(void* dst, int dtype, size_t count, int op, uint6
     const bool prod = op == kProd;
     const auto s = static_cast<hipStream_t>(hip_stream);
     switch (dtype) {
-    case kInt8: return fill<int8_t>(dst, count, prod, key, s);
-    case kUint8: return fill<uint8_t>(dst, count, prod, key, s);
-    case kInt32: return fill<int32_t>(dst, count, prod, key, s);
-    case kUint32: return fill<uint32_t>(dst, count, prod, key, s);
-    case kInt64: return fill<int64_t>(dst, count, prod, key, s);
-    case kUint64: return fill<uint64_t>(dst, count, prod, key, s);
-    case kFloat16: return fill<f16_bits>(dst, count, prod, key, s);
-    case kFloat32: return fill<float>(dst, count, prod, key, s);
-    case kFloat64: return fill<double>(dst, count, prod, key, s);
-    case kBfloat16: return fill<bf16_bits>(dst, count, prod, key, s);
+    case kInt8: return fill<int8_t>(dst, count, prod, key, first, s);
+    case kUint8: return fill<uint8_t>(dst, count, prod, key, first, s);
+    case kInt32: return fill<int32_t>(dst, count, prod, key, first, s);
+    case kUint32: return fill<uint32_t>(dst, count, prod, key, first, s);
+    case kInt64: return fill<int64_t>(dst, count, prod, key, first, s);
+    case kUint64: return fill<uint64_t>(dst, count, prod, key, first, s);
+    case kFloat16: return fill<f16_bits>(dst, count, prod, key, first, s);
+    case kFloat32: return fill<float>(dst, count, prod, key, first, s);
+    case kFloat64: return fill<double>(dst, count, prod, key, first, s);
+    case kBfloat16: return fill<bf16_bits>(dst, count, prod, key, first, s);
     default: return DCCL_INVALID_ARGUMENT;
     }
+}
+
+extern "C" int dccl_synth_fill(void* dst, int dtype, size_t count, int op, uint64_t seed, uint64_t buffer_id,
+                               void* hip_stream) {
+    return dccl_synth_fill_range(dst, dtype, count, op, seed, buffer_id, 0, hip_stream);
 }

@@ -29,6 +29,11 @@ extern "C" {
 int dccl_synth_fill(void* dst, int dtype, size_t count, int op, uint64_t seed, uint64_t buffer_id,
                     void* hip_stream);
 
+/** Elements [first, first + count) of the same operand: a slice of a larger buffer, e.g. to rebuild
+ *  the inputs of a sampled range of a combine for checking. */
+int dccl_synth_fill_range(void* dst, int dtype, size_t count, int op, uint64_t seed, uint64_t buffer_id,
+                          size_t first, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

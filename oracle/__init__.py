@@ -5,10 +5,14 @@ leg import this package, and only as the checker or the timed CPU baseline.
 The product path (``dccl_amd``) never imports it.
 
 * ``restatement()`` — ``oracle/liboracle_host_reduce.so``, the C restatement of
-  ``do_host_reduce<DT>`` (/root/reference/src/core/internal_common.hpp:496-586).
-* ``reference()`` — ``oracle/_ref/libref_host_reduce.so``, the reference's own
-  loop compiled from /root/reference by ``oracle/build_ref.sh`` (None when it
-  was never built, e.g. on a box that never saw the reference).
+  ``do_host_reduce<DT>`` (/root/reference/src/core/internal_common.hpp:496-586),
+  compiled with the reference's Release flags (CMakeLists.txt:25).
+* ``restatement_native()`` — the same source with the reference's Benchmark flags
+  (-Ofast -march=native, CMakeLists.txt:26), a labelled CPU-baseline variant only.
+
+Parity unpinned: the reference's own combine is not built here (it needs its
+CMake-generated config.h and spdlog, which the image lacks), and the reference
+holds no test vectors.
 """
 from __future__ import annotations
 
@@ -20,8 +24,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 _RESTATEMENT = os.path.join(HERE, "liboracle_host_reduce.so")
-_REFERENCE = os.path.join(HERE, "_ref", "libref_host_reduce.so")
-_REFERENCE_NATIVE = os.path.join(HERE, "_ref", "libref_host_reduce_native.so")
+_NATIVE = os.path.join(HERE, "liboracle_host_reduce_native.so")
 
 # ncclDataType_t -> numpy dtype (fp16 / bf16 travel as raw uint16 bit patterns)
 NP_DTYPES = {
@@ -33,9 +36,8 @@ _cache: dict = {}
 
 
 def build() -> None:
-    """Compile the restatement (and the reference oracle when the reference tree exists)."""
-    subprocess.run(["make", "-s", "-C", HERE, "liboracle_host_reduce.so"], check=True)
-    subprocess.run([os.path.join(HERE, "build_ref.sh")], check=True)
+    """Compile the restatement (Release flags, plus the labelled -Ofast -march=native variant)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
 def _bind(path: str, names: list[str]):
@@ -67,19 +69,11 @@ def restatement():
     return _cache["rs"]
 
 
-def reference():
-    """The reference's compiled do_host_reduce, or None if it is not built."""
-    if "ref" not in _cache:
-        _cache["ref"] = _bind(_REFERENCE, ["ref_host_reduce"]) if os.path.exists(_REFERENCE) else None
-    return _cache["ref"]
-
-
-def reference_native():
-    """The reference loop built with its Benchmark flags (-Ofast -march=native), or None."""
-    if "ref_native" not in _cache:
-        _cache["ref_native"] = (_bind(_REFERENCE_NATIVE, ["ref_host_reduce"])
-                                if os.path.exists(_REFERENCE_NATIVE) else None)
-    return _cache["ref_native"]
+def restatement_native():
+    """The restatement built with the reference's Benchmark flags (-Ofast -march=native), or None."""
+    if "native" not in _cache:
+        _cache["native"] = _bind(_NATIVE, ["oracle_host_reduce"]) if os.path.exists(_NATIVE) else None
+    return _cache["native"]
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -96,14 +90,6 @@ def expected_reduce(send: np.ndarray, recv: np.ndarray, dtype: int, op: int, cou
     """Intended semantics, plain pass — in place on ``recv``."""
     n = recv.size if count is None else count
     return restatement().oracle_expected_reduce(_ptr(send), _ptr(recv), n, dtype, op)
-
-
-def ref_reduce(send: np.ndarray, recv: np.ndarray, dtype: int, op: int, count: int | None = None) -> int:
-    lib = reference()
-    if lib is None:
-        raise RuntimeError("reference oracle not built (oracle/_ref missing)")
-    n = recv.size if count is None else count
-    return lib.ref_host_reduce(_ptr(send), _ptr(recv), n, dtype, op)
 
 
 def synth(n: int, dtype: int, op: int, seed: int, buffer_id: int, first: int = 0) -> np.ndarray:

@@ -1,9 +1,13 @@
-"""CPU tests: the oracle restatement is pinned to the reference and to the golden fixtures.
+"""CPU tests of the oracle restatement (oracle/host_reduce.c) against the committed fixtures.
 
-Pinning chain (DESIGN.md "Oracle"):
-  reference do_host_reduce (compiled from /root/reference, oracle/_ref)  ==  oracle/host_reduce.c
-  reference outputs frozen in tests/golden/host_reduce_ref.npz            ==  oracle/host_reduce.c
-  numpy float16 / torch bfloat16 (tests/golden/host_reduce_half.npz)      ==  oracle/host_reduce.c
+Parity is UNPINNED by the reference: the reference has no tests and no golden vectors
+(SURVEY.md §4), and its combine does not compile here without stand-ins for its CMake-generated
+config.h and for spdlog, so it is treated as unbuildable.  What the restatement is checked against:
+  tests/golden/host_reduce_ref.npz   frozen outputs of the round-1 build of the reference loop (a build
+                                     that used such stand-ins; kept as regression data, not as a pin)
+  tests/golden/host_reduce_half.npz  numpy float16 / torch bfloat16 arithmetic (independent of DCCL)
+  tests/golden/c1_ring.json          the dccl_cli all_reduce known answers recorded in SURVEY.md §8(c)
+  the edge semantics listed in SURVEY.md §8(c) / Appendix A, restated from the reference source text
 """
 import json
 import os
@@ -76,32 +80,6 @@ def test_return_codes_match_reference_fixture():
         s = oracle.aligned_empty(max(c["count"], 1), npd)
         r = oracle.aligned_empty(max(c["count"], 1), npd)
         assert oracle.host_reduce(s, r, c["dtype"], c["op"], count=c["count"]) == c["rc"], c
-
-
-@pytest.mark.skipif(oracle.reference() is None, reason="oracle/_ref not built (no /root/reference)")
-@pytest.mark.parametrize("dt", HOST_DTYPES)
-def test_restatement_matches_reference_fuzz(dt):
-    rng = np.random.default_rng(1234 + dt)
-    npd = oracle.NP_DTYPES[dt]
-    for op in range(6):
-        for n in [0, 1, 7, 63, 64, 65, 129, 1000, 4099]:
-            if np.issubdtype(npd, np.integer):
-                info = np.iinfo(npd)
-                s = rng.integers(info.min, info.max, n, dtype=npd, endpoint=True)
-                r = rng.integers(info.min, info.max, n, dtype=npd, endpoint=True)
-            else:
-                s = (rng.standard_normal(n) * 1e3).astype(npd)
-                r = (rng.standard_normal(n) * 1e3).astype(npd)
-            for off in [0, np.dtype(npd).itemsize * 3]:  # 64-B aligned and misaligned recv
-                # pad so the reference's misalignment overrun stays in bounds
-                a = oracle.aligned_empty(n, npd, offset_bytes=off, pad_elems=64)
-                b = oracle.aligned_empty(n, npd, offset_bytes=off, pad_elems=64)
-                sa = oracle.aligned_empty(n, npd, offset_bytes=off, pad_elems=64)
-                a[:] = r
-                b[:] = r
-                sa[:] = s
-                assert oracle.host_reduce(sa, a, dt, op) == oracle.ref_reduce(sa, b, dt, op)
-                assert with_pad(a, 64).tobytes() == with_pad(b, 64).tobytes(), (dt, op, n, off)
 
 
 def test_misalignment_overrun_is_reproduced():

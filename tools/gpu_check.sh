@@ -4,7 +4,7 @@
 # own time limit and the steps are chained, so the first failure ends the run.
 set -eo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-out=gpurun_out/${TAG:-r1}
+out=gpurun_out/${TAG:-r2}
 mkdir -p "$out"
 export TMPDIR=/tmp
 if [[ -z "${SKIP_TESTS:-}" ]]; then
@@ -20,11 +20,16 @@ timeout -k 10 600 python bench.py > "$out/bench.json" 2> "$out/bench.err"
 cat "$out/bench.json"
 if [[ "${PROF:-1}" != 0 ]]; then
   echo "== rocprof kernel trace"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --no-cpu --no-host-staged --no-other-layout --c5-gib 0 > "$out/prof.log" 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --no-cpu --no-host-staged --no-other-layout --no-pmc --c5-gib 0 > "$out/prof.log" 2>&1
   echo "== pmc FETCH_SIZE"
   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc_fetch" -o fetch -- python3 tools/pmc_probe.py > "$out/pmc_fetch.log" 2>&1
   echo "== pmc WRITE_SIZE"
   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/pmc_write" -o write -- python3 tools/pmc_probe.py > "$out/pmc_write.log" 2>&1
+fi
+if [[ -n "${KWAYW:-}" ]]; then
+  echo "== k-way / chain occupancy caps at 1 GiB"
+  timeout -k 10 600 python tools/kway_waves.py --out "$out/kway_waves.json" > "$out/kway_waves.log" 2>&1
+  tail -20 "$out/kway_waves.log"
 fi
 if [[ -n "${CEILING:-}" ]]; then
   echo "== HBM ceiling probes"

@@ -28,6 +28,9 @@ int dccl_tune_reduce_f32_sum_lds(const void* send, void* recv, size_t count, int
 int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count, int waves, int skew, void* stream);
 /* k-way fp32 Sum (the dccl_local_reduce_multi kernel) in shape `variant` 0-7 (see tune_kernels.hip),
  * with `lds_bytes` (<= 64 KiB) of unused dynamic LDS per block to cap resident blocks per CU. */
+/* the in-phase chain kernel (dccl_local_reduce_chain) with `lds_bytes` of unused LDS per one-wave block */
+int dccl_tune_chain_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
+                            size_t lds_bytes, void* stream);
 int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
                             size_t lds_bytes, void* stream);
 /* HBM ceiling probes (see tune_kernels.hip): kind 0 read send, 1 read send+recv, 2 write recv,

@@ -240,7 +240,7 @@ extern "C" int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void
     }
     if (ar & 3) return DCCL_INVALID_ARGUMENT;
     if (count == 0) return DCCL_SUCCESS;
-    const Split sp = split_for_vectors<float>(ar, count);
+    const Split sp = split_for_vectors<float>(ar, count, 128);  // recv line-aligned, as the shipped launch
     auto r = static_cast<unsigned char*>(recv);
     const auto st = static_cast<hipStream_t>(stream);
     switch (nsend) {
@@ -252,6 +252,50 @@ extern "C" int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void
     case 6: return tune_multi_k<6>(variant, sl, r, sp, st, lds_bytes);
     case 7: return tune_multi_k<7>(variant, sl, r, sp, st, lds_bytes);
     default: return tune_multi_k<8>(variant, sl, r, sp, st, lds_bytes);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning only: the chain kernel (dccl_local_reduce_chain's in-phase kernel) with an explicit occupancy
+// cap: `lds_bytes` of unused dynamic LDS per one-wave block (0 = 32 waves per CU).
+// ---------------------------------------------------------------------------------
+namespace {
+template <int K>
+int tune_chain_k(SendList sl, const unsigned char* own, unsigned char* d, Split sp, hipStream_t st, size_t lds) {
+    using C = VecCfg<64, 1, 7, false, 1>;
+    size_t grid = ceil_div(sp.nvec, C::TILE);
+    if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    void* args[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&reduce_chain_vec_kernel<float, kSum, K, C>), grid, args, st, 64, lds);
+}
+}  // namespace
+
+extern "C" int dccl_tune_chain_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
+                                       size_t lds_bytes, void* stream) {
+    if (lds_bytes > (64u << 10)) return DCCL_INVALID_ARGUMENT;
+    if (nsend < 1 || nsend > 8 || sends == nullptr || own == nullptr || dst == nullptr) return DCCL_INVALID_ARGUMENT;
+    SendList sl{};
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
+    if ((ad & 3) || ((reinterpret_cast<uintptr_t>(own) ^ ad) & 15)) return DCCL_INVALID_ARGUMENT;
+    for (int k = 0; k < nsend; ++k) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(sends[k]);
+        if ((a & 3) || ((a ^ ad) & 15)) return DCCL_INVALID_ARGUMENT;
+        sl.p[k] = static_cast<const unsigned char*>(sends[k]);
+    }
+    if (count == 0) return DCCL_SUCCESS;
+    const Split sp = split_for_vectors<float>(ad, count, 128);
+    const auto o = static_cast<const unsigned char*>(own);
+    auto d = static_cast<unsigned char*>(dst);
+    const auto st = static_cast<hipStream_t>(stream);
+    switch (nsend) {
+    case 1: return tune_chain_k<1>(sl, o, d, sp, st, lds_bytes);
+    case 2: return tune_chain_k<2>(sl, o, d, sp, st, lds_bytes);
+    case 3: return tune_chain_k<3>(sl, o, d, sp, st, lds_bytes);
+    case 4: return tune_chain_k<4>(sl, o, d, sp, st, lds_bytes);
+    case 5: return tune_chain_k<5>(sl, o, d, sp, st, lds_bytes);
+    case 6: return tune_chain_k<6>(sl, o, d, sp, st, lds_bytes);
+    case 7: return tune_chain_k<7>(sl, o, d, sp, st, lds_bytes);
+    default: return tune_chain_k<8>(sl, o, d, sp, st, lds_bytes);
     }
 }
 
