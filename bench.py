@@ -259,7 +259,8 @@ def cpu_baseline(budget_s: float, nbytes: int) -> dict | None:
         "all_cores": {"value": round(3 * nbytes / tmt / GIB, 2), "cores": nthr, "passes": reps_mt,
                       "payload_gib_s": round(nbytes / tmt / GIB, 2), "ms_per_pass": round(tmt * 1e3, 2),
                       "slices": "64-B aligned contiguous, one thread each"},
-        "nproc": len(os.sched_getaffinity(0)), "machine_cpus": os.cpu_count(),
+        "affinity_cpus": len(os.sched_getaffinity(0)), "machine_cpus": os.cpu_count(),
+        "cores_note": "all_cores uses min(affinity, OMP_NUM_THREADS): the GPU box grants 16 host threads per GPU",
         "native_flags_variant": native,
         "cpu_model": cpu_model,
     }

@@ -19,7 +19,6 @@
 #include <functional>
 
 #include "algorithms.hpp"
-#include "rccl_transport.hpp"
 
 namespace dccl_amd {
 
@@ -47,13 +46,12 @@ ncclResult_t reduce_scatter_ring(dccl::dcclComm* c, void* buffer, void* scratch,
     const uint32_t r = to_new(c->rank);
     auto data = [&](int64_t i) { return static_cast<unsigned char*>(buffer) + slot_bytes * mod(i, W); };
     const uint32_t to = to_old(mod(int64_t(r) + 1, W)), from = to_old(mod(int64_t(r) - 1, W));
-    if (c->rccl != nullptr) {  // cross-process: RCCL p2p into the scratchpad, then the combine
-        ncclResult_t rc = ensure_scratch(c, slot_bytes, true);
+    if (c->p2p != nullptr) {  // cross-process (RCCL or a plugged-in transport): into the scratchpad, then combine
+        ncclResult_t rc = ensure_scratch(c, slot_bytes, device);
+        void* pad = device ? c->dev_scratch : c->host_scratch;
         for (uint32_t s = 0; s + 1 < W && rc == dccl::ncclSuccess; ++s) {
-            rc = static_cast<ncclResult_t>(rccl_exchange(c->rccl, data(int64_t(r) - s), slot_bytes, to,
-                                                         c->dev_scratch, slot_bytes, from, st));
-            if (rc == dccl::ncclSuccess)
-                rc = combine(c->dev_scratch, data(int64_t(r) - s - 1), dtype, slot_elems, op, true, st);
+            rc = p2p_exchange(c, data(int64_t(r) - s), slot_bytes, to, pad, slot_bytes, from, st);
+            if (rc == dccl::ncclSuccess) rc = combine(pad, data(int64_t(r) - s - 1), dtype, slot_elems, op, device, st);
         }
         return rc;
     }
@@ -85,11 +83,11 @@ ncclResult_t all_gather_ring(dccl::dcclComm* c, void* buffer, size_t slot_elems,
     const uint32_t r = to_new(c->rank);
     auto data = [&](int64_t i) { return static_cast<unsigned char*>(buffer) + slot_bytes * mod(i, W); };
     const uint32_t to = to_old(mod(int64_t(r) + 1, W)), from = to_old(mod(int64_t(r) - 1, W));
-    if (c->rccl != nullptr) {
+    if (c->p2p != nullptr) {
         for (uint32_t s = 0; s + 1 < W; ++s) {
-            const int rc = rccl_exchange(c->rccl, data(int64_t(r) - s), slot_bytes, to, data(int64_t(r) - s - 1),
-                                         slot_bytes, from, st);
-            if (rc != 0) return static_cast<ncclResult_t>(rc);
+            const ncclResult_t rc =
+                p2p_exchange(c, data(int64_t(r) - s), slot_bytes, to, data(int64_t(r) - s - 1), slot_bytes, from, st);
+            if (rc != dccl::ncclSuccess) return rc;
         }
         return dccl::ncclSuccess;
     }
@@ -149,8 +147,7 @@ inline uint32_t reverse_low_bits(uint32_t x, uint32_t nbits) {
 // (skipped if rbuf is null).
 ncclResult_t swap(dccl::dcclComm* c, uint32_t peer, const void* sbuf, size_t sbytes, void* rbuf, size_t rbytes,
                   bool device, hipStream_t st) {
-    if (c->rccl != nullptr)
-        return static_cast<ncclResult_t>(rccl_exchange(c->rccl, sbuf, sbytes, peer, rbuf, rbytes, peer, st));
+    if (c->p2p != nullptr) return p2p_exchange(c, sbuf, sbytes, peer, rbuf, rbytes, peer, st);
     ncclResult_t rc = dccl::ncclSuccess;
     if (sbuf != nullptr) rc = xport_send(c, peer, sbuf, sbytes, device, st);
     if (rc == dccl::ncclSuccess && rbuf != nullptr) rc = xport_recv(c, peer, rbuf, rbytes, device, st);
@@ -165,11 +162,11 @@ ncclResult_t swap(dccl::dcclComm* c, uint32_t peer, const void* sbuf, size_t sby
 ncclResult_t swap_combine(dccl::dcclComm* c, uint32_t peer, const void* sbuf, void* dst, size_t elems, int dtype,
                           int op, void* scratch, bool device, hipStream_t st) {
     const size_t bytes = elems * size_of_dtype(dtype);
-    if (c->rccl != nullptr) {
-        ncclResult_t rc = ensure_scratch(c, bytes, true);
-        if (rc == dccl::ncclSuccess)
-            rc = static_cast<ncclResult_t>(rccl_exchange(c->rccl, sbuf, bytes, peer, c->dev_scratch, bytes, peer, st));
-        return rc == dccl::ncclSuccess ? combine(c->dev_scratch, dst, dtype, elems, op, true, st) : rc;
+    if (c->p2p != nullptr) {
+        ncclResult_t rc = ensure_scratch(c, bytes, device);
+        void* pad = device ? c->dev_scratch : c->host_scratch;
+        if (rc == dccl::ncclSuccess) rc = p2p_exchange(c, sbuf, bytes, peer, pad, bytes, peer, st);
+        return rc == dccl::ncclSuccess ? combine(pad, dst, dtype, elems, op, device, st) : rc;
     }
     ncclResult_t rc = xport_send(c, peer, sbuf, bytes, device, st);
     if (rc == dccl::ncclSuccess) {

@@ -31,6 +31,14 @@
 
 namespace dccl_amd {
 
+// Point-to-point transport of ranks in different processes: one exchange = send `send_bytes` from
+// `sendbuf` to rank `to` and receive `recv_bytes` from rank `from` into `recvbuf` (either side skipped
+// with a null buffer), ordered on `stream` for device buffers, complete on return for host buffers.
+// RCCL's grouped ncclSend/ncclRecv over xGMI is one (rccl_transport.hpp); a host may plug in its own,
+// e.g. Derecho's OOB send/recv (dccl_comm_init_p2p, include/dccl/dccl_comm.h).
+using P2PExchangeFn = int (*)(void* ctx, const void* sendbuf, size_t send_bytes, uint32_t to, void* recvbuf,
+                              size_t recv_bytes, uint32_t from, void* stream);
+
 struct Message {
     const void* ptr = nullptr;
     size_t bytes = 0;
@@ -89,7 +97,13 @@ struct dccl::dcclComm {
     uint32_t rank = 0;
     uint32_t world = 1;
     int device = -1;  // HIP device current at init
-    void* rccl = nullptr;  // non-null: cross-process RCCL transport (rccl_transport.hpp), device buffers only
+    void* rccl = nullptr;  // the RCCL communicator this comm owns (DCCL_TRANSPORT=rccl), destroyed at finalize
+    // Cross-process p2p transport (RCCL, or a plugged-in one): when set, the ring algorithms move chunks
+    // with p2p(p2p_ctx, ...) instead of the in-process channels.
+    dccl_amd::P2PExchangeFn p2p = nullptr;
+    void* p2p_ctx = nullptr;
+    bool p2p_host = false;    // the p2p transport moves host memory (RCCL: no)
+    bool p2p_device = true;   // the p2p transport moves device memory (RCCL: yes)
     void* ipc = nullptr;   // non-null: cross-process IPC peer-read transport (direct.hpp), device buffers only
     // Events of the stream-ordered device transport: a ring of `event_ring` per peer, indexed by the
     // channel's message count, so that no event is recorded again before every wait on its previous
@@ -131,6 +145,12 @@ ncclResult_t xport_wait_send(dccl::dcclComm* c, uint32_t peer, bool device, hipS
 // One HBM/xGMI read of the peer chunk instead of read + write + read.
 ncclResult_t xport_recv_combine(dccl::dcclComm* c, uint32_t peer, void* dst, size_t count, int dtype, int op,
                                 bool device, hipStream_t stream);
+
+// One exchange through c->p2p (see P2PExchangeFn).
+inline ncclResult_t p2p_exchange(dccl::dcclComm* c, const void* sendbuf, size_t send_bytes, uint32_t to, void* recvbuf,
+                                 size_t recv_bytes, uint32_t from, hipStream_t stream) {
+    return static_cast<ncclResult_t>(c->p2p(c->p2p_ctx, sendbuf, send_bytes, to, recvbuf, recv_bytes, from, stream));
+}
 
 // Scratch management (grown on demand, page/line rounded; never shrinks until finalize).
 ncclResult_t ensure_scratch(dccl::dcclComm* c, size_t bytes, bool device);

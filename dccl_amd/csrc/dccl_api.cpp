@@ -31,6 +31,7 @@
 #include "direct.hpp"
 #include "rccl_transport.hpp"
 #include "dccl/dccl.hpp"
+#include "dccl/dccl_comm.h"
 #include "dccl/dccl_reduce.h"
 
 using dccl::dcclComm;
@@ -182,6 +183,11 @@ ncclResult_t join(dcclComm** out, uint32_t world, int64_t want_rank) {
     return dccl::ncclSuccess;
 }
 
+int rccl_p2p(void* ctx, const void* sendbuf, size_t send_bytes, uint32_t to, void* recvbuf, size_t recv_bytes,
+             uint32_t from, void* stream) {
+    return rccl_exchange(ctx, sendbuf, send_bytes, to, recvbuf, recv_bytes, from, static_cast<hipStream_t>(stream));
+}
+
 // Cross-process communicator on the RCCL transport; the current HIP device is this rank's GPU.
 ncclResult_t join_rccl(dcclComm** out, uint32_t world, uint32_t rank, const void* id128) {
     if (world == 0 || rank >= world || id128 == nullptr) return dccl::ncclInvalidArgument;
@@ -191,6 +197,27 @@ ncclResult_t join_rccl(dcclComm** out, uint32_t world, uint32_t rank, const void
     c->world = world;
     const int rc = rccl_comm_init(&c->rccl, world, rank, id128);
     if (rc != 0) return static_cast<ncclResult_t>(rc);
+    c->p2p = &rccl_p2p;  // RCCL moves device memory only
+    c->p2p_ctx = c->rccl;
+    *out = c.release();
+    return dccl::ncclSuccess;
+}
+
+// A plugged-in point-to-point transport (P2PExchangeFn, comm.hpp): `memory` bit 0 = it moves host
+// buffers, bit 1 = device buffers.
+ncclResult_t join_p2p(dcclComm** out, uint32_t world, uint32_t rank, P2PExchangeFn fn, void* ctx, int memory) {
+    if (world == 0 || rank >= world || fn == nullptr || memory < 1 || memory > 3) return dccl::ncclInvalidArgument;
+    auto c = std::make_unique<dcclComm>();
+    if (hipGetDevice(&c->device) != hipSuccess) {
+        (void)hipGetLastError();
+        c->device = -1;
+    }
+    c->rank = rank;
+    c->world = world;
+    c->p2p = fn;
+    c->p2p_ctx = ctx;
+    c->p2p_host = (memory & 1) != 0;
+    c->p2p_device = (memory & 2) != 0;
     *out = c.release();
     return dccl::ncclSuccess;
 }
@@ -250,8 +277,13 @@ uint32_t floor_log2_u32(uint32_t n) {
     return k;
 }
 
-// Cross-process transports move device memory only.
-bool cross_process(const dcclComm* c) { return c->rccl != nullptr || c->ipc != nullptr; }
+// Which buffers the communicator's transport can move: the in-process channels both; the IPC transport
+// and RCCL device memory only; a plugged-in p2p transport what it declared at init.
+bool transport_accepts(const dcclComm* c, bool device) {
+    if (c->ipc != nullptr) return device;
+    if (c->p2p != nullptr) return device ? c->p2p_device : c->p2p_host;
+    return true;
+}
 
 }  // namespace
 
@@ -317,9 +349,9 @@ ncclResult_t ncclCommFinalize(ncclComm_t comm) {
     } else if (comm->ipc != nullptr) {
         const ncclResult_t r = ipc_leave(comm);
         if (rc == ncclSuccess) rc = r;
-    } else {
+    } else if (comm->group != nullptr) {
         comm->group->barrier();  // no peer may still be reading our buffers
-    }
+    }  // a plugged-in p2p transport belongs to the caller
     for (hipEvent_t e : comm->ready_events)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : comm->done_events)
@@ -373,7 +405,7 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
     if (sendbuff == nullptr || recvbuff == nullptr) return ncclInvalidArgument;
     bool dev = false;
     if ((rc = placement(sendbuff, recvbuff, &dev)) != ncclSuccess) return rc;
-    if (cross_process(comm) && !dev) return ncclInvalidUsage;  // the cross-process transports move device memory
+    if (!transport_accepts(comm, dev)) return ncclInvalidUsage;  // e.g. host buffers on RCCL / IPC
     const size_t total = count * size_of_dtype(datatype);
     const uint32_t W = comm->world;
     const Algorithm algo = allreduce_algorithm();  // dccl.cpp:412-413,454
@@ -406,7 +438,7 @@ ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recv
     if (sendbuff == nullptr || recvbuff == nullptr) return ncclInvalidArgument;
     bool dev = false;
     if ((rc = placement(sendbuff, recvbuff, &dev)) != ncclSuccess) return rc;
-    if (cross_process(comm) && !dev) return ncclInvalidUsage;
+    if (!transport_accepts(comm, dev)) return ncclInvalidUsage;
     const uint32_t W = comm->world, r = comm->rank;
     const size_t slot = recvcount * size_of_dtype(datatype), total = slot * W;
     if (W > 1 && dev && direct_selected(comm))
@@ -440,7 +472,7 @@ ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, nccl
     if (sendbuff == nullptr || (iamroot && recvbuff == nullptr)) return ncclInvalidArgument;
     bool dev = false;
     if ((rc = placement(sendbuff, iamroot ? recvbuff : sendbuff, &dev)) != ncclSuccess) return rc;
-    if (cross_process(comm) && !dev) return ncclInvalidUsage;
+    if (!transport_accepts(comm, dev)) return ncclInvalidUsage;
     if (W > 1 && dev && direct_selected(comm))
         return direct_reduce(comm, sendbuff, recvbuff, count, datatype, op, uint32_t(root), stream);
     const size_t total = count * size_of_dtype(datatype), slot = total / W;
@@ -457,8 +489,14 @@ ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, nccl
                              [W](uint32_t o) { return (o + W - 1) % W; }, [W](uint32_t n) { return (n + 1) % W; });
     if (rc != ncclSuccess) return rc;
     auto at = [&](uint32_t i) { return static_cast<unsigned char*>(rbuf) + size_t(i) * slot; };
-    if (comm->rccl != nullptr)
-        return static_cast<ncclResult_t>(rccl_gather_p2p(comm->rccl, rbuf, slot, uint32_t(root), r, W, stream));
+    if (comm->p2p != nullptr) {  // gather to the root (dccl.cpp:803-840), one exchange per peer
+        for (uint32_t p = 0; p < W && rc == ncclSuccess; ++p) {
+            if (p == uint32_t(root) || (!iamroot && p != r)) continue;
+            rc = iamroot ? p2p_exchange(comm, nullptr, 0, 0, at(p), slot, p, stream)
+                         : p2p_exchange(comm, at(r), slot, uint32_t(root), nullptr, 0, 0, stream);
+        }
+        return rc;
+    }
     if (iamroot) {
         for (uint32_t p = 0; p < W; ++p)
             if (p != r && (rc = xport_recv(comm, p, at(p), slot, dev, stream)) != ncclSuccess) return rc;
@@ -478,7 +516,7 @@ ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcoun
     bool dev = false;
     ncclResult_t rc = placement(sendbuff, recvbuff, &dev);
     if (rc != ncclSuccess) return rc;
-    if (cross_process(comm) && !dev) return ncclInvalidUsage;
+    if (!transport_accepts(comm, dev)) return ncclInvalidUsage;
     if (comm->world > 1 && dev && direct_selected(comm))
         return direct_all_gather(comm, sendbuff, recvbuff, sendcount, datatype, stream);
     void* slot = static_cast<unsigned char*>(recvbuff) + sendcount * comm->rank * esz;
@@ -498,15 +536,14 @@ ncclResult_t ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, n
     bool dev = false;
     ncclResult_t rc = placement(r == uint32_t(root) ? sendbuff : recvbuff, recvbuff, &dev);
     if (rc != ncclSuccess) return rc;
-    if (comm->ipc != nullptr && !dev) return ncclInvalidUsage;
+    if (!transport_accepts(comm, dev)) return ncclInvalidUsage;
     if (W > 1 && dev && direct_selected(comm))
         return direct_broadcast(comm, sendbuff, recvbuff, count, datatype, uint32_t(root), stream);
-    if (comm->rccl != nullptr) {
-        if (!dev) return ncclInvalidUsage;
-        rc = static_cast<ncclResult_t>(rccl_bcast_p2p(comm->rccl, sendbuff, recvbuff, bytes, uint32_t(root), r, W,
-                                                      stream));
-        if (rc == ncclSuccess && r == uint32_t(root)) rc = copy_bytes(recvbuff, sendbuff, bytes, true, stream);
-        return rc;
+    if (comm->p2p != nullptr) {  // root -> every rank, one exchange per peer
+        if (r != uint32_t(root)) return p2p_exchange(comm, nullptr, 0, 0, recvbuff, bytes, uint32_t(root), stream);
+        for (uint32_t p = 0; p < W && rc == ncclSuccess; ++p)
+            if (p != r) rc = p2p_exchange(comm, sendbuff, bytes, p, nullptr, 0, 0, stream);
+        return rc == ncclSuccess ? copy_bytes(recvbuff, sendbuff, bytes, dev, stream) : rc;
     }
     if (r == uint32_t(root)) {
         for (uint32_t p = 0; p < W; ++p)
@@ -532,10 +569,8 @@ ncclResult_t ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatyp
         return ncclInvalidArgument;  // dccl.cpp:869-872
     const bool dev = is_device_ptr(sendbuff);
     if (comm->ipc != nullptr) return ncclInvalidUsage;  // the IPC transport has no point-to-point verbs
-    if (comm->rccl != nullptr)
-        return dev ? static_cast<ncclResult_t>(rccl_exchange(comm->rccl, sendbuff, count * esz, uint32_t(peer),
-                                                             nullptr, 0, 0, stream))
-                   : ncclInvalidUsage;
+    if (!transport_accepts(comm, dev)) return ncclInvalidUsage;
+    if (comm->p2p != nullptr) return p2p_exchange(comm, sendbuff, count * esz, uint32_t(peer), nullptr, 0, 0, stream);
     ncclResult_t rc = xport_send(comm, uint32_t(peer), sendbuff, count * esz, dev, stream);
     if (rc != ncclSuccess) return rc;
     return xport_wait_send(comm, uint32_t(peer), dev, stream);
@@ -549,10 +584,8 @@ ncclResult_t ncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int
         return ncclInvalidArgument;  // dccl.cpp:893-896
     const bool dev = is_device_ptr(recvbuff);
     if (comm->ipc != nullptr) return ncclInvalidUsage;
-    if (comm->rccl != nullptr)
-        return dev ? static_cast<ncclResult_t>(rccl_exchange(comm->rccl, nullptr, 0, 0, recvbuff, count * esz,
-                                                             uint32_t(peer), stream))
-                   : ncclInvalidUsage;
+    if (!transport_accepts(comm, dev)) return ncclInvalidUsage;
+    if (comm->p2p != nullptr) return p2p_exchange(comm, nullptr, 0, 0, recvbuff, count * esz, uint32_t(peer), stream);
     return xport_recv(comm, uint32_t(peer), recvbuff, count * esz, dev, stream);
 }
 
@@ -585,6 +618,14 @@ extern "C" int dccl_comm_init_rccl(void** comm, uint32_t world, uint32_t rank, c
     if (comm == nullptr) return DCCL_INVALID_ARGUMENT;
     return guarded([&] {
         return dccl::dcclCommInitRccl(reinterpret_cast<dccl::ncclComm_t*>(comm), world, rank, id128);
+    });
+}
+
+extern "C" int dccl_comm_init_p2p(void** comm, uint32_t world, uint32_t rank, dccl_p2p_exchange_fn exchange,
+                                  void* ctx, int memory) {
+    if (comm == nullptr) return DCCL_INVALID_ARGUMENT;
+    return guarded([&] {
+        return join_p2p(reinterpret_cast<dccl::ncclComm_t*>(comm), world, rank, exchange, ctx, memory);
     });
 }
 

@@ -330,7 +330,7 @@ ncclResult_t ipc_leave(dcclComm* c) {
 // the ring's results bit for bit.  Host buffers, the RCCL transport and groups above 8 ranks keep the ring.
 bool direct_selected(const dcclComm* c) {
     if (c->ipc != nullptr) return true;
-    if (c->rccl != nullptr || c->world > kDirectMaxWorld) return false;
+    if (c->p2p != nullptr || c->world > kDirectMaxWorld) return false;
     const char* a = std::getenv("DCCL_ALLREDUCE_ALGORITHM");
     if (a == nullptr || *a == 0) return true;
     const std::string s(a);
@@ -365,7 +365,7 @@ ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t
 
 bool host_direct_selected(const dcclComm* c, size_t slot_bytes) {
     (void)slot_bytes;  // any size: dccl_local_reduce_chain_host stages in pieces
-    if (c->ipc != nullptr || c->rccl != nullptr || c->group == nullptr || c->world > kDirectMaxWorld) return false;
+    if (c->ipc != nullptr || c->p2p != nullptr || c->group == nullptr || c->world > kDirectMaxWorld) return false;
     const char* a = std::getenv("DCCL_ALLREDUCE_ALGORITHM");
     if (a == nullptr || *a == 0) return true;
     const std::string s(a);

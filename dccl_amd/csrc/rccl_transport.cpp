@@ -86,39 +86,4 @@ int rccl_exchange(void* rcomm, const void* sendbuf, size_t send_bytes, uint32_t 
     return r != 0 ? r : re;
 }
 
-int rccl_bcast_p2p(void* rcomm, const void* buf, void* dst, size_t bytes, uint32_t root, uint32_t rank,
-                   uint32_t world, hipStream_t stream) {
-    const RcclApi& a = api();
-    if (!a.ok) return kSystem;
-    auto c = static_cast<ncclComm_t>(rcomm);
-    int r = rc(a.group_start());
-    if (r != 0) return r;
-    if (rank == root) {
-        for (uint32_t p = 0; p < world && r == 0; ++p)
-            if (p != root) r = rc(a.send(buf, bytes, ncclUint8, int(p), c, stream));
-    } else {
-        r = rc(a.recv(dst, bytes, ncclUint8, int(root), c, stream));
-    }
-    const int re = rc(a.group_end());
-    return r != 0 ? r : re;
-}
-
-int rccl_gather_p2p(void* rcomm, void* slots, size_t bytes, uint32_t root, uint32_t rank, uint32_t world,
-                    hipStream_t stream) {
-    const RcclApi& a = api();
-    if (!a.ok) return kSystem;
-    auto c = static_cast<ncclComm_t>(rcomm);
-    auto base = static_cast<unsigned char*>(slots);
-    int r = rc(a.group_start());
-    if (r != 0) return r;
-    if (rank == root) {
-        for (uint32_t p = 0; p < world && r == 0; ++p)
-            if (p != root) r = rc(a.recv(base + size_t(p) * bytes, bytes, ncclUint8, int(p), c, stream));
-    } else {
-        r = rc(a.send(base + size_t(rank) * bytes, bytes, ncclUint8, int(root), c, stream));
-    }
-    const int re = rc(a.group_end());
-    return r != 0 ? r : re;
-}
-
 }  // namespace dccl_amd

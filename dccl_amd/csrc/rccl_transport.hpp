@@ -27,11 +27,5 @@ int rccl_comm_destroy(void* rcomm);
 // `recvbuf` from `from` (either side may be skipped with a null buffer), enqueued on `stream`.
 int rccl_exchange(void* rcomm, const void* sendbuf, size_t send_bytes, uint32_t to, void* recvbuf,
                   size_t recv_bytes, uint32_t from, hipStream_t stream);
-// Grouped fan-out / fan-in of the same buffer size: root sends `buf` to every other rank, or
-// receives slot p of `buf` (stride `bytes`) from every rank p != root.
-int rccl_bcast_p2p(void* rcomm, const void* buf, void* dst, size_t bytes, uint32_t root, uint32_t rank,
-                   uint32_t world, hipStream_t stream);
-int rccl_gather_p2p(void* rcomm, void* slots, size_t bytes, uint32_t root, uint32_t rank, uint32_t world,
-                    hipStream_t stream);
 
 }  // namespace dccl_amd

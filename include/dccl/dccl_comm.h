@@ -7,6 +7,15 @@
  *                         `world` ranks joined (dcclCommInitRank)
  *   dccl_get_unique_id /  cross-process group over the RCCL (xGMI) transport, one process per
  *   dccl_comm_init_rccl   GPU; the 128-byte id travels out of band (dcclCommInitRccl)
+ *   dccl_comm_init_p2p    a group over a point-to-point transport the caller plugs in: one exchange
+ *                         call sends one buffer to a rank and receives one from a rank (either side may
+ *                         be skipped with NULL), complete on return for host buffers and ordered on
+ *                         `stream` for device buffers; `memory` = 1 host buffers, 2 device buffers,
+ *                         3 both.  This is where the reference's own transport plugs in: Derecho's OOB
+ *                         send / recv / wait (/root/reference/src/core/internal_common.hpp:698-792)
+ *                         wrapped as one exchange.  The ring collectives
+ *                         (reduce_scatter_ring.cpp:73-101, all_gather_ring.cpp:44-64) then run on it,
+ *                         with the gfx950 combine after every receive.
  *   dccl_comm_init_ipc    cross-process group over the IPC peer-read transport (one process per GPU
  *                         on one node; rendezvous through DCCL_BOOTSTRAP_DIR, dcclCommInitIpc)
  *   dccl_bootstrap_unique_id  single-node exchange of the RCCL id through DCCL_BOOTSTRAP_DIR: rank 0
@@ -28,10 +37,15 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* returns 0 on success, else an ncclResult_t value (the collective returns it) */
+typedef int (*dccl_p2p_exchange_fn)(void* ctx, const void* sendbuf, size_t send_bytes, uint32_t to, void* recvbuf,
+                                    size_t recv_bytes, uint32_t from, void* stream);
 int dccl_comm_init_rank(void** comm, uint32_t world, uint32_t rank);
 int dccl_get_unique_id(void* unique_id_128);
 int dccl_comm_init_rccl(void** comm, uint32_t world, uint32_t rank, const void* unique_id_128);
 int dccl_comm_init_ipc(void** comm, uint32_t world, uint32_t rank);
+int dccl_comm_init_p2p(void** comm, uint32_t world, uint32_t rank, dccl_p2p_exchange_fn exchange, void* ctx,
+                       int memory);
 int dccl_bootstrap_unique_id(uint32_t rank, uint32_t world, void* unique_id_128);
 int dccl_comm_finalize(void* comm);
 int dccl_all_reduce(const void* send, void* recv, size_t count, int dtype, int op, void* comm, void* stream);
