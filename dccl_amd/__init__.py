@@ -71,6 +71,11 @@ class DcclError(RuntimeError):
         super().__init__(f"{what} failed: {code} ({result_string(code)})")
 
 
+#: dccl_p2p_exchange_fn of include/dccl/dccl_comm.h
+P2P_EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p)
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
@@ -100,6 +105,8 @@ def _load():
         "dccl_comm_init_rccl": (c_int, [ctypes.POINTER(c_void_p), ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
         "dccl_comm_finalize": (c_int, [c_void_p]),
         "dccl_comm_init_ipc": (c_int, [ctypes.POINTER(c_void_p), ctypes.c_uint32, ctypes.c_uint32]),
+        "dccl_comm_init_p2p": (c_int, [ctypes.POINTER(c_void_p), ctypes.c_uint32, ctypes.c_uint32, P2P_EXCHANGE_FN,
+                                       c_void_p, c_int]),
         "dccl_reduce": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_int, c_void_p, c_void_p]),
         "dccl_broadcast": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
         "dccl_all_reduce": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
@@ -128,7 +135,7 @@ EXPORTED_SYMBOLS = [
     "dccl_comm_init_rank", "dccl_get_unique_id", "dccl_comm_init_rccl", "dccl_comm_finalize", "dccl_all_reduce",
     "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available", "dccl_bootstrap_unique_id",
     "dccl_synth_fill", "dccl_synth_fill_range", "dccl_local_reduce_chain", "dccl_copy_multi",
-    "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_local_reduce_chain_host",
+    "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_local_reduce_chain_host", "dccl_comm_init_p2p",
 ]
 
 
@@ -236,6 +243,23 @@ class Comm:
         h = ctypes.c_void_p()
         check(lib.dccl_comm_init_ipc(ctypes.byref(h), world, rank), "dccl_comm_init_ipc")
         return cls(h.value)
+
+    @classmethod
+    def p2p(cls, world: int, rank: int, exchange, memory: int = 3) -> "Comm":
+        """A group over a caller-supplied point-to-point transport (dccl_comm_init_p2p):
+        ``exchange(send_ptr, send_bytes, to, recv_ptr, recv_bytes, frm, stream) -> int`` moves one buffer
+        each way (a 0 pointer skips that side); ``memory`` 1 = host buffers, 2 = device, 3 = both."""
+        def trampoline(ctx, sbuf, sn, to, rbuf, rn, frm, stream):
+            try:
+                return int(exchange(sbuf or 0, sn, to, rbuf or 0, rn, frm, stream or 0))
+            except Exception:  # an exception must not cross the C frames
+                return int(ncclResult_t.ncclSystemError)
+        fn = P2P_EXCHANGE_FN(trampoline)
+        h = ctypes.c_void_p()
+        check(lib.dccl_comm_init_p2p(ctypes.byref(h), world, rank, fn, None, memory), "dccl_comm_init_p2p")
+        c = cls(h.value)
+        c._keep = fn  # the callback must outlive the communicator
+        return c
 
     def all_reduce(self, send: int, recv: int, count: int, dtype: int, op: int, stream: int = 0) -> int:
         return int(lib.dccl_all_reduce(send, recv, count, dtype, op, self.handle, stream or None))
