@@ -13,7 +13,8 @@
 //   * dtype and op are template parameters (no per-element switch);
 //   * unaligned head / tail elements are folded into block 0 of the same launch;
 //   * element-aligned operands with different 16-B phases take the shifted vector kernel
-//     (aligned loads of both, a cross-lane funnel shift of send); element-misaligned ones a byte kernel.
+//     (aligned loads of both, a cross-lane funnel shift of send), and so does a send at any byte address
+//     against an element-aligned recv; only a recv that is not element-aligned takes a byte kernel.
 // No LDS and no MFMA: each element is touched once (BASELINE.json north_star).
 //
 // Roofline: HBM, 3 * count * sizeof(T) algorithmic bytes (read send, read recv, write recv).
@@ -79,8 +80,14 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
     const auto s = static_cast<const unsigned char*>(send);
     const auto r = static_cast<unsigned char*>(recv);
     const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
-    if ((as | ar) % sizeof(T)) return launch_scalar<T, OP>(s, r, count, false, stream);
     const size_t align = recv_align();
+    if (ar % sizeof(T)) return launch_scalar<T, OP>(s, r, count, false, stream);  // recv's elements straddle vectors
+    if (as % sizeof(T)) {  // an element-aligned recv and a send at any byte address: the shifted kernel
+        const Split sp = split_for_vectors<T>(ar, count, align);
+        const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);
+        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, false>(s, r, count, stream, align)
+                         : launch_shift<T, OP, ShiftPolicy, false, 0, false>(s, r, count, stream, align);
+    }
     const Split sp = split_for_vectors<T>(ar, count, align);
     if ((as ^ ar) & 15) {
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);  // the shifted kernel's send vectors

@@ -59,13 +59,13 @@ struct VecCfg {
 };
 
 // Block 0's scalar elements outside the vector body: head [0, head) (< the recv alignment) and tail
-// (< one vector).
-template <typename T, int OP>
+// (< one vector).  SEND_ALIGNED false: send is not element-aligned (byte loads of its elements).
+template <typename T, int OP, bool SEND_ALIGNED = true>
 __device__ __forceinline__ void edge_scalars(const unsigned char* send, unsigned char* recv, size_t head,
                                              size_t nvec, size_t tail) {
     for (size_t j = threadIdx.x; j < head + tail; j += blockDim.x) {
         const size_t i = j < head ? j : head + nvec * Pack<T>::N + (j - head);
-        const T a = ld_elem<T, true>(recv, i), b = ld_elem<T, true>(send, i);
+        const T a = ld_elem<T, true>(recv, i), b = ld_elem<T, SEND_ALIGNED>(send, i);
         st_elem<T, true>(recv, i, Combine<T, OP>::apply(a, b));
     }
 }
@@ -133,6 +133,9 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_vec_kernel(const unsigned cha
 // funnel-shifts the 32 bytes by p (v_alignbyte_b32), so every access stays a 16-B vector.
 // A[nvec] is loaded although only its first p bytes belong to send: an aligned 16-B load never
 // leaves the page of its first byte, which is send's.
+// v_alignbyte shifts by any byte count, so p need not be a multiple of sizeof(T): a send that is not
+// even element-aligned, against an element-aligned recv, takes this kernel too (SEND_ALIGNED false: its
+// head / tail elements are read bytewise).
 // ---------------------------------------------------------------------------------
 constexpr int kNtExtra = 8;  // policy bit: non-temporal load of lane 63's extra vector
 
@@ -158,7 +161,7 @@ __device__ __forceinline__ u32x4 from_next_lane(u32x4 x) {
     return o;
 }
 
-template <typename T, int OP, int POLICY, bool XCD, int TAG = 0>
+template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true>
 __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* __restrict__ send,
                                                           unsigned char* __restrict__ recv, size_t head,
                                                           size_t nvec, size_t tail, unsigned p) {
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
             else vr[v] = o;
         }
     }
-    if (blockIdx.x == 0) edge_scalars<T, OP>(send, recv, head, nvec, tail);
+    if (blockIdx.x == 0) edge_scalars<T, OP, SEND_ALIGNED>(send, recv, head, nvec, tail);
 }
 
 // ---------------------------------------------------------------------------------
@@ -492,16 +495,17 @@ int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t s
                   lds_bytes);
 }
 
-// Element-aligned operands with different 16-B phases: the shifted vector kernel.
-template <typename T, int OP, int POLICY, bool XCD, int TAG = 0>
+// Element-aligned operands with different 16-B phases (or an element-aligned recv and a send at any byte
+// address, SEND_ALIGNED false): the shifted vector kernel.
+template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true>
 int launch_shift(const unsigned char* s, unsigned char* r, size_t count, hipStream_t stream, size_t align = 16) {
     Split sp = split_for_vectors<T>(reinterpret_cast<uintptr_t>(r), count, align);
     unsigned p = unsigned((reinterpret_cast<uintptr_t>(s) + sp.head * sizeof(T)) & 15);
     size_t grid = ceil_div(sp.nvec, size_t(64));
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&s, &r, &sp.head, &sp.nvec, &sp.tail, &p};
-    return launch(reinterpret_cast<const void*>(&reduce_shift_kernel<T, OP, POLICY, XCD, TAG>), grid, args, stream,
-                  64);
+    return launch(reinterpret_cast<const void*>(&reduce_shift_kernel<T, OP, POLICY, XCD, TAG, SEND_ALIGNED>), grid,
+                  args, stream, 64);
 }
 
 // 16-B phase of an operand whose body starts `off` bytes in (see PhaseList).

@@ -190,6 +190,31 @@ def test_element_misaligned_every_offset(dccl, dt):
                 assert not tr[:roff].any() and not tr[roff + nb:].any(), (dt, n, soff, roff)
 
 
+@pytest.mark.parametrize("dt", [2, 3, 4, 5, 6, 7, 8, 9])
+def test_send_byte_misaligned_every_offset(dccl, dt):
+    """A send at any byte address against an element-aligned recv (the shifted kernel with a byte phase, send's
+    head / tail elements read bytewise): every send byte offset that is not a multiple of sizeof(T), recv in
+    and off its 16-B and 128-B grids, sizes around a 64-vector tile; nothing outside recv's bytes is written."""
+    rng = np.random.default_rng(900 + dt)
+    esz = np.dtype(oracle.NP_DTYPES[dt]).itemsize
+    per_tile = 64 * (16 // esz)
+    sizes = [1, 2, 16 // esz + 1, per_tile - 1, per_tile + 1, 2 * per_tile + 16 // esz + 3, 40001]
+    for soff in range(1, 32):
+        if soff % esz == 0:
+            continue
+        for roff in (0, esz, 48, 128 - esz):
+            for n in sizes:
+                s, r = rand_inputs(rng, dt, n)
+                op = int(rng.integers(0, 4))
+                ts, ps = dev_bytes(s, soff)
+                tr, pr = dev_bytes(r, roff)
+                assert dccl.local_reduce(ps, pr, dt, n, op, 0) == 0
+                torch.cuda.synchronize()
+                assert fp_equal(host_of(tr, roff, r), expected(s, r, dt, op), dt), (dt, op, n, soff, roff)
+                nb = n * esz
+                assert not tr[:roff].any() and not tr[roff + nb:].any(), (dt, n, soff, roff)
+
+
 @pytest.mark.parametrize("dt", [6, 9])
 def test_all_16bit_patterns(dccl, dt):
     """Every fp16 / bf16 bit pattern as recv against a fixed set of partners."""

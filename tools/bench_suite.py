@@ -261,7 +261,8 @@ def c1(results):
 
 def misaligned(results, mib=1024):
     """Operands off their 128-B lines (vector kernel), off the 16-B phase of each other (shifted vector
-    kernel) or off element alignment (byte-gather kernel), fp32 Sum, 1 GiB."""
+    kernel), a send off element alignment (shifted kernel, byte phase) or a recv off element alignment
+    (byte-gather kernel), fp32 Sum, 1 GiB."""
     st = torch.cuda.current_stream().cuda_stream
     nbytes = mib << 20
     n = nbytes // 4 - 4
@@ -273,7 +274,10 @@ def misaligned(results, mib=1024):
                              (0, 16, "same 16-B phase, recv off its lines (vector, recv realigned by the head)"),
                              (4, 0, "4-B phase mismatch (shifted vector kernel)"),
                              (8, 4, "8/4-B offsets (shifted vector kernel, recv realigned)"),
-                             (1, 1, "byte offsets, same phase (element-misaligned byte path)")):
+                             (1, 0, "send at a byte offset, recv aligned (shifted vector kernel, byte phase)"),
+                             (3, 0, "send at a byte offset, recv aligned (shifted vector kernel, byte phase)"),
+                             (1, 1, "byte offsets, recv element-misaligned (byte-gather kernel)"),
+                             (0, 2, "recv element-misaligned (byte-gather kernel)")):
         fn = lambda soff=soff, roff=roff: dccl_amd.local_reduce(s.data_ptr() + soff, r.data_ptr() + roff, 7, n, 0, st)
         med, _ = time_launches([fn], rounds=5)
         gbs = 3 * n * 4 / (med * 1e-3) / 1e9
