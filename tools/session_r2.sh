@@ -8,7 +8,7 @@ out=gpurun_out/r2/${TAG:-s1}; mkdir -p "$out"; export TMPDIR=/tmp
 stop_if_fatal() { local rc=$1; if [[ $rc -eq 124 || $rc -gt 128 ]]; then echo "fatal rc=$rc: stopping"; exit "$rc"; fi; }
 if [[ -z "${SKIP_TESTS:-}" ]]; then
   echo "== pytest"
-  timeout -k 10 1500 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS:-} > "$out/pytest_gpu.log" 2>&1; rc=$?; echo "pytest rc=$rc"
+  timeout -k 10 1500 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread -p no:cacheprovider ${PYTEST_K:+-k "$PYTEST_K"} > "$out/pytest_gpu.log" 2>&1; rc=$?; echo "pytest rc=$rc"
   tail -3 "$out/pytest_gpu.log"; grep -E "^(FAILED|ERROR)" "$out/pytest_gpu.log" | head -20
   stop_if_fatal $rc
   echo "== smoke"
