@@ -14,7 +14,8 @@
 //   * unaligned head / tail elements are folded into block 0 of the same launch;
 //   * element-aligned operands with different 16-B phases take the shifted vector kernel
 //     (aligned loads of both, a cross-lane funnel shift of send), and so does a send at any byte address
-//     against an element-aligned recv; only a recv that is not element-aligned takes a byte kernel.
+//     against an element-aligned recv; a recv that is not element-aligned takes a boundary pass and a
+//     vector pass (misaligned.hip).
 // No LDS and no MFMA: each element is touched once (BASELINE.json north_star).
 //
 // Roofline: HBM, 3 * count * sizeof(T) algorithmic bytes (read send, read recv, write recv).
@@ -81,7 +82,13 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
     const auto r = static_cast<unsigned char*>(recv);
     const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
     const size_t align = recv_align();
-    if (ar % sizeof(T)) return launch_scalar<T, OP>(s, r, count, false, stream);  // recv's elements straddle vectors
+    if (ar % sizeof(T)) {  // recv's elements straddle its vectors: boundary pass + vector pass (misaligned.hip)
+        if constexpr (sizeof(T) > 1) {
+            const int rc = reduce_misaligned_typed<T, OP>(s, r, count, stream);
+            if (rc != kNoScratch) return rc;
+        }
+        return launch_scalar<T, OP>(s, r, count, false, stream);
+    }
     if (as % sizeof(T)) {  // an element-aligned recv and a send at any byte address: the shifted kernel
         const Split sp = split_for_vectors<T>(ar, count, align);
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);

@@ -524,6 +524,11 @@ int multi_straddle_typed(SendList sl, int nsend, unsigned char* r, Split sp, hip
 template <typename T, int OP>
 int chain_straddle_typed(SendList sl, int nsend, const unsigned char* own, unsigned char* d, Split sp,
                          hipStream_t stream);
+// A recv that is not element-aligned (misaligned.hip): boundary pass + vector pass, every recv vector
+// written whole by one wave.  sizeof(T) > 1.  kNoScratch: the stream-ordered scratch could not be had.
+constexpr int kNoScratch = -1;
+template <typename T, int OP>
+int reduce_misaligned_typed(const unsigned char* s, unsigned char* r, size_t count, hipStream_t stream);
 template <typename T, int OP>
 int chain_phased_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp,
                        hipStream_t stream);

@@ -127,3 +127,24 @@ def test_kway_and_chain_line_straddling_sources(gpu, k):
             assert fp_equal(host_of(to, roff, r), want_c, dt), ("chain", k, dt, n, op, soffs, roff)
             assert fp_equal(host_of(td, doff, r), want_c, dt), ("chain dst", k, dt, n, op, soffs, doff)
             assert host_of(to2, doff, r).tobytes() == r.tobytes()  # own untouched
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("dt,roff,soff", [(7, 1, 0), (7, 2, 7), (8, 3, 0), (8, 4, 12), (9, 1, 0), (2, 3, 2)])
+def test_recv_misaligned_large_against_oracle(gpu, dt, roff, soff):
+    """A recv that is not element-aligned (boundary pass + vector pass, misaligned.hip) at 64 MiB, across
+    many tiles and grid strides: the whole result against the oracle, nothing outside recv written."""
+    import dccl_amd
+    esz = int(oracle.NP_DTYPES[dt]().itemsize)
+    n = (64 << 20) // esz + 5
+    op = 0 if dt != 9 else 2
+    s = oracle.synth(n, dt, op, SEED, 40)
+    r = oracle.synth(n, dt, op, SEED, 41)
+    ts, ps = dev_bytes(s, soff)
+    tr, pr = dev_bytes(r, roff)
+    assert dccl_amd.local_reduce(ps, pr, dt, n, op, 0) == 0
+    torch.cuda.synchronize()
+    got = host_of(tr, roff, r)
+    assert got.tobytes() == oracle.combine(s, r, dt, op).tobytes()
+    nb = n * esz
+    assert not tr[:roff].any() and not tr[roff + nb:].any()
