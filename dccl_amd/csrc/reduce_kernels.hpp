@@ -150,15 +150,62 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, unsigned b) {
     return o;
 }
 
-// lane l receives lane (l+1) % 64's vector
-__device__ __forceinline__ u32x4 from_next_lane(u32x4 x) {
-    const int a = int((threadIdx.x + 1) & 63) << 2;
+// Cross-lane moves by one lane with DPP wave shifts (a VALU modifier, no LDS round trip), lane mapping
+// verified on gfx950 by tools/dpp_probe.hip: wave_rol:1 (0x134) gives lane l lane (l+1) % 64's value,
+// wave_shl:1 (0x130) the same except that lane 63 keeps `old`; wave_ror:1 (0x13C) gives lane l lane
+// (l+63) % 64's value, wave_shr:1 (0x138) the same except that lane 0 keeps `old`.
+// DCCL_LANE_SHIFT_BPERMUTE selects the round-1 ds_bpermute form (tuning A/B only).
+template <int CTRL>
+__device__ __forceinline__ u32x4 dpp16(u32x4 x, u32x4 old) {
+    u32x4 o;
+    o.x = unsigned(__builtin_amdgcn_update_dpp(int(old.x), int(x.x), CTRL, 0xF, 0xF, false));
+    o.y = unsigned(__builtin_amdgcn_update_dpp(int(old.y), int(x.y), CTRL, 0xF, 0xF, false));
+    o.z = unsigned(__builtin_amdgcn_update_dpp(int(old.z), int(x.z), CTRL, 0xF, 0xF, false));
+    o.w = unsigned(__builtin_amdgcn_update_dpp(int(old.w), int(x.w), CTRL, 0xF, 0xF, false));
+    return o;
+}
+__device__ __forceinline__ u32x4 bpermute16(u32x4 x, int src_lane) {
+    const int a = src_lane << 2;
     u32x4 o;
     o.x = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.x)));
     o.y = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.y)));
     o.z = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.z)));
     o.w = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.w)));
     return o;
+}
+// lane l receives lane (l+1) % 64's vector
+__device__ __forceinline__ u32x4 from_next_lane(u32x4 x) {
+#ifdef DCCL_LANE_SHIFT_BPERMUTE
+    return bpermute16(x, int((threadIdx.x + 1) & 63));
+#else
+    return dpp16<0x134>(x, x);
+#endif
+}
+// lane l < 63 receives lane l+1's x, lane 63 keeps its own `last`
+__device__ __forceinline__ u32x4 from_next_lane_or(u32x4 x, u32x4 last) {
+#ifdef DCCL_LANE_SHIFT_BPERMUTE
+    const u32x4 o = bpermute16(x, int((threadIdx.x + 1) & 63));
+    return (threadIdx.x & 63) == 63 ? last : o;
+#else
+    return dpp16<0x130>(x, last);
+#endif
+}
+// lane l receives lane (l+63) % 64's vector
+__device__ __forceinline__ u32x4 from_prev_lane(u32x4 x) {
+#ifdef DCCL_LANE_SHIFT_BPERMUTE
+    return bpermute16(x, int((threadIdx.x + 63) & 63));
+#else
+    return dpp16<0x13C>(x, x);
+#endif
+}
+// lane l > 0 receives lane l-1's x, lane 0 keeps its own `first`
+__device__ __forceinline__ u32x4 from_prev_lane_or(u32x4 x, u32x4 first) {
+#ifdef DCCL_LANE_SHIFT_BPERMUTE
+    const u32x4 o = bpermute16(x, int((threadIdx.x + 63) & 63));
+    return (threadIdx.x & 63) == 0 ? first : o;
+#else
+    return dpp16<0x138>(x, first);
+#endif
 }
 
 template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true>
@@ -178,8 +225,7 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
         if (v <= nvec) lo = ld16<(POLICY & kNtSend) != 0>(va + v);
         if (v < nvec) r = ld16<(POLICY & kNtRecv) != 0>(vr + v);
         if (last_lane && v < nvec) ex = ld16<(POLICY & kNtExtra) != 0>(va + v + 1);
-        u32x4 hi = from_next_lane(lo);
-        if (last_lane) hi = ex;
+        const u32x4 hi = from_next_lane_or(lo, ex);
         if (v < nvec) {
             u32x4 s;
             switch (q) {  // uniform
@@ -364,8 +410,7 @@ __device__ __forceinline__ u32x4 ld_phased(const unsigned char* body, unsigned p
     u32x4 ex = {0u, 0u, 0u, 0u};
     if (v <= nvec) lo = __builtin_nontemporal_load(va + v);  // A[nvec] holds the last p body bytes
     if (last_lane && v < nvec) ex = va[v + 1];
-    u32x4 hi = from_next_lane(lo);
-    if (last_lane) hi = ex;
+    const u32x4 hi = from_next_lane_or(lo, ex);
     const unsigned b = p & 3;
     switch (p >> 2) {  // uniform
     case 0: return funnel16<0>(lo, hi, b);
@@ -445,10 +490,11 @@ inline constexpr size_t kLdsPerCu = 160u << 10;
 constexpr size_t multi_lds(int k) {
     return kMultiWaves[k] >= 32 ? 0 : (kLdsPerCu / kMultiWaves[k] + 255) / 256 * 256;
 }
-// The in-phase chain kernel's own caps (K sources + own, one store): swept on MI355X at 256 MiB per
-// operand, fp32 Sum (profiles/r1_s5_chain_waves_sweep.json; k = 1, 2, 4, 7 measured, 3, 5, 6
-// interpolated): k = 2 79.5 -> 82.2 % with 24 waves instead of 18, k = 4 81.8 -> 82.9 % with 16
-// instead of 13, k = 1 and 7 unchanged.
+// The chain kernel's own caps (K sources + own, one store), used by its in-phase launch and by its
+// line-straddling launch alike: first swept at 256 MiB per operand (profiles/r1_s5_chain_waves_sweep.json,
+// k = 2 79.5 -> 82.2 % with 24 waves instead of 18); re-swept for every k at 1 GiB in round 2, both
+// kernels and both operand layouts (tools/kway_waves.py, profiles/r2_kway_waves.json): no cap beat the
+// shipped ones by more than 0.7 points at any k, and every k runs at >= 80.1 % of (k+2)N.
 inline constexpr int kChainWaves[9] = {32, 32, 24, 20, 16, 13, 11, 10, 9};
 constexpr size_t chain_lds(int k) {
     return kChainWaves[k] >= 32 ? 0 : (kLdsPerCu / kChainWaves[k] + 255) / 256 * 256;

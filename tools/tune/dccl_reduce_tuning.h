@@ -31,6 +31,8 @@ int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count, int waves
 /* the in-phase chain kernel (dccl_local_reduce_chain) with `lds_bytes` of unused LDS per one-wave block */
 int dccl_tune_chain_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
                             size_t lds_bytes, void* stream);
+/* the misaligned-recv combine (dccl_amd/csrc/misaligned.hpp) in shape `variant` 0-6 (see tune_kernels.hip) */
+int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t count, int variant, void* stream);
 int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
                             size_t lds_bytes, void* stream);
 /* HBM ceiling probes (see tune_kernels.hip): kind 0 read send, 1 read send+recv, 2 write recv,

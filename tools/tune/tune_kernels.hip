@@ -8,6 +8,7 @@
 
 #include "dccl/dccl_reduce.h"
 #include "dccl_reduce_tuning.h"
+#include "misaligned.hpp"
 #include "reduce_kernels.hpp"
 
 using namespace dccl_amd;
@@ -486,3 +487,30 @@ extern "C" int dccl_tune_pipelined_f32_sum(const void* send, void* recv, size_t 
                ? DCCL_SUCCESS
                : DCCL_UNHANDLED_DEVICE_ERROR;
 }
+
+// ---------------------------------------------------------------------------------
+// Tuning only: the misaligned-recv combine (misaligned.hpp) in shape `variant`:
+// 0/1 = 1 vector per lane, send cached / non-temporal; 2/3 = 2 vectors; 4/5 = 4 vectors; 6 = the byte kernel.
+// recv must not be element-aligned (fp32: an address that is not a multiple of 4).
+// ---------------------------------------------------------------------------------
+extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t count, int variant, void* stream) {
+    const auto s = static_cast<const unsigned char*>(send);
+    const auto r = static_cast<unsigned char*>(recv);
+    const auto st = static_cast<hipStream_t>(stream);
+    if ((reinterpret_cast<uintptr_t>(recv) & 3) == 0 || count == 0) return DCCL_INVALID_ARGUMENT;
+    switch (variant) {
+    case 0: return mis::launch_misaligned<float, kSum, 1, false>(s, r, count, st);
+    case 1: return mis::launch_misaligned<float, kSum, 1, true>(s, r, count, st);
+    case 2: return mis::launch_misaligned<float, kSum, 2, false>(s, r, count, st);
+    case 3: return mis::launch_misaligned<float, kSum, 2, true>(s, r, count, st);
+    case 4: return mis::launch_misaligned<float, kSum, 4, false>(s, r, count, st);
+    case 5: return mis::launch_misaligned<float, kSum, 4, true>(s, r, count, st);
+    case 6: {
+        void* args[] = {const_cast<unsigned char**>(&s), const_cast<unsigned char**>(&r), &count};
+        return launch(reinterpret_cast<const void*>(&reduce_scalar_kernel<float, kSum, false>),
+                      ceil_div(count, size_t(kBlock) * 4), args, st);
+    }
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+
