@@ -14,8 +14,8 @@
 //   * unaligned head / tail elements are folded into block 0 of the same launch;
 //   * element-aligned operands with different 16-B phases take the shifted vector kernel
 //     (aligned loads of both, a cross-lane funnel shift of send), and so does a send at any byte address
-//     against an element-aligned recv; a recv that is not element-aligned takes a boundary pass and a
-//     vector pass (misaligned.hip).
+//     against an element-aligned recv; a recv that is not element-aligned takes one 16-B access per lane
+//     at the displaced addresses themselves (reduce_unaligned_kernel).
 // No LDS and no MFMA: each element is touched once (BASELINE.json north_star).
 //
 // Roofline: HBM, 3 * count * sizeof(T) algorithmic bytes (read send, read recv, write recv).
@@ -82,12 +82,14 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
     const auto r = static_cast<unsigned char*>(recv);
     const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
     const size_t align = recv_align();
-    if (ar % sizeof(T)) {  // recv's elements straddle its vectors: boundary pass + vector pass (misaligned.hip)
-        if constexpr (sizeof(T) > 1) {
-            const int rc = reduce_misaligned_typed<T, OP>(s, r, count, stream);
-            if (rc != kNoScratch) return rc;
-        }
-        return launch_scalar<T, OP>(s, r, count, false, stream);
+    if (ar % sizeof(T)) {  // recv's elements straddle its 16-B vectors: one 16-B access per lane at any address
+        const size_t nvec = count / Pack<T>::N;
+        size_t grid = ceil_div(ceil_div(nvec, size_t(64)), size_t(8)) * 8;  // a multiple of 8 (kMaxGrid is one)
+        if (grid == 0) grid = 8;
+        unsigned p = unsigned(as & 15);
+        void* args[] = {const_cast<unsigned char**>(&s), &p, const_cast<unsigned char**>(&r),
+                        const_cast<size_t*>(&nvec), &count};
+        return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<T, OP>), grid, args, stream, 64);
     }
     if (as % sizeof(T)) {  // an element-aligned recv and a send at any byte address: the shifted kernel
         const Split sp = split_for_vectors<T>(ar, count, align);

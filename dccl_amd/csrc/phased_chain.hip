@@ -17,7 +17,7 @@ int launch_phased(SendList sl, PhaseList ph, const unsigned char* own, unsigned 
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &ph, &own, &d, &sp.head, &sp.nvec, &sp.tail};
     // No occupancy cap, unlike the k-way kernel (reduce_kernels.hpp, "Phased k-way and chain kernels").
-    return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K>), grid, args, stream, 64);
+    return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K, (K <= kPhasedXcdMaxK)>), grid, args, stream, 64);
 }
 
 using StraddleKwayCfg = VecCfg<64, 1, kNtRecv | kNtStore, false>;

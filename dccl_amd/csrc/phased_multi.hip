@@ -17,7 +17,7 @@ int launch_phased(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStre
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &ph, &r, &sp.head, &sp.nvec, &sp.tail};
     // No occupancy cap, unlike the k-way kernel (reduce_kernels.hpp, "Phased k-way and chain kernels").
-    return launch(reinterpret_cast<const void*>(&reduce_multi_phased_kernel<T, OP, K>), grid, args, stream, 64);
+    return launch(reinterpret_cast<const void*>(&reduce_multi_phased_kernel<T, OP, K, (K <= kPhasedXcdMaxK)>), grid, args, stream, 64);
 }
 
 using StraddleKwayCfg = VecCfg<64, 1, kNtRecv | kNtStore, false>;

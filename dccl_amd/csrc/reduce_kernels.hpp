@@ -268,6 +268,23 @@ __global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(const unsigned ch
 }
 
 // ---------------------------------------------------------------------------------
+// A recv that is not element-aligned (e.g. fp32 at an odd byte address; the reference's host loop takes
+// it with a warning, internal_common.hpp:504-512, its CUDA kernel not at all).  gfx950 executes
+// global_load_dwordx4 / global_store_dwordx4 at any byte address (tools/unaligned_probe.hip checks every
+// element), so lane i simply moves the 16 bytes of elements [V i, V i + V) of each operand at their own
+// addresses (V = 16 / sizeof(T)): adjacent lanes' windows are disjoint and hold whole elements, so no byte
+// is written twice and nothing needs a neighbour's original bytes.  send is read as the shifted kernel
+// reads it (aligned loads, lane exchange, funnel shift by its own phase): unaligned send loads as well
+// cost a further 7-10 points.  A 1 KiB tile spans 9 lines of recv, one shared with the next tile;
+// consecutive tiles go to one XCD (blocks are dealt round-robin over the 8 XCDs), so the shared lines meet
+// in one L2.  1 GiB fp32 Sum on MI355X, recv + 1 B: 76.4-76.7 % of HBM peak, against 74.6-74.8 % with
+// consecutive tiles on different XCDs and 72-73 % for a byte-gather kernel; a two-pass form writing every
+// recv vector whole from one wave reached 74-75.5 % (tools/tune/, profiles/r2_misaligned_ab.json).  The
+// tail (< V elements) is block 0's, element by element.  Kernel: after ld_phased below.
+// ---------------------------------------------------------------------------------
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+
+// ---------------------------------------------------------------------------------
 // k-way vector kernel: recv = op(...op(op(recv, s0), s1)..., s{K-1}), one pass.
 // ---------------------------------------------------------------------------------
 struct SendList { const unsigned char* p[8]; };
@@ -397,6 +414,13 @@ __global__ __launch_bounds__(kBlock) void reduce_chain_scalar_kernel(SendList se
 // ---------------------------------------------------------------------------------
 struct PhaseList { unsigned p[9]; };
 
+// XCD: consecutive tiles on one XCD (xcd_remap), so the vector lane 63 reads past its tile and the
+// next tile's first line meet in one L2.  It pays while few operands share the L2.  1 GiB fp32 Sum,
+// sources 4 B off phase, on two boxes (tools/phased_probe.py, profiles/r2_phased_xcd_*.json), points of
+// HBM peak gained: k-way k = 2 +2.1..+4.0, k = 3 +2.1..+2.5, k = 4 +0.6..+1.7, k = 5 -0.2..+0.8,
+// k = 7 -2.2..-5.1; the chain kernel (in place) within 0.5 points of the same at every k.
+inline constexpr int kPhasedXcdMaxK = 4;
+
 // The 16 body bytes of vector v (zero for v >= nvec) of an operand whose body starts at `body`,
 // phase p.  All 64 lanes must call it (p is uniform).
 __device__ __forceinline__ u32x4 ld_phased(const unsigned char* body, unsigned p, size_t v, size_t nvec) {
@@ -420,14 +444,34 @@ __device__ __forceinline__ u32x4 ld_phased(const unsigned char* body, unsigned p
     }
 }
 
-template <typename T, int OP, int K>
+// grid: a multiple of 8.  Block b takes tile (b % 8) * (grid / 8) + b / 8, then strides by grid.  send's
+// 16 bytes per lane come from aligned loads and the lane exchange (ld_phased, phase p = send & 15).
+template <typename T, int OP>
+__global__ __launch_bounds__(64) void reduce_unaligned_kernel(const unsigned char* __restrict__ send, unsigned p,
+                                                              unsigned char* __restrict__ recv, size_t nvec,
+                                                              size_t count) {
+    const size_t g = gridDim.x;
+    for (size_t t = size_t(blockIdx.x % 8) * (g / 8) + blockIdx.x / 8; t * 64 < nvec; t += g) {
+        const size_t i = t * 64 + threadIdx.x;
+        const u32x4 b = ld_phased(send, p, i, nvec);
+        if (i < nvec) {
+            u32x4_u* pr = reinterpret_cast<u32x4_u*>(recv + 16 * i);
+            __builtin_nontemporal_store(combine16<T, OP>(__builtin_nontemporal_load(pr), b), pr);
+        }
+    }
+    if (blockIdx.x == 0)
+        for (size_t j = nvec * Pack<T>::N + threadIdx.x; j < count; j += 64)
+            st_elem<T, false>(recv, j, Combine<T, OP>::apply(ld_elem<T, false>(recv, j), ld_elem<T, false>(send, j)));
+}
+
+template <typename T, int OP, int K, bool XCD>
 __global__ __launch_bounds__(64) void reduce_multi_phased_kernel(SendList sends, PhaseList ph,
                                                                  unsigned char* __restrict__ recv, size_t head,
                                                                  size_t nvec, size_t tail) {
     const size_t off = head * sizeof(T);
     u32x4* vr = reinterpret_cast<u32x4*>(recv + off);
     const size_t ntiles = (nvec + 63) / 64;
-    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (size_t t = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; t < ntiles; t += gridDim.x) {
         const size_t v = t * 64 + threadIdx.x;
         u32x4 s[K];
 #pragma unroll
@@ -451,14 +495,14 @@ __global__ __launch_bounds__(64) void reduce_multi_phased_kernel(SendList sends,
 }
 
 // Chain order as reduce_chain_vec_kernel; ph.p[K] is own's phase.
-template <typename T, int OP, int K>
+template <typename T, int OP, int K, bool XCD>
 __global__ __launch_bounds__(64) void reduce_chain_phased_kernel(SendList sends, PhaseList ph,
                                                                  const unsigned char* own, unsigned char* dst,
                                                                  size_t head, size_t nvec, size_t tail) {
     const size_t off = head * sizeof(T);
     u32x4* vd = reinterpret_cast<u32x4*>(dst + off);
     const size_t ntiles = (nvec + 63) / 64;
-    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (size_t t = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; t < ntiles; t += gridDim.x) {
         const size_t v = t * 64 + threadIdx.x;
         u32x4 s[K];
 #pragma unroll
@@ -570,11 +614,6 @@ int multi_straddle_typed(SendList sl, int nsend, unsigned char* r, Split sp, hip
 template <typename T, int OP>
 int chain_straddle_typed(SendList sl, int nsend, const unsigned char* own, unsigned char* d, Split sp,
                          hipStream_t stream);
-// A recv that is not element-aligned (misaligned.hip): boundary pass + vector pass, every recv vector
-// written whole by one wave.  sizeof(T) > 1.  kNoScratch: the stream-ordered scratch could not be had.
-constexpr int kNoScratch = -1;
-template <typename T, int OP>
-int reduce_misaligned_typed(const unsigned char* s, unsigned char* r, size_t count, hipStream_t stream);
 template <typename T, int OP>
 int chain_phased_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp,
                        hipStream_t stream);

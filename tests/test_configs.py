@@ -132,7 +132,8 @@ def test_kway_and_chain_line_straddling_sources(gpu, k):
 @pytest.mark.slow
 @pytest.mark.parametrize("dt,roff,soff", [(7, 1, 0), (7, 2, 7), (8, 3, 0), (8, 4, 12), (9, 1, 0), (2, 3, 2)])
 def test_recv_misaligned_large_against_oracle(gpu, dt, roff, soff):
-    """A recv that is not element-aligned (boundary pass + vector pass, misaligned.hip) at 64 MiB, across
+    """A recv that is not element-aligned (reduce_unaligned_kernel: one 16-B access per lane at
+    the displaced addresses) at 64 MiB, across
     many tiles and grid strides: the whole result against the oracle, nothing outside recv written."""
     import dccl_amd
     esz = int(oracle.NP_DTYPES[dt]().itemsize)

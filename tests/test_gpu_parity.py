@@ -167,8 +167,8 @@ def test_shifted_kernel_every_phase(dccl, dt):
 
 @pytest.mark.parametrize("dt", [2, 3, 4, 5, 6, 7, 8, 9])
 def test_element_misaligned_every_offset(dccl, dt):
-    """Element-misaligned operands (recv not a multiple of sizeof(T); the byte-gather kernel): every
-    recv byte offset in a 16-B vector, send at several byte phases, sizes around a 64-vector tile,
+    """Element-misaligned operands (recv not a multiple of sizeof(T); reduce_unaligned_kernel, 16-B accesses
+    at any byte address, and its element-wise tail): every recv byte offset in a 16-B vector, send at several byte phases, sizes around a 64-vector tile,
     partial tiles; nothing outside recv's bytes is written."""
     rng = np.random.default_rng(700 + dt)
     esz = np.dtype(oracle.NP_DTYPES[dt]).itemsize

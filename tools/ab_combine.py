@@ -36,11 +36,15 @@ def bind(path):
     return lib
 
 
+NVAR = 18
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("libs", nargs=2)
     p.add_argument("--rounds", type=int, default=7)
     p.add_argument("--tune", action="store_true", help="also time the misaligned-recv shape variants")
+    p.add_argument("--tune-only", action="store_true", help="only the misaligned-recv shape variants")
     p.add_argument("--out", default="")
     a = p.parse_args()
     libs = [bind(x) for x in a.libs]
@@ -70,6 +74,8 @@ def main():
     cases.append(("chain k=7, sources +4 B (phased)", 9,
                   lambda lib: lib.dccl_local_reduce_chain(arr7, 7, recv0, recv0, 7, n, 0, st)))
     rows = []
+    if a.tune_only:
+        a.tune, cases = True, []
     for name, mult, call in cases:
         t = {0: [], 1: []}
         for _ in range(a.rounds):
@@ -82,17 +88,23 @@ def main():
             print(json.dumps(rows[-1]), flush=True)
     if a.tune:
         from tools import tune_lib
-        for roff in (1, 2):
-            t = {v: [] for v in range(7)}
-            for _ in range(a.rounds):
-                for v in range(7):
-                    fn = lambda v=v: tune_lib.lib.dccl_tune_misaligned_f32_sum(send0, recv0 + roff, n, v, st)
-                    t[v].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
-            for v in range(7):
-                ms = statistics.median(t[v])
-                rows.append({"lib": "tune", "case": f"misaligned recv +{roff} variant {v}", "ms": round(ms, 4),
-                             "frac": round(3 * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
-                print(json.dumps(rows[-1]), flush=True)
+        del srcs
+        s2 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        r2 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        dccl_amd.check(dccl_amd.synth_fill(s2.data_ptr(), 7, nbytes // 4, 0, 0xDCC1, 3, st), "synth")
+        dccl_amd.check(dccl_amd.synth_fill(r2.data_ptr(), 7, nbytes // 4, 0, 0xDCC1, 4, st), "synth")
+        for layout, sb, rb in (("pooled", send0, recv0), ("separate", s2.data_ptr(), r2.data_ptr())):
+            for roff in (1,):
+                t = {v: [] for v in range(NVAR)}
+                for _ in range(a.rounds):
+                    for v in range(NVAR):
+                        fn = lambda v=v: tune_lib.lib.dccl_tune_misaligned_f32_sum(sb, rb + roff, n, v, st)
+                        t[v].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+                for v in range(NVAR):
+                    ms = statistics.median(t[v])
+                    rows.append({"lib": "tune", "case": f"{layout}: misaligned recv +{roff} variant {v}",
+                                 "ms": round(ms, 4), "frac": round(3 * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
+                    print(json.dumps(rows[-1]), flush=True)
     if a.out:
         with open(a.out, "w") as f:
             json.dump(rows, f, indent=1)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Workload for rocprofv3 passes over the misaligned-recv combine (misaligned.hip): fp32 Sum, 1 GiB per
+"""Workload for rocprofv3 passes over the misaligned-recv combine (reduce_unaligned_kernel): fp32 Sum, 1 GiB per
 operand, recv at byte offset --roff (default 1) and send at --soff, --launches launches; with --roff 0 the
 aligned combine for comparison.  Run under `rocprofv3 --kernel-trace --stats` (durations of the boundary
 pass and the vector pass) and `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` (traffic).

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Tuning only: the phased k-way combine's shape variants (tools/tune/tune_kernels.hip,
+dccl_tune_phased_f32_sum) at 1 GiB per operand, fp32 Sum, k = 2-5 and 7 sources at a 16-B phase of +4 B
+(and +12 B for k = 2; k = 2 again at the end, after the other allocations); then the phased chain
+kernel (in place, own = recv) for k = 1-5, 7 with the XCD tile order off and on. against a 128-B aligned recv, interleaved over --rounds; HBM fraction of (k+2)N.
+    python tools/phased_probe.py [--rounds 5] [--out f.json]
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import dccl_amd  # noqa: E402
+from tools import tune_lib  # noqa: E402
+from tools.bench_suite import PEAK, time_launches  # noqa: E402
+
+NVAR = 2  # the lane-exchange forms; 2-3 (unaligned loads) lost 3-8 points at every k (round 2)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--out", default="")
+    a = p.parse_args()
+    st = torch.cuda.current_stream().cuda_stream
+    nbytes = 1 << 30
+    n = nbytes // 4 - 64
+    recv = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    srcs = torch.empty(7 * (nbytes + 4096), dtype=torch.uint8, device="cuda")
+    dccl_amd.check(dccl_amd.synth_fill(recv.data_ptr(), 7, nbytes // 4, 0, 0xDCC1, 1, st), "synth")
+    rows = []
+    for k, phase in ((2, 4), (2, 12), (3, 4), (4, 4), (5, 4), (2, 4), (7, 4)):
+        sp = [srcs.data_ptr() + j * (nbytes + 4096) + phase for j in range(k)]
+        for j, q in enumerate(sp):
+            dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
+        arr = (ctypes.c_void_p * k)(*sp)
+        t = {v: [] for v in range(NVAR)}
+        for _ in range(a.rounds):
+            for v in range(NVAR):
+                fn = lambda v=v: dccl_amd.check(tune_lib.lib.dccl_tune_phased_f32_sum(arr, k, recv.data_ptr(), n, v,
+                                                                                     st), "phased")
+                t[v].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+        for v in range(NVAR):
+            ms = statistics.median(t[v])
+            rows.append({"k": k, "phase": phase, "variant": v, "ms": round(ms, 4),
+                         "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
+            print(json.dumps(rows[-1]), flush=True)
+    # chain (ring order), in place: own = recv (in phase), k sources +4 B; XCD order off (0) / on (1)
+    for k in (1, 2, 3, 4, 5, 7):
+        sp = [srcs.data_ptr() + j * (nbytes + 4096) + 4 for j in range(k)]
+        arr = (ctypes.c_void_p * k)(*sp)
+        t = {v: [] for v in (0, 1)}
+        for _ in range(a.rounds):
+            for v in (0, 1):
+                fn = lambda v=v: dccl_amd.check(tune_lib.lib.dccl_tune_chain_phased_f32_sum(
+                    arr, k, recv.data_ptr(), recv.data_ptr(), n, v, st), "chain phased")
+                t[v].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+        for v in (0, 1):
+            ms = statistics.median(t[v])
+            rows.append({"chain_k": k, "phase": 4, "xcd": v, "ms": round(ms, 4),
+                         "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
+            print(json.dumps(rows[-1]), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -31,7 +31,7 @@ int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count, int waves
 /* the in-phase chain kernel (dccl_local_reduce_chain) with `lds_bytes` of unused LDS per one-wave block */
 int dccl_tune_chain_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
                             size_t lds_bytes, void* stream);
-/* the misaligned-recv combine (dccl_amd/csrc/misaligned.hpp) in shape `variant` 0-6 (see tune_kernels.hip) */
+/* the misaligned-recv combine in shape `variant` 0-9 (see tune_kernels.hip) */
 int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t count, int variant, void* stream);
 int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
                             size_t lds_bytes, void* stream);
@@ -54,6 +54,14 @@ int dccl_tune_pipelined_f32_sum(const void* send, void* recv, size_t count, int 
 int dccl_tune_write_num_variants(void);
 int dccl_tune_write_probe(int variant, void* recv, size_t count_f32, int* block, int* unroll, int* policy,
                           void* stream);
+/* the phased k-way combine (k = 2-5, 7) in shape `variant` 0-3 (see tune_kernels.hip) */
+int dccl_tune_phased_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
+                             void* stream);
+
+/* the phased chain combine (k = 1-5, 7) with the XCD tile order on (xcd 1) or off */
+int dccl_tune_chain_phased_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
+                                   int xcd, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,10 +1,12 @@
-// dccl_amd/csrc/misaligned.hpp — the combine for a recv that is not element-aligned (e.g. an fp32 chunk at
-// an odd byte address), at vector speed.  Instantiated by misaligned.hip (production) and by the tuning
-// library (shape variants).
+// tools/tune/misaligned_2pass.hpp — TUNING ONLY (not shipped): a two-pass combine for a recv that is not
+// element-aligned, kept for the record of round 2's measurements.  On MI355X it ran at
+// 74.6-75.6 % of HBM peak (4 vectors per lane, send cached), 1-2 points above the one-access-per-lane kernel
+// that ships (reduce_unaligned_kernel: 73.6-74.8 %), which needs no scratch, no second launch and no
+// allocation on the device path (tools/ab_combine.py --tune, profiles/r2_misaligned_ab.json).
 //
 // The reference's host loop accepts such a recv with a warning (/root/reference/src/core/
 // internal_common.hpp:504-512); its CUDA kernel cannot take one at all.  Round 1 ran it as a byte kernel
-// (65-71 % of HBM peak).  The difficulty is the write side: with recv's elements straddling every 16-B
+// (65-73 % of HBM peak).  The difficulty is the write side: with recv's elements straddling every 16-B
 // vector boundary, an element that straddles the boundary between two waves' tiles is half written by
 // each, and whichever wave writes first destroys the original bytes the other still has to read.  Byte
 // stores of the shared vector by both waves were measured in round 1 and lose (partial line writes,
@@ -150,7 +152,7 @@ __global__ __launch_bounds__(64) void reduce_misaligned_kernel(Geometry g, const
     }
 }
 
-// The two passes on `stream`, with a stream-ordered scratch of 32 B per tile.  kNoScratch if it cannot be
+// The two passes on `stream`, with a stream-ordered scratch of 32 B per tile.  -1 if it cannot be
 // allocated (the caller then takes the byte kernel).
 template <typename T, int OP, int U, bool SEND_NT>
 int launch_misaligned(const unsigned char* s, unsigned char* r, size_t count, hipStream_t stream) {
@@ -172,7 +174,7 @@ int launch_misaligned(const unsigned char* s, unsigned char* r, size_t count, hi
     u32x4* saved = nullptr;
     if (hipMallocAsync(reinterpret_cast<void**>(&saved), 2 * ntiles * sizeof(u32x4), stream) != hipSuccess) {
         (void)hipGetLastError();
-        return kNoScratch;
+        return -1;
     }
     void* a1[] = {&g, &saved, &ntiles};
     int rc = launch(reinterpret_cast<const void*>(&save_boundaries_kernel<U>), ceil_div(ntiles, size_t(256)), a1,

@@ -8,7 +8,7 @@
 
 #include "dccl/dccl_reduce.h"
 #include "dccl_reduce_tuning.h"
-#include "misaligned.hpp"
+#include "misaligned_2pass.hpp"
 #include "reduce_kernels.hpp"
 
 using namespace dccl_amd;
@@ -489,8 +489,86 @@ extern "C" int dccl_tune_pipelined_f32_sum(const void* send, void* recv, size_t 
 }
 
 // ---------------------------------------------------------------------------------
-// Tuning only: the misaligned-recv combine (misaligned.hpp) in shape `variant`:
-// 0/1 = 1 vector per lane, send cached / non-temporal; 2/3 = 2 vectors; 4/5 = 4 vectors; 6 = the byte kernel.
+// Tuning only: the misaligned-recv combine in shape `variant` (two-pass: misaligned_2pass.hpp):
+// 0/1 = 1 vector per lane, send cached / non-temporal; 2/3 = 2 vectors; 4/5 = 4 vectors; 6 = the byte kernel;
+// 7/8/9 = one 16-B access per lane at the displaced address itself (align-1 vector types: gfx950 takes
+// global_load/store_dwordx4 at any byte address, tools/unaligned_probe.hip), 7 all non-temporal (the shipped
+// reduce_unaligned_kernel's shape), 8 send cached, 9 nothing non-temporal; 10-17 the walking / XCD-grouped
+// forms of 7 (tune_unaligned_walk_kernel).  Adjacent lanes' 16-B windows are disjoint and hold whole elements.
+namespace {
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+template <int P>  // policy bits as VecCfg: kNtSend | kNtRecv | kNtStore
+__global__ __launch_bounds__(64) void tune_unaligned_kernel(const unsigned char* s, unsigned char* r, size_t nvec,
+                                                            size_t count) {
+    const size_t i = size_t(blockIdx.x) * 64 + threadIdx.x;
+    if (i < nvec) {
+        const u32x4_u* ps = reinterpret_cast<const u32x4_u*>(s + 16 * i);
+        u32x4_u* pr = reinterpret_cast<u32x4_u*>(r + 16 * i);
+        u32x4 a, b;
+        if constexpr ((P & kNtRecv) != 0) a = __builtin_nontemporal_load(pr); else a = *pr;
+        if constexpr ((P & kNtSend) != 0) b = __builtin_nontemporal_load(ps); else b = *ps;
+        const u32x4 o = combine16<float, kSum>(a, b);
+        if constexpr ((P & kNtStore) != 0) __builtin_nontemporal_store(o, pr); else *pr = o;
+    }
+    if (blockIdx.x == 0)
+        for (size_t j = 4 * nvec + threadIdx.x; j < count; j += 64)
+            st_elem<float, false>(r, j, Combine<float, kSum>::apply(ld_elem<float, false>(r, j), ld_elem<float, false>(s, j)));
+}
+template <int P>
+int tune_unaligned(const unsigned char* s, unsigned char* r, size_t count, hipStream_t st) {
+    size_t nvec = count / 4;
+    void* args[] = {const_cast<unsigned char**>(&s), &r, &nvec, &count};
+    return launch(reinterpret_cast<const void*>(&tune_unaligned_kernel<P>), ceil_div(nvec, size_t(64)) + 1, args, st, 64);
+}
+// Each wave walks CH consecutive 1 KiB chunks (so the lines two chunks share are touched by one wave, in
+// one XCD's L2), four chunks' loads in flight at a time.  XCD: CH = 1 and consecutive tiles on one XCD
+// (blocks are dealt round-robin over the 8 XCDs).
+template <int P, int CH, bool XCD>
+__global__ __launch_bounds__(64) void tune_unaligned_walk_kernel(const unsigned char* s, unsigned char* r, size_t nvec,
+                                                                 size_t count) {
+    size_t t0 = size_t(blockIdx.x) * CH;
+    if constexpr (XCD) {
+        const size_t per = gridDim.x / 8;  // grid is a multiple of 8
+        t0 = size_t(blockIdx.x % 8) * per + blockIdx.x / 8;
+    }
+    constexpr int G = CH < 4 ? CH : 4;
+    for (int c0 = 0; c0 < CH; c0 += G) {
+        u32x4 a[G], b[G];
+#pragma unroll
+        for (int c = 0; c < G; ++c) {
+            const size_t i = (t0 + c0 + c) * 64 + threadIdx.x;
+            if (i < nvec) {
+                const u32x4_u* ps = reinterpret_cast<const u32x4_u*>(s + 16 * i);
+                const u32x4_u* pr = reinterpret_cast<const u32x4_u*>(r + 16 * i);
+                if constexpr ((P & kNtRecv) != 0) a[c] = __builtin_nontemporal_load(pr); else a[c] = *pr;
+                if constexpr ((P & kNtSend) != 0) b[c] = __builtin_nontemporal_load(ps); else b[c] = *ps;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < G; ++c) {
+            const size_t i = (t0 + c0 + c) * 64 + threadIdx.x;
+            if (i < nvec) {
+                u32x4_u* pr = reinterpret_cast<u32x4_u*>(r + 16 * i);
+                const u32x4 o = combine16<float, kSum>(a[c], b[c]);
+                if constexpr ((P & kNtStore) != 0) __builtin_nontemporal_store(o, pr); else *pr = o;
+            }
+        }
+    }
+    if (blockIdx.x == 0)
+        for (size_t j = 4 * nvec + threadIdx.x; j < count; j += 64)
+            st_elem<float, false>(r, j, Combine<float, kSum>::apply(ld_elem<float, false>(r, j), ld_elem<float, false>(s, j)));
+}
+template <int P, int CH, bool XCD>
+int tune_unaligned_walk(const unsigned char* s, unsigned char* r, size_t count, hipStream_t st) {
+    size_t nvec = count / 4;
+    size_t grid = ceil_div(ceil_div(nvec, size_t(64)), size_t(CH));
+    if (XCD) grid = ceil_div(grid, size_t(8)) * 8;
+    if (grid == 0) grid = 1;
+    if (grid > kMaxGrid) return DCCL_INVALID_ARGUMENT;  // no grid stride here
+    void* args[] = {const_cast<unsigned char**>(&s), &r, &nvec, &count};
+    return launch(reinterpret_cast<const void*>(&tune_unaligned_walk_kernel<P, CH, XCD>), grid, args, st, 64);
+}
+}  // namespace
 // recv must not be element-aligned (fp32: an address that is not a multiple of 4).
 // ---------------------------------------------------------------------------------
 extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t count, int variant, void* stream) {
@@ -510,7 +588,154 @@ extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t
         return launch(reinterpret_cast<const void*>(&reduce_scalar_kernel<float, kSum, false>),
                       ceil_div(count, size_t(kBlock) * 4), args, st);
     }
+    case 7: return tune_unaligned<kNtSend | kNtRecv | kNtStore>(s, r, count, st);
+    case 8: return tune_unaligned<kNtRecv | kNtStore>(s, r, count, st);
+    case 9: return tune_unaligned<0>(s, r, count, st);
+    case 10: return tune_unaligned_walk<kNtSend | kNtRecv | kNtStore, 4, false>(s, r, count, st);
+    case 11: return tune_unaligned_walk<kNtStore, 4, false>(s, r, count, st);
+    case 12: return tune_unaligned_walk<kNtSend | kNtRecv | kNtStore, 16, false>(s, r, count, st);
+    case 13: return tune_unaligned_walk<kNtStore, 16, false>(s, r, count, st);
+    case 14: return tune_unaligned_walk<0, 16, false>(s, r, count, st);
+    case 15: return tune_unaligned_walk<kNtStore, 1, true>(s, r, count, st);
+    case 16: return tune_unaligned_walk<kNtSend | kNtRecv | kNtStore, 1, true>(s, r, count, st);
+    case 17: return tune_unaligned_walk<kNtStore, 64, false>(s, r, count, st);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
 
+
+// ---------------------------------------------------------------------------------
+// Tuning only: the phased k-way combine (sources element-aligned at other 16-B phases than recv) in
+// shape `variant`, recv 128-B aligned past the head scalars:
+//   0 the shipped shape (reduce_multi_phased_kernel: aligned loads, DPP neighbour, funnel shift);
+//   1 the same with consecutive tiles on one XCD (lane 63's extra vector and the next tile's first line
+//     then meet in one L2);
+//   2 every off-phase source read with one 16-B load at its own (unaligned) address, no lane exchange;
+//   3 = 2 with consecutive tiles on one XCD.
+// ---------------------------------------------------------------------------------
+namespace {
+template <int K, int MODE>
+__global__ __launch_bounds__(64) void tune_phased_kernel(SendList sends, PhaseList ph, unsigned char* __restrict__ recv,
+                                                         size_t head, size_t nvec, size_t tail) {
+    constexpr bool XCD = (MODE & 1) != 0, UNALIGNED = (MODE & 2) != 0;
+    const size_t off = head * sizeof(float);
+    u32x4* vr = reinterpret_cast<u32x4*>(recv + off);
+    const size_t ntiles = (nvec + 63) / 64;
+    const size_t t0 = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    for (size_t t = t0; t < ntiles; t += gridDim.x) {
+        const size_t v = t * 64 + threadIdx.x;
+        u32x4 s[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if constexpr (UNALIGNED) {
+                s[k] = u32x4{0u, 0u, 0u, 0u};
+                if (v < nvec) s[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(sends.p[k] + off) + v);
+            } else {
+                s[k] = ld_phased(sends.p[k] + off, ph.p[k], v, nvec);
+            }
+        }
+        if (v < nvec) {
+            u32x4 acc = ld16<true>(vr + v);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = combine16<float, kSum>(acc, s[k]);
+            __builtin_nontemporal_store(acc, vr + v);
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (size_t j = threadIdx.x; j < head + tail; j += blockDim.x) {
+            const size_t i = j < head ? j : head + nvec * 4 + (j - head);
+            float acc = ld_elem<float, true>(recv, i);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = Combine<float, kSum>::apply(acc, ld_elem<float, true>(sends.p[k], i));
+            st_elem<float, true>(recv, i, acc);
+        }
+    }
+}
+template <int K, int MODE>
+int tune_phased_k(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStream_t st) {
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0) grid = 1;
+    if (grid > kMaxGrid) return DCCL_INVALID_ARGUMENT;  // one tile per block (the XCD map is over the grid)
+    void* args[] = {&sl, &ph, &r, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&tune_phased_kernel<K, MODE>), grid, args, st, 64);
+}
+template <int MODE>
+int tune_phased_mode(SendList sl, PhaseList ph, int k, unsigned char* r, Split sp, hipStream_t st) {
+    switch (k) {
+    case 2: return tune_phased_k<2, MODE>(sl, ph, r, sp, st);
+    case 3: return tune_phased_k<3, MODE>(sl, ph, r, sp, st);
+    case 4: return tune_phased_k<4, MODE>(sl, ph, r, sp, st);
+    case 5: return tune_phased_k<5, MODE>(sl, ph, r, sp, st);
+    case 7: return tune_phased_k<7, MODE>(sl, ph, r, sp, st);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+}  // namespace
+
+extern "C" int dccl_tune_phased_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
+                                        void* stream) {
+    if (sends == nullptr || recv == nullptr) return DCCL_INVALID_ARGUMENT;
+    const uintptr_t ar = reinterpret_cast<uintptr_t>(recv);
+    if (ar & 3) return DCCL_INVALID_ARGUMENT;
+    SendList sl{};
+    for (int k = 0; k < nsend && k < 8; ++k) {
+        if (reinterpret_cast<uintptr_t>(sends[k]) & 3) return DCCL_INVALID_ARGUMENT;
+        sl.p[k] = static_cast<const unsigned char*>(sends[k]);
+    }
+    const Split sp = split_for_vectors<float>(ar, count, 128);
+    PhaseList ph{};
+    for (int k = 0; k < nsend && k < 8; ++k) ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(float));
+    auto r = static_cast<unsigned char*>(recv);
+    const auto st = static_cast<hipStream_t>(stream);
+    switch (variant) {
+    case 0: return tune_phased_mode<0>(sl, ph, nsend, r, sp, st);
+    case 1: return tune_phased_mode<1>(sl, ph, nsend, r, sp, st);
+    case 2: return tune_phased_mode<2>(sl, ph, nsend, r, sp, st);
+    case 3: return tune_phased_mode<3>(sl, ph, nsend, r, sp, st);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+
+// Tuning only: the shipped phased chain kernel with the XCD tile order forced on (xcd 1) or off (0).
+namespace {
+template <int K, bool X>
+int tune_chain_phased_k(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, Split sp, hipStream_t st) {
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0) grid = 1;
+    void* args[] = {&sl, &ph, &own, &d, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<float, kSum, K, X>), grid, args, st, 64);
+}
+template <bool X>
+int tune_chain_phased_x(SendList sl, PhaseList ph, int k, const unsigned char* own, unsigned char* d, Split sp,
+                        hipStream_t st) {
+    switch (k) {
+    case 1: return tune_chain_phased_k<1, X>(sl, ph, own, d, sp, st);
+    case 2: return tune_chain_phased_k<2, X>(sl, ph, own, d, sp, st);
+    case 3: return tune_chain_phased_k<3, X>(sl, ph, own, d, sp, st);
+    case 4: return tune_chain_phased_k<4, X>(sl, ph, own, d, sp, st);
+    case 5: return tune_chain_phased_k<5, X>(sl, ph, own, d, sp, st);
+    case 7: return tune_chain_phased_k<7, X>(sl, ph, own, d, sp, st);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+}  // namespace
+
+extern "C" int dccl_tune_chain_phased_f32_sum(const void* const* sends, int nsend, const void* own, void* dst,
+                                              size_t count, int xcd, void* stream) {
+    if (sends == nullptr || own == nullptr || dst == nullptr || nsend < 1 || nsend > 8) return DCCL_INVALID_ARGUMENT;
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
+    if ((ad & 3) || (reinterpret_cast<uintptr_t>(own) & 3)) return DCCL_INVALID_ARGUMENT;
+    SendList sl{};
+    for (int k = 0; k < nsend; ++k) {
+        if (reinterpret_cast<uintptr_t>(sends[k]) & 3) return DCCL_INVALID_ARGUMENT;
+        sl.p[k] = static_cast<const unsigned char*>(sends[k]);
+    }
+    const Split sp = split_for_vectors<float>(ad, count, 128);
+    PhaseList ph{};
+    for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(float));
+    const auto o = static_cast<const unsigned char*>(own);
+    ph.p[nsend] = phase_word(o, sp.head * sizeof(float));
+    auto d = static_cast<unsigned char*>(dst);
+    const auto st = static_cast<hipStream_t>(stream);
+    return xcd ? tune_chain_phased_x<true>(sl, ph, nsend, o, d, sp, st) : tune_chain_phased_x<false>(sl, ph, nsend, o, d, sp, st);
+}
