@@ -21,7 +21,9 @@ Rank 0 prints ONE JSON line:
   cpu_baseline     the build's C restatement of the reference loop (oracle/host_reduce.c, Release flags)
                    on the headline's own 1 GiB operands in host memory: 1 core and every core this
                    process may use (rank 0, N=1); nproc and the CPU model are stated
-Extra keys: payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
+Extra keys: c3 (BASELINE C3: 4 ops x fp16/bf16/fp32/int32/int64 at 1 GiB, timed and sample-verified) and
+c4 (BASELINE C4: fp32 Sum size sweep 4 KiB - 4 GiB, per-launch duration and fraction of HBM peak), rank 0 at
+N=1; payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
 rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately),
 c5 (BASELINE config C5 on every run: --c5-gib GiB per operand sharded over the N GPUs, strong scaling,
 combine time and, N>1, the RCCL all-gather of the reduced shards),
@@ -76,6 +78,8 @@ def parse():
                    help="skip the rocprofv3 --pmc passes that measure roofline.traffic (N=1)")
     p.add_argument("--no-other-layout", action="store_true",
                    help="skip timing the other operand layout (profiling runs: one layout per kernel average)")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip the C3 (ops x dtypes, 1 GiB) and C4 (size sweep 4 KiB - 4 GiB) legs (rank 0, N=1)")
     p.add_argument("--layout", default="pooled", choices=["pooled", "separate"],
                    help="operand placement in HBM (see operand_pair); the other layout is also timed briefly")
     return p.parse_args()
@@ -328,6 +332,89 @@ def host_staged_rate(nbytes: int, dt: int, op: int) -> dict:
     t = (time.perf_counter() - t0) / reps
     return {"payload_gib_s": round(nbytes / t / GIB, 2), "ms": round(t * 1e3, 3),
             "bytes_per_operand": nbytes, "note": "pinned host operands; PCIe H2D 2N + D2H N bytes"}
+
+
+def config_c3(dev, stream, nbytes: int = 1 << 30, launches: int = 10) -> list:
+    """BASELINE config C3: every ncclRedOp_t x {fp16, bf16, fp32, int32, int64} on 1 GiB operands (pooled
+    layout), each timed over `launches` back-to-back launches (HIP events on the launch stream) and its
+    result checked by verify_sample (3 + launches applications)."""
+    out = []
+    pool = torch.empty(2 * nbytes + PAIR_GAP, dtype=torch.uint8, device=dev)
+    names = {6: "f16", 9: "bf16", 7: "f32", 2: "i32", 4: "i64"}
+    for dt in (6, 9, 7, 2, 4):
+        esz = dccl_amd.size_of_type(dt)
+        n = nbytes // esz
+        tdt = dccl_amd.TORCH_DTYPES[dt]
+        recv = pool[:nbytes].view(tdt)
+        send = pool[nbytes + PAIR_GAP:].view(tdt)
+        for op, oname in enumerate(("sum", "prod", "max", "min")):
+            synth_into(send, n, dt, op, 20)
+            synth_into(recv, n, dt, op, 21)
+            k = time_kernel(send.data_ptr(), recv.data_ptr(), dt, n, op, stream, launches)
+            ok = verify_sample(recv, n, dt, op, 20, 21, 3 + launches)
+            out.append({"dtype": names[dt], "op": oname, "kernel_ms_avg": round(k, 4),
+                        "frac": round(3 * nbytes / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "verified": ok})
+    del pool
+    torch.cuda.empty_cache()
+    return out
+
+
+def graph_us_per_launch(ps: int, pr: int, n: int, dev, per_graph: int = 200, replays: int = 10) -> float:
+    """Average duration (us) of one fp32 Sum combine of n elements when `per_graph` launches are captured in
+    one HIP graph (torch.cuda.CUDAGraph over dccl_local_reduce on the capture stream) and the graph is replayed
+    `replays` times: the device-side cost per launch without the host's issue rate."""
+    side = torch.cuda.Stream(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        dccl_amd.check(dccl_amd.local_reduce(ps, pr, 7, n, 0, side.cuda_stream), "warm")
+        side.synchronize()
+        with torch.cuda.graph(g, stream=side):
+            for _ in range(per_graph):
+                dccl_amd.check(dccl_amd.local_reduce(ps, pr, 7, n, 0, side.cuda_stream), "capture")
+    g.replay()
+    torch.cuda.synchronize(dev)
+    cur = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(cur)
+    for _ in range(replays):
+        g.replay()
+    ev1.record(cur)
+    ev1.synchronize()
+    ms = ev0.elapsed_time(ev1)
+    del g
+    return ms * 1e3 / (replays * per_graph)
+
+
+def config_c4(dev, stream) -> list:
+    """BASELINE config C4: size sweep 4 KiB - 4 GiB per operand, ncclSum fp32, pooled layout.  Per size: the
+    average duration of back-to-back launches (HIP events on the launch stream, >= ~20 ms of launches), the
+    HBM rate 3*bytes/t against the 8 TB/s roofline and the payload GiB/s; small sizes are launch-bound, so up
+    to 64 MiB the same launches are also replayed from a HIP graph (graph_us_per_launch, graph_frac)."""
+    out = []
+    top = 4 << 30
+    pool = torch.empty(2 * top + PAIR_GAP, dtype=torch.uint8, device=dev)
+    synth_into(pool[:top].view(torch.float32), top // 4, 7, 0, 30)
+    synth_into(pool[top + PAIR_GAP:].view(torch.float32), top // 4, 7, 0, 31)
+    pr, ps = pool.data_ptr(), pool.data_ptr() + top + PAIR_GAP
+    nb = 4 << 10
+    while nb <= top:
+        n = nb // 4
+        k = time_kernel(ps, pr, 7, n, 0, stream, 5)
+        launches = int(min(20000, max(10, 20.0 / max(k, 1e-4))))
+        k = time_kernel(ps, pr, 7, n, 0, stream, launches)
+        row = {"bytes_per_operand": nb, "launches": launches, "us_per_launch": round(k * 1e3, 2),
+               "hbm_gb_s": round(3 * nb / (k * 1e-3) / 1e9, 1),
+               "frac": round(3 * nb / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+               "payload_gib_s": round(nb / (k * 1e-3) / GIB, 2)}
+        if nb <= (64 << 20):  # eager launches are host-issue-bound here: replay them from a HIP graph too
+            g = graph_us_per_launch(ps, pr, n, dev)
+            row["graph_us_per_launch"] = round(g, 2)
+            row["graph_frac"] = round(3 * nb / (g * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+        out.append(row)
+        nb *= 4
+    del pool
+    torch.cuda.empty_cache()
+    return out
 
 
 def run_with_watchdog(fn, seconds: float):
@@ -778,6 +865,13 @@ def main():
         res.update(extra)
         if world == 1 and not a.no_host_staged:
             res["host_staged"] = host_staged_rate(nbytes, dt, op)
+        if world == 1 and not a.no_configs:
+            send = recv = None
+            torch.cuda.empty_cache()
+            progress("C3: ops x dtypes at 1 GiB")
+            res["c3"] = config_c3(dev, stream)
+            progress("C4: size sweep 4 KiB - 4 GiB")
+            res["c4"] = config_c4(dev, stream)
         if world == 1 and not a.no_cpu:
             res["cpu_baseline"] = cpu_baseline(a.cpu_seconds, nbytes)
         print(json.dumps(res), flush=True)

@@ -73,7 +73,8 @@ def test_bench_direct_allreduce_two_processes_one_gpu():
 
 
 def test_bench_single_gpu_line():
-    """bench.py at N=1 prints exactly one JSON line with the contract's keys and the C5 extra."""
+    """bench.py at N=1 prints exactly one JSON line with the contract's keys, the C5 extra and the C3 / C4
+    legs (every C3 entry sample-verified)."""
     import json
     import subprocess
     import sys
@@ -93,3 +94,7 @@ def test_bench_single_gpu_line():
     assert res["cpu_baseline"]["cores"] >= 1 and res["cpu_baseline"]["value"] > 0
     c5 = res["c5"]
     assert c5["scaling"] == "strong" and c5["combine_ms"] > 0 and "allgather" not in c5
+    assert len(res["c3"]) == 20 and all(r["verified"] for r in res["c3"]), res["c3"]
+    sizes = [r["bytes_per_operand"] for r in res["c4"]]
+    assert sizes[0] == 4096 and sizes[-1] == 4 << 30 and all(r["us_per_launch"] > 0 for r in res["c4"])
+    assert all(r["graph_us_per_launch"] > 0 for r in res["c4"] if r["bytes_per_operand"] <= 64 << 20)
