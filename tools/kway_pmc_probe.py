@@ -4,7 +4,8 @@
 Workload (run under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE --kernel-trace): ten 1 GiB fp32 operands
 carved from one allocation with a 4 KiB x (j+1) stagger (tools/bench_suite.py's "staggered" layout);
 for k = 1..8, --launches launches of dccl_local_reduce_multi (recv = recv + s0 + ... ) and of
-dccl_local_reduce_chain (own in place), in that order.  The parse step joins each dispatch's duration
+dccl_local_reduce_chain (own in place), in that order; --phase P puts every source P bytes further (P = 4:
+the phased kernels, sources off the destination's 16-B phase).  Counts are N - 16 elements.  The parse step joins each dispatch's duration
 with its counters and reports, per kernel and k, read bytes = 2 x FETCH_SIZE (gfx950 wide-read halving,
 MI355X_MICROARCH.md §HBM), write bytes = WRITE_SIZE, their ratio to (k+1)*N and N, and the fraction
 of the 8 TB/s peak the dispatch ran at.
@@ -26,31 +27,31 @@ NBYTES = 1 << 30
 PEAK = 8e12
 
 
-def run(launches: int, mib: int) -> None:
+def run(launches: int, mib: int, phase: int = 0) -> None:
     import torch
     sys.path.insert(0, ROOT)
     import dccl_amd
     nbytes = mib << 20
     n = nbytes // 4
     st = torch.cuda.current_stream().cuda_stream
-    pool = torch.empty(10 * nbytes + 4096 * 55, dtype=torch.uint8, device="cuda")
+    pool = torch.empty(10 * nbytes + 4096 * 55 + 64, dtype=torch.uint8, device="cuda")
     ptrs, off = [], 0
     for j in range(10):
         ptrs.append(pool.data_ptr() + off)
         dccl_amd.check(dccl_amd.synth_fill(ptrs[-1], 7, n, 0, 0xDCC1, 10 + j, st), "synth")
         off += nbytes + 4096 * (j + 1)
-    sends, recv = ptrs[:8], ptrs[8]
+    sends, recv = [q + phase for q in ptrs[:8]], ptrs[8]  # phase != 0: the phased kernels
     torch.cuda.synchronize()
     order = []
     for k in range(1, 9):
         for _ in range(launches):
-            dccl_amd.check(dccl_amd.local_reduce_multi(sends[:k], recv, 7, n, 0, st), "multi")
+            dccl_amd.check(dccl_amd.local_reduce_multi(sends[:k], recv, 7, n - 16, 0, st), "multi")
             order.append({"what": "multi", "k": k})
         for _ in range(launches):
-            dccl_amd.check(dccl_amd.local_reduce_chain(sends[:k], recv, recv, 7, n, 0, st), "chain")
+            dccl_amd.check(dccl_amd.local_reduce_chain(sends[:k], recv, recv, 7, n - 16, 0, st), "chain")
             order.append({"what": "chain", "k": k})
     torch.cuda.synchronize()
-    print(json.dumps({"order": order, "bytes_per_operand": nbytes}), flush=True)
+    print(json.dumps({"order": order, "bytes_per_operand": nbytes, "phase": phase}), flush=True)
 
 
 def _load(pdir):
@@ -68,7 +69,7 @@ def _load(pdir):
     with open(ktr[0]) as f:
         for row in csv.DictReader(f):
             nm = row.get("Kernel_Name", "")
-            if "multi" in nm or "chain" in nm:
+            if "multi" in nm or "chain" in nm or "shift" in nm or "vec_kernel" in nm:
                 d = int(row["Dispatch_Id"])
                 dur[d] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6
                 names[d] = nm
@@ -125,10 +126,11 @@ if __name__ == "__main__":
     p = argparse.ArgumentParser()
     p.add_argument("--launches", type=int, default=2)
     p.add_argument("--mib", type=int, default=1024)
+    p.add_argument("--phase", type=int, default=0, help="byte offset of every source (4: the phased kernels)")
     p.add_argument("--parse", default="")
     p.add_argument("--out", default="")
     a = p.parse_args()
     if a.parse:
         parse(a.parse, a.out)
     else:
-        run(a.launches, a.mib)
+        run(a.launches, a.mib, a.phase)

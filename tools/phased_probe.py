@@ -19,39 +19,44 @@ import dccl_amd  # noqa: E402
 from tools import tune_lib  # noqa: E402
 from tools.bench_suite import PEAK, time_launches  # noqa: E402
 
-NVAR = 2  # the lane-exchange forms; 2-3 (unaligned loads) lost 3-8 points at every k (round 2)
+VARIANTS = (0, 1, 4)  # the lane-exchange forms; 2-3 (unaligned loads) lost 3-8 points at every k (round 2)
 
 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--walk", action="store_true", help="the walking variants (dccl_tune_phased_walk_f32_sum) instead")
+    p.add_argument("--chain", action="store_true", help="also the phased chain kernel, XCD order off / on")
     p.add_argument("--out", default="")
     a = p.parse_args()
     st = torch.cuda.current_stream().cuda_stream
     nbytes = 1 << 30
     n = nbytes // 4 - 64
     recv = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    srcs = torch.empty(7 * (nbytes + 4096), dtype=torch.uint8, device="cuda")
+    srcs = torch.empty(8 * (nbytes + 4096), dtype=torch.uint8, device="cuda")
     dccl_amd.check(dccl_amd.synth_fill(recv.data_ptr(), 7, nbytes // 4, 0, 0xDCC1, 1, st), "synth")
     rows = []
-    for k, phase in ((2, 4), (2, 12), (3, 4), (4, 4), (5, 4), (2, 4), (7, 4)):
+    if a.walk:
+        walk(a, recv, srcs, n, nbytes, st, rows)
+        return finish(a, rows)
+    for k, phase in ((1, 4), (2, 4), (3, 4), (4, 4), (5, 4), (6, 4), (7, 4), (8, 4)):
         sp = [srcs.data_ptr() + j * (nbytes + 4096) + phase for j in range(k)]
         for j, q in enumerate(sp):
             dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
         arr = (ctypes.c_void_p * k)(*sp)
-        t = {v: [] for v in range(NVAR)}
+        t = {v: [] for v in VARIANTS}
         for _ in range(a.rounds):
-            for v in range(NVAR):
+            for v in VARIANTS:
                 fn = lambda v=v: dccl_amd.check(tune_lib.lib.dccl_tune_phased_f32_sum(arr, k, recv.data_ptr(), n, v,
                                                                                      st), "phased")
                 t[v].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
-        for v in range(NVAR):
+        for v in VARIANTS:
             ms = statistics.median(t[v])
             rows.append({"k": k, "phase": phase, "variant": v, "ms": round(ms, 4),
                          "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
             print(json.dumps(rows[-1]), flush=True)
     # chain (ring order), in place: own = recv (in phase), k sources +4 B; XCD order off (0) / on (1)
-    for k in (1, 2, 3, 4, 5, 7):
+    for k in ((1, 2, 3, 4, 5, 7) if a.chain else ()):
         sp = [srcs.data_ptr() + j * (nbytes + 4096) + 4 for j in range(k)]
         arr = (ctypes.c_void_p * k)(*sp)
         t = {v: [] for v in (0, 1)}
@@ -65,9 +70,47 @@ def main():
             rows.append({"chain_k": k, "phase": 4, "xcd": v, "ms": round(ms, 4),
                          "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
             print(json.dumps(rows[-1]), flush=True)
+    finish(a, rows)
+
+
+def finish(a, rows):
     if a.out:
         with open(a.out, "w") as f:
             json.dump(rows, f, indent=1)
+
+
+def walk(a, recv, srcs, n, nbytes, st, rows):
+    """Variants 0-8 of the walking kernel (U = 1, 2, 4 tiles per wave x block order in order / range split per
+    XCD / group-interleaved), each first checked bit-exact against dccl_local_reduce_multi on a fresh copy."""
+    ref = recv.clone()
+    for k in (1, 2, 4, 7):
+        sp = [srcs.data_ptr() + j * (nbytes + 4096) + 4 for j in range(k)]
+        for j, q in enumerate(sp):
+            dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
+        arr = (ctypes.c_void_p * k)(*sp)
+        want = ref.clone()
+        dccl_amd.check(dccl_amd.local_reduce_multi(sp, want.data_ptr(), 7, n, 0, st), "multi")
+        ok = {}
+        for v in range(9):
+            got = ref.clone()
+            dccl_amd.check(tune_lib.lib.dccl_tune_phased_walk_f32_sum(arr, k, got.data_ptr(), n, v, st), "walk")
+            torch.cuda.synchronize()
+            ok[v] = bool(torch.equal(got, want))
+            del got
+        t = {v: [] for v in range(9)}
+        for _ in range(a.rounds):
+            for v in range(9):
+                fn = lambda v=v: dccl_amd.check(tune_lib.lib.dccl_tune_phased_walk_f32_sum(
+                    arr, k, recv.data_ptr(), n, v, st), "walk")
+                t[v].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+        for v in range(9):
+            ms = statistics.median(t[v])
+            rows.append({"k": k, "phase": 4, "walk_variant": v, "tiles_per_wave": 1 << (v % 3),
+                         "order": ("blocks in order", "range split per XCD", "group-interleaved")[v // 3],
+                         "bit_exact": ok[v], "ms": round(ms, 4),
+                         "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
+            print(json.dumps(rows[-1]), flush=True)
+        del want
 
 
 if __name__ == "__main__":

@@ -54,13 +54,17 @@ int dccl_tune_pipelined_f32_sum(const void* send, void* recv, size_t count, int 
 int dccl_tune_write_num_variants(void);
 int dccl_tune_write_probe(int variant, void* recv, size_t count_f32, int* block, int* unroll, int* policy,
                           void* stream);
-/* the phased k-way combine (k = 2-5, 7) in shape `variant` 0-3 (see tune_kernels.hip) */
+/* the phased k-way combine (k = 1-8) in shape `variant` 0-4 (see tune_kernels.hip) */
 int dccl_tune_phased_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
                              void* stream);
 
 /* the phased chain combine (k = 1-5, 7) with the XCD tile order on (xcd 1) or off */
 int dccl_tune_chain_phased_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
                                    int xcd, void* stream);
+
+/* the phased k-way combine (k = 1, 2, 4, 7) walking U tiles per wave: variant = 3 * order + log2(U) */
+int dccl_tune_phased_walk_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
+                                  void* stream);
 
 #ifdef __cplusplus
 }

@@ -611,17 +611,19 @@ extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t
 //   1 the same with consecutive tiles on one XCD (lane 63's extra vector and the next tile's first line
 //     then meet in one L2);
 //   2 every off-phase source read with one 16-B load at its own (unaligned) address, no lane exchange;
-//   3 = 2 with consecutive tiles on one XCD.
+//   3 = 2 with consecutive tiles on one XCD;
+//   4 the shipped shape in the group-interleaved XCD order (xcd_group_tile: 8 consecutive tiles per XCD
+//     within each group of 64 blocks, the groups in order).
 // ---------------------------------------------------------------------------------
 namespace {
 template <int K, int MODE>
 __global__ __launch_bounds__(64) void tune_phased_kernel(SendList sends, PhaseList ph, unsigned char* __restrict__ recv,
                                                          size_t head, size_t nvec, size_t tail) {
-    constexpr bool XCD = (MODE & 1) != 0, UNALIGNED = (MODE & 2) != 0;
+    constexpr bool XCD = (MODE & 1) != 0, UNALIGNED = (MODE & 2) != 0, GROUP = (MODE & 4) != 0;
     const size_t off = head * sizeof(float);
     u32x4* vr = reinterpret_cast<u32x4*>(recv + off);
     const size_t ntiles = (nvec + 63) / 64;
-    const size_t t0 = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const size_t t0 = XCD ? xcd_remap(blockIdx.x, gridDim.x) : GROUP ? xcd_group_tile(blockIdx.x, gridDim.x) : blockIdx.x;
     for (size_t t = t0; t < ntiles; t += gridDim.x) {
         const size_t v = t * 64 + threadIdx.x;
         u32x4 s[K];
@@ -662,11 +664,14 @@ int tune_phased_k(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStre
 template <int MODE>
 int tune_phased_mode(SendList sl, PhaseList ph, int k, unsigned char* r, Split sp, hipStream_t st) {
     switch (k) {
+    case 1: return tune_phased_k<1, MODE>(sl, ph, r, sp, st);
     case 2: return tune_phased_k<2, MODE>(sl, ph, r, sp, st);
     case 3: return tune_phased_k<3, MODE>(sl, ph, r, sp, st);
     case 4: return tune_phased_k<4, MODE>(sl, ph, r, sp, st);
     case 5: return tune_phased_k<5, MODE>(sl, ph, r, sp, st);
+    case 6: return tune_phased_k<6, MODE>(sl, ph, r, sp, st);
     case 7: return tune_phased_k<7, MODE>(sl, ph, r, sp, st);
+    case 8: return tune_phased_k<8, MODE>(sl, ph, r, sp, st);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
@@ -692,6 +697,7 @@ extern "C" int dccl_tune_phased_f32_sum(const void* const* sends, int nsend, voi
     case 1: return tune_phased_mode<1>(sl, ph, nsend, r, sp, st);
     case 2: return tune_phased_mode<2>(sl, ph, nsend, r, sp, st);
     case 3: return tune_phased_mode<3>(sl, ph, nsend, r, sp, st);
+    case 4: return tune_phased_mode<4>(sl, ph, nsend, r, sp, st);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
@@ -738,4 +744,139 @@ extern "C" int dccl_tune_chain_phased_f32_sum(const void* const* sends, int nsen
     auto d = static_cast<unsigned char*>(dst);
     const auto st = static_cast<hipStream_t>(stream);
     return xcd ? tune_chain_phased_x<true>(sl, ph, nsend, o, d, sp, st) : tune_chain_phased_x<false>(sl, ph, nsend, o, d, sp, st);
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning only: the phased k-way combine with U consecutive tiles per wave (dccl_tune_phased_walk_f32_sum):
+// lane 63's neighbour vector for tile c is lane 0's vector of tile c + 1 (a wave rotate), so only the
+// last tile's loads one vector past the wave's range; the line two waves share is fetched twice once per
+// U KiB instead of once per KiB.  ORDER 0: blocks in order; 1: range split per XCD (xcd_remap);
+// 2: group-interleaved (xcd_group_tile).
+// ---------------------------------------------------------------------------------
+namespace {
+template <int Q>
+__device__ __forceinline__ u32x4 shift_q(u32x4 lo, u32x4 hi, unsigned b) { return funnel16<Q>(lo, hi, b); }
+
+template <int K, int U, int ORDER>
+__global__ __launch_bounds__(64) void tune_phased_walk_kernel(SendList sends, PhaseList ph,
+                                                              unsigned char* __restrict__ recv, size_t head,
+                                                              size_t nvec, size_t tail) {
+    const size_t off = head * sizeof(float);
+    u32x4* vr = reinterpret_cast<u32x4*>(recv + off);
+    const size_t nw = (nvec + 64 * U - 1) / (64 * U);
+    const size_t b0 = ORDER == 1 ? xcd_remap(blockIdx.x, gridDim.x)
+                                 : ORDER == 2 ? xcd_group_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+    const bool last_lane = (threadIdx.x & 63) == 63;
+    for (size_t w = b0; w < nw; w += gridDim.x) {
+        u32x4 acc[U];
+#pragma unroll
+        for (int c = 0; c < U; ++c) {
+            const size_t v = (w * U + c) * 64 + threadIdx.x;
+            acc[c] = u32x4{0u, 0u, 0u, 0u};
+            if (v < nvec) acc[c] = ld16<true>(vr + v);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned p = ph.p[k];
+            const unsigned char* body = sends.p[k] + off;
+            u32x4 sv[U];
+            if (p == 0) {
+#pragma unroll
+                for (int c = 0; c < U; ++c) {
+                    const size_t v = (w * U + c) * 64 + threadIdx.x;
+                    sv[c] = u32x4{0u, 0u, 0u, 0u};
+                    if (v < nvec) sv[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(body) + v);
+                }
+            } else {
+                const u32x4* va = reinterpret_cast<const u32x4*>(body - p);
+                u32x4 lo[U];
+#pragma unroll
+                for (int c = 0; c < U; ++c) {
+                    const size_t v = (w * U + c) * 64 + threadIdx.x;
+                    lo[c] = u32x4{0u, 0u, 0u, 0u};
+                    if (v <= nvec) lo[c] = __builtin_nontemporal_load(va + v);
+                }
+                u32x4 ex = {0u, 0u, 0u, 0u};
+                const size_t vl = (w * U + U - 1) * 64 + threadIdx.x;
+                if (last_lane && vl < nvec) ex = va[vl + 1];
+                const unsigned bb = p & 3;
+#pragma unroll
+                for (int c = 0; c < U; ++c) {
+                    const u32x4 nx = c + 1 < U ? from_next_lane(lo[c + 1 < U ? c + 1 : c]) : ex;
+                    const u32x4 hi = from_next_lane_or(lo[c], nx);
+                    switch (p >> 2) {
+                    case 0: sv[c] = shift_q<0>(lo[c], hi, bb); break;
+                    case 1: sv[c] = shift_q<1>(lo[c], hi, bb); break;
+                    case 2: sv[c] = shift_q<2>(lo[c], hi, bb); break;
+                    default: sv[c] = shift_q<3>(lo[c], hi, bb); break;
+                    }
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < U; ++c) acc[c] = combine16<float, kSum>(acc[c], sv[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < U; ++c) {
+            const size_t v = (w * U + c) * 64 + threadIdx.x;
+            if (v < nvec) __builtin_nontemporal_store(acc[c], vr + v);
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (size_t j = threadIdx.x; j < head + tail; j += blockDim.x) {
+            const size_t i = j < head ? j : head + nvec * 4 + (j - head);
+            float a = ld_elem<float, true>(recv, i);
+#pragma unroll
+            for (int k = 0; k < K; ++k) a = Combine<float, kSum>::apply(a, ld_elem<float, true>(sends.p[k], i));
+            st_elem<float, true>(recv, i, a);
+        }
+    }
+}
+template <int K, int U, int ORDER>
+int tune_phased_walk_k(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStream_t st) {
+    size_t grid = ceil_div(sp.nvec, size_t(64 * U));
+    if (grid == 0) grid = 1;
+    if (grid > kMaxGrid) return DCCL_INVALID_ARGUMENT;
+    void* args[] = {&sl, &ph, &r, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&tune_phased_walk_kernel<K, U, ORDER>), grid, args, st, 64);
+}
+template <int U, int ORDER>
+int tune_phased_walk_u(SendList sl, PhaseList ph, int k, unsigned char* r, Split sp, hipStream_t st) {
+    switch (k) {
+    case 1: return tune_phased_walk_k<1, U, ORDER>(sl, ph, r, sp, st);
+    case 2: return tune_phased_walk_k<2, U, ORDER>(sl, ph, r, sp, st);
+    case 4: return tune_phased_walk_k<4, U, ORDER>(sl, ph, r, sp, st);
+    case 7: return tune_phased_walk_k<7, U, ORDER>(sl, ph, r, sp, st);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+}  // namespace
+
+// variant: U = 1 << (variant % 3) (1, 2, 4) consecutive tiles per wave, ORDER = variant / 3 (0-2).
+extern "C" int dccl_tune_phased_walk_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
+                                             void* stream) {
+    if (sends == nullptr || recv == nullptr || nsend < 1 || nsend > 8 || variant < 0 || variant > 8)
+        return DCCL_INVALID_ARGUMENT;
+    const uintptr_t ar = reinterpret_cast<uintptr_t>(recv);
+    if (ar & 3) return DCCL_INVALID_ARGUMENT;
+    SendList sl{};
+    for (int k = 0; k < nsend; ++k) {
+        if (reinterpret_cast<uintptr_t>(sends[k]) & 3) return DCCL_INVALID_ARGUMENT;
+        sl.p[k] = static_cast<const unsigned char*>(sends[k]);
+    }
+    const Split sp = split_for_vectors<float>(ar, count, 128);
+    PhaseList ph{};
+    for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(float));
+    auto r = static_cast<unsigned char*>(recv);
+    const auto st = static_cast<hipStream_t>(stream);
+    switch (variant) {
+    case 0: return tune_phased_walk_u<1, 0>(sl, ph, nsend, r, sp, st);
+    case 1: return tune_phased_walk_u<2, 0>(sl, ph, nsend, r, sp, st);
+    case 2: return tune_phased_walk_u<4, 0>(sl, ph, nsend, r, sp, st);
+    case 3: return tune_phased_walk_u<1, 1>(sl, ph, nsend, r, sp, st);
+    case 4: return tune_phased_walk_u<2, 1>(sl, ph, nsend, r, sp, st);
+    case 5: return tune_phased_walk_u<4, 1>(sl, ph, nsend, r, sp, st);
+    case 6: return tune_phased_walk_u<1, 2>(sl, ph, nsend, r, sp, st);
+    case 7: return tune_phased_walk_u<2, 2>(sl, ph, nsend, r, sp, st);
+    default: return tune_phased_walk_u<4, 2>(sl, ph, nsend, r, sp, st);
+    }
 }
