@@ -22,8 +22,8 @@ Rank 0 prints ONE JSON line:
                    on the headline's own 1 GiB operands in host memory: 1 core and every core this
                    process may use (rank 0, N=1); nproc and the CPU model are stated
 Extra keys: c3 (BASELINE C3: 4 ops x fp16/bf16/fp32/int32/int64 at 1 GiB, timed and sample-verified) and
-c4 (BASELINE C4: fp32 Sum size sweep 4 KiB - 4 GiB, per-launch duration and fraction of HBM peak), rank 0 at
-N=1; payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
+c4 (BASELINE C4: fp32 Sum size sweep 4 KiB - 4 GiB, 21 points, operand sets rotated below a 512 MiB working
+set, per-launch duration eager and graph-replayed, fraction of HBM peak), rank 0 at N=1; payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
 rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately),
 c5 (BASELINE config C5 on every run: --c5-gib GiB per operand sharded over the N GPUs, strong scaling,
 combine time and, N>1, the RCCL all-gather of the reduced shards),
@@ -359,17 +359,35 @@ def config_c3(dev, stream, nbytes: int = 1 << 30, launches: int = 10) -> list:
     return out
 
 
-def graph_us_per_launch(ps: int, pr: int, n: int, dev, per_graph: int = 200, replays: int = 10) -> float:
-    """Average duration (us) of one fp32 Sum combine of n elements when `per_graph` launches are captured in
-    one HIP graph (torch.cuda.CUDAGraph over dccl_local_reduce on the capture stream) and the graph is replayed
-    `replays` times: the device-side cost per launch without the host's issue rate."""
+def _time_pairs(pairs, n: int, stream, launches: int) -> float:
+    """Average duration (ms) of `launches` back-to-back fp32 Sum combines cycling over the (send, recv)
+    pointer pairs, HIP events on `stream`."""
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    sh = stream.cuda_stream
+    for ps, pr in pairs[:3]:
+        dccl_amd.check(dccl_amd.local_reduce(ps, pr, 7, n, 0, sh))
+    ev0.record(stream)
+    for i in range(launches):
+        ps, pr = pairs[i % len(pairs)]
+        dccl_amd.check(dccl_amd.local_reduce(ps, pr, 7, n, 0, sh))
+    ev1.record(stream)
+    ev1.synchronize()
+    return ev0.elapsed_time(ev1) / launches
+
+
+def graph_us_per_launch(pairs, n: int, dev, per_graph: int = 200, replays: int = 10) -> float:
+    """Average duration (us) of one fp32 Sum combine of n elements when `per_graph` launches (cycling over
+    the pointer pairs) are captured in one HIP graph (torch.cuda.CUDAGraph over dccl_local_reduce on the
+    capture stream) and the graph is replayed `replays` times: the device-side cost per launch without the
+    host's issue rate."""
     side = torch.cuda.Stream(dev)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(side):
-        dccl_amd.check(dccl_amd.local_reduce(ps, pr, 7, n, 0, side.cuda_stream), "warm")
+        dccl_amd.check(dccl_amd.local_reduce(pairs[0][0], pairs[0][1], 7, n, 0, side.cuda_stream), "warm")
         side.synchronize()
         with torch.cuda.graph(g, stream=side):
-            for _ in range(per_graph):
+            for i in range(per_graph):
+                ps, pr = pairs[i % len(pairs)]
                 dccl_amd.check(dccl_amd.local_reduce(ps, pr, 7, n, 0, side.cuda_stream), "capture")
     g.replay()
     torch.cuda.synchronize(dev)
@@ -385,33 +403,42 @@ def graph_us_per_launch(ps: int, pr: int, n: int, dev, per_graph: int = 200, rep
     return ms * 1e3 / (replays * per_graph)
 
 
+MALL_BYTES = 256 << 20  # MI355X Infinity Cache
+
+
 def config_c4(dev, stream) -> list:
-    """BASELINE config C4: size sweep 4 KiB - 4 GiB per operand, ncclSum fp32, pooled layout.  Per size: the
-    average duration of back-to-back launches (HIP events on the launch stream, >= ~20 ms of launches), the
-    HBM rate 3*bytes/t against the 8 TB/s roofline and the payload GiB/s; small sizes are launch-bound, so up
-    to 64 MiB the same launches are also replayed from a HIP graph (graph_us_per_launch, graph_frac)."""
+    """BASELINE config C4: 2^12 ... 2^32 bytes per operand, powers of 2 (21 points), ncclSum
+    fp32, pooled layout.  Below a 512 MiB working set the launches rotate over `sets` operand pairs spread
+    over 8 GiB, so the 256 MiB Infinity Cache does not hold the operands from one launch to the next; points
+    whose single-pair working set (3 x bytes) fits that cache are labelled `mall`.  Per size: the average
+    duration of back-to-back launches (HIP events on the launch stream, >= ~20 ms of launches), the HBM rate
+    3*bytes/t against the 8 TB/s roofline and the payload GiB/s; up to 64 MiB eager launches are
+    host-issue-bound, so the same rotation is also replayed from a HIP graph (graph_us_per_launch,
+    graph_frac)."""
     out = []
     top = 4 << 30
     pool = torch.empty(2 * top + PAIR_GAP, dtype=torch.uint8, device=dev)
     synth_into(pool[:top].view(torch.float32), top // 4, 7, 0, 30)
     synth_into(pool[top + PAIR_GAP:].view(torch.float32), top // 4, 7, 0, 31)
-    pr, ps = pool.data_ptr(), pool.data_ptr() + top + PAIR_GAP
-    nb = 4 << 10
-    while nb <= top:
+    pr0, ps0 = pool.data_ptr(), pool.data_ptr() + top + PAIR_GAP
+    for e in range(12, 33):
+        nb = 1 << e
         n = nb // 4
-        k = time_kernel(ps, pr, 7, n, 0, stream, 5)
+        sets = 1 if 2 * nb >= (512 << 20) else min(top // nb, max(2, -(-(512 << 20) // (2 * nb))))
+        stride = top // sets // 4096 * 4096 if sets > 1 else 0
+        pairs = [(ps0 + j * stride, pr0 + j * stride) for j in range(sets)]
+        k = _time_pairs(pairs, n, stream, 5)
         launches = int(min(20000, max(10, 20.0 / max(k, 1e-4))))
-        k = time_kernel(ps, pr, 7, n, 0, stream, launches)
-        row = {"bytes_per_operand": nb, "launches": launches, "us_per_launch": round(k * 1e3, 2),
-               "hbm_gb_s": round(3 * nb / (k * 1e-3) / 1e9, 1),
+        k = _time_pairs(pairs, n, stream, launches)
+        row = {"bytes_per_operand": nb, "sets": sets, "mall": 3 * nb <= MALL_BYTES, "launches": launches,
+               "us_per_launch": round(k * 1e3, 2), "hbm_gb_s": round(3 * nb / (k * 1e-3) / 1e9, 1),
                "frac": round(3 * nb / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                "payload_gib_s": round(nb / (k * 1e-3) / GIB, 2)}
-        if nb <= (64 << 20):  # eager launches are host-issue-bound here: replay them from a HIP graph too
-            g = graph_us_per_launch(ps, pr, n, dev)
+        if nb <= (64 << 20):
+            g = graph_us_per_launch(pairs, n, dev)
             row["graph_us_per_launch"] = round(g, 2)
             row["graph_frac"] = round(3 * nb / (g * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
         out.append(row)
-        nb *= 4
     del pool
     torch.cuda.empty_cache()
     return out
