@@ -28,7 +28,7 @@ if [[ -n "${KWAYW:-}" ]]; then
 fi
 if [[ -n "${PROF:-}" ]]; then
   echo "== rocprof kernel trace"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --no-cpu --no-host-staged --no-other-layout --no-pmc --c5-gib 0 > "$out/prof.log" 2>&1; rc=$?; echo "prof rc=$rc"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --no-cpu --no-host-staged --no-other-layout --no-pmc --no-configs --c5-gib 0 > "$out/prof.log" 2>&1; rc=$?; echo "prof rc=$rc"
   stop_if_fatal $rc
 fi
 echo "== done"
