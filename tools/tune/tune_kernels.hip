@@ -612,20 +612,61 @@ extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t
 //     then meet in one L2);
 //   2 every off-phase source read with one 16-B load at its own (unaligned) address, no lane exchange;
 //   3 = 2 with consecutive tiles on one XCD;
+//   8 every operand's loads issued before the first shift (ld_phased_issue / ld_phased_finish); 9 = 8 with
+//     consecutive tiles on one XCD; 16 / 24 / 25 = 0 / 8 / 9 under the k-way kernel's wave caps (multi_lds);
 //   4 the shipped shape in the group-interleaved XCD order (xcd_group_tile: 8 consecutive tiles per XCD
 //     within each group of 64 blocks, the groups in order).
 // ---------------------------------------------------------------------------------
 namespace {
+// Tuning only: ld_phased in two halves, so a kernel can issue every operand's loads before it uses any of them (one
+// wait for all of them instead of one round trip per operand): ld_phased_issue starts the loads,
+// ld_phased_finish does the lane exchange and the shift.  All 64 lanes call both (p is uniform).
+struct PhasedLoad {
+    u32x4 lo, ex;
+};
+__device__ __forceinline__ PhasedLoad ld_phased_issue(const unsigned char* body, unsigned p, size_t v, size_t nvec) {
+    // one load path for every phase (no uniform branch between two operands' loads): with p == 0, va is
+    // the body itself and vector nvec is not read
+    PhasedLoad x{{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+    const u32x4* va = reinterpret_cast<const u32x4*>(body - p);
+    if (p != 0 ? v <= nvec : v < nvec) x.lo = __builtin_nontemporal_load(va + v);  // A[nvec]: the last p bytes
+    if (p != 0 && (threadIdx.x & 63) == 63 && v < nvec) x.ex = va[v + 1];
+    return x;
+}
+__device__ __forceinline__ u32x4 ld_phased_finish(const PhasedLoad& x, unsigned p) {
+    if (p == 0) return x.lo;
+    const u32x4 hi = from_next_lane_or(x.lo, x.ex);
+    const unsigned b = p & 3;
+    switch (p >> 2) {  // uniform
+    case 0: return funnel16<0>(x.lo, hi, b);
+    case 1: return funnel16<1>(x.lo, hi, b);
+    case 2: return funnel16<2>(x.lo, hi, b);
+    default: return funnel16<3>(x.lo, hi, b);
+    }
+}
+
 template <int K, int MODE>
 __global__ __launch_bounds__(64) void tune_phased_kernel(SendList sends, PhaseList ph, unsigned char* __restrict__ recv,
                                                          size_t head, size_t nvec, size_t tail) {
-    constexpr bool XCD = (MODE & 1) != 0, UNALIGNED = (MODE & 2) != 0, GROUP = (MODE & 4) != 0;
+    constexpr bool XCD = (MODE & 1) != 0, UNALIGNED = (MODE & 2) != 0, GROUP = (MODE & 4) != 0,
+                   FIRST = (MODE & 8) != 0;  // MODE & 16: the k-way kernel's wave caps (launch side)
     const size_t off = head * sizeof(float);
     u32x4* vr = reinterpret_cast<u32x4*>(recv + off);
     const size_t ntiles = (nvec + 63) / 64;
     const size_t t0 = XCD ? xcd_remap(blockIdx.x, gridDim.x) : GROUP ? xcd_group_tile(blockIdx.x, gridDim.x) : blockIdx.x;
     for (size_t t = t0; t < ntiles; t += gridDim.x) {
         const size_t v = t * 64 + threadIdx.x;
+        if constexpr (FIRST) {  // recv, then every source's loads, then the shifts and combines
+            u32x4 acc = {0u, 0u, 0u, 0u};
+            if (v < nvec) acc = ld16<true>(vr + v);
+            PhasedLoad x[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[k] = ld_phased_issue(sends.p[k] + off, ph.p[k], v, nvec);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = combine16<float, kSum>(acc, ld_phased_finish(x[k], ph.p[k]));
+            if (v < nvec) __builtin_nontemporal_store(acc, vr + v);
+            continue;
+        }
         u32x4 s[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -659,7 +700,8 @@ int tune_phased_k(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStre
     if (grid == 0) grid = 1;
     if (grid > kMaxGrid) return DCCL_INVALID_ARGUMENT;  // one tile per block (the XCD map is over the grid)
     void* args[] = {&sl, &ph, &r, &sp.head, &sp.nvec, &sp.tail};
-    return launch(reinterpret_cast<const void*>(&tune_phased_kernel<K, MODE>), grid, args, st, 64);
+    return launch(reinterpret_cast<const void*>(&tune_phased_kernel<K, MODE>), grid, args, st, 64,
+                  (MODE & 16) ? multi_lds(K) : 0);
 }
 template <int MODE>
 int tune_phased_mode(SendList sl, PhaseList ph, int k, unsigned char* r, Split sp, hipStream_t st) {
@@ -698,6 +740,11 @@ extern "C" int dccl_tune_phased_f32_sum(const void* const* sends, int nsend, voi
     case 2: return tune_phased_mode<2>(sl, ph, nsend, r, sp, st);
     case 3: return tune_phased_mode<3>(sl, ph, nsend, r, sp, st);
     case 4: return tune_phased_mode<4>(sl, ph, nsend, r, sp, st);
+    case 8: return tune_phased_mode<8>(sl, ph, nsend, r, sp, st);
+    case 9: return tune_phased_mode<9>(sl, ph, nsend, r, sp, st);
+    case 24: return tune_phased_mode<24>(sl, ph, nsend, r, sp, st);
+    case 25: return tune_phased_mode<25>(sl, ph, nsend, r, sp, st);
+    case 16: return tune_phased_mode<16>(sl, ph, nsend, r, sp, st);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
