@@ -68,15 +68,6 @@ size_t occupancy_lds() {
     return v;
 }
 template <typename T, int OP>
-int launch_scalar(const unsigned char* s, unsigned char* r, size_t count, bool elem_aligned, hipStream_t stream) {
-    const size_t grid = ceil_div(count, size_t(kBlock) * 4);
-    void* args[] = {&s, &r, &count};
-    const void* fn = elem_aligned ? reinterpret_cast<const void*>(&reduce_scalar_kernel<T, OP, true>)
-                                  : reinterpret_cast<const void*>(&reduce_scalar_kernel<T, OP, false>);
-    return launch(fn, grid, args, stream);
-}
-
-template <typename T, int OP>
 int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream) {
     const auto s = static_cast<const unsigned char*>(send);
     const auto r = static_cast<unsigned char*>(recv);

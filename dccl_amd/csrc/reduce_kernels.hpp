@@ -252,31 +252,6 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
 }
 
 // ---------------------------------------------------------------------------------
-// Scalar fallback for operands that are not even element-aligned (!ALIGNED: byte gathers; the
-// pairwise combine's only scalar path since the shifted kernel took over different 16-B phases).
-// ALIGNED is kept for tuning comparisons.  Grid-stride, 4 independent elements per thread.
-// ---------------------------------------------------------------------------------
-template <typename T, int OP, bool ALIGNED>
-__global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(const unsigned char* __restrict__ send,
-                                                               unsigned char* __restrict__ recv,
-                                                               size_t count) {
-    const size_t stride = size_t(gridDim.x) * kBlock;
-    for (size_t i0 = size_t(blockIdx.x) * kBlock * 4 + threadIdx.x; i0 < count; i0 += stride * 4) {
-        T a[4], b[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const size_t i = i0 + u * kBlock;
-            if (i < count) { a[u] = ld_elem<T, ALIGNED>(recv, i); b[u] = ld_elem<T, ALIGNED>(send, i); }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const size_t i = i0 + u * kBlock;
-            if (i < count) st_elem<T, ALIGNED>(recv, i, Combine<T, OP>::apply(a[u], b[u]));
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------
 // A recv that is not element-aligned (e.g. fp32 at an odd byte address; the reference's host loop takes
 // it with a warning, internal_common.hpp:504-512, its CUDA kernel not at all).  gfx950 executes
 // global_load_dwordx4 / global_store_dwordx4 at any byte address (tools/unaligned_probe.hip checks every

@@ -496,7 +496,30 @@ extern "C" int dccl_tune_pipelined_f32_sum(const void* send, void* recv, size_t 
 // reduce_unaligned_kernel's shape), 8 send cached, 9 nothing non-temporal; 10-17 the walking / XCD-grouped
 // forms of 7 (tune_unaligned_walk_kernel).  Adjacent lanes' 16-B windows are disjoint and hold whole elements.
 namespace {
-typedef u32x4 u32x4_u __attribute__((aligned(1)));
+// ---------------------------------------------------------------------------------
+// Tuning only: the byte-gather kernel the misaligned-recv combine used before round 2 (!ALIGNED: byte
+// gathers, 4 independent elements per thread, grid-stride), kept as the comparison point.
+// ---------------------------------------------------------------------------------
+template <typename T, int OP, bool ALIGNED>
+__global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(const unsigned char* __restrict__ send,
+                                                               unsigned char* __restrict__ recv,
+                                                               size_t count) {
+    const size_t stride = size_t(gridDim.x) * kBlock;
+    for (size_t i0 = size_t(blockIdx.x) * kBlock * 4 + threadIdx.x; i0 < count; i0 += stride * 4) {
+        T a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t i = i0 + u * kBlock;
+            if (i < count) { a[u] = ld_elem<T, ALIGNED>(recv, i); b[u] = ld_elem<T, ALIGNED>(send, i); }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t i = i0 + u * kBlock;
+            if (i < count) st_elem<T, ALIGNED>(recv, i, Combine<T, OP>::apply(a[u], b[u]));
+        }
+    }
+}
+
 template <int P>  // policy bits as VecCfg: kNtSend | kNtRecv | kNtStore
 __global__ __launch_bounds__(64) void tune_unaligned_kernel(const unsigned char* s, unsigned char* r, size_t nvec,
                                                             size_t count) {
