@@ -25,6 +25,7 @@ VARIANTS = (0, 1, 16, 24, 25)  # the lane-exchange forms; 2-3 (unaligned loads) 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--caps", action="store_true", help="wave-cap sweep of the loads-first variants (8, 9)")
     p.add_argument("--walk", action="store_true", help="the walking variants (dccl_tune_phased_walk_f32_sum) instead")
     p.add_argument("--chain", action="store_true", help="also the phased chain kernel, XCD order off / on")
     p.add_argument("--out", default="")
@@ -39,6 +40,9 @@ def main():
     if a.walk:
         walk(a, recv, srcs, n, nbytes, st, rows)
         return finish(a, rows)
+    if a.caps:
+        caps(a, recv, srcs, n, nbytes, st, rows)
+        return finish(a, rows)
     for k, phase in ((1, 4), (2, 4), (3, 4), (4, 4), (5, 4), (6, 4), (7, 4), (8, 4)):
         sp = [srcs.data_ptr() + j * (nbytes + 4096) + phase for j in range(k)]
         for j, q in enumerate(sp):
@@ -48,7 +52,7 @@ def main():
         for _ in range(a.rounds):
             for v in VARIANTS:
                 fn = lambda v=v: dccl_amd.check(tune_lib.lib.dccl_tune_phased_f32_sum(arr, k, recv.data_ptr(), n, v,
-                                                                                     st), "phased")
+                                                                                     0, st), "phased")
                 t[v].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
         for v in VARIANTS:
             ms = statistics.median(t[v])
@@ -77,6 +81,29 @@ def finish(a, rows):
     if a.out:
         with open(a.out, "w") as f:
             json.dump(rows, f, indent=1)
+
+
+def caps(a, recv, srcs, n, nbytes, st, rows):
+    """Variants 0 (shipped, uncapped), 8 (loads first) and 9 (loads first, XCD order) under explicit wave caps
+    (unused dynamic LDS per one-wave block: 160 KiB / waves), k = 2, 4, 7, sources +4 B."""
+    configs = [(0, 0)] + [(v, w) for v in (8, 9) for w in (32, 24, 20, 16, 13, 11)]
+    for k in (2, 4, 7):
+        sp = [srcs.data_ptr() + j * (nbytes + 4096) + 4 for j in range(k)]
+        for j, q in enumerate(sp):
+            dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
+        arr = (ctypes.c_void_p * k)(*sp)
+        t = {c: [] for c in configs}
+        for _ in range(a.rounds):
+            for v, w in configs:
+                lds = 0 if w in (0, 32) else ((160 << 10) // w + 255) // 256 * 256
+                fn = lambda v=v, lds=lds: dccl_amd.check(tune_lib.lib.dccl_tune_phased_f32_sum(
+                    arr, k, recv.data_ptr(), n, v, lds, st), "phased caps")
+                t[(v, w)].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+        for v, w in configs:
+            ms = statistics.median(t[(v, w)])
+            rows.append({"k": k, "phase": 4, "variant": v, "waves": w or 32, "ms": round(ms, 4),
+                         "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
+            print(json.dumps(rows[-1]), flush=True)
 
 
 def walk(a, recv, srcs, n, nbytes, st, rows):

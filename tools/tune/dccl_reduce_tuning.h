@@ -56,7 +56,7 @@ int dccl_tune_write_probe(int variant, void* recv, size_t count_f32, int* block,
                           void* stream);
 /* the phased k-way combine (k = 1-8) in shape `variant` 0-4 (see tune_kernels.hip) */
 int dccl_tune_phased_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
-                             void* stream);
+                             size_t lds_bytes, void* stream);
 
 /* the phased chain combine (k = 1-5, 7) with the XCD tile order on (xcd 1) or off */
 int dccl_tune_chain_phased_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,

@@ -637,6 +637,7 @@ extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t
 //   3 = 2 with consecutive tiles on one XCD;
 //   8 every operand's loads issued before the first shift (ld_phased_issue / ld_phased_finish); 9 = 8 with
 //     consecutive tiles on one XCD; 16 / 24 / 25 = 0 / 8 / 9 under the k-way kernel's wave caps (multi_lds);
+//   lds_bytes != 0: that much unused dynamic LDS per one-wave block instead (an explicit wave cap).
 //   4 the shipped shape in the group-interleaved XCD order (xcd_group_tile: 8 consecutive tiles per XCD
 //     within each group of 64 blocks, the groups in order).
 // ---------------------------------------------------------------------------------
@@ -718,32 +719,33 @@ __global__ __launch_bounds__(64) void tune_phased_kernel(SendList sends, PhaseLi
     }
 }
 template <int K, int MODE>
-int tune_phased_k(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStream_t st) {
+int tune_phased_k(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStream_t st, size_t lds) {
     size_t grid = ceil_div(sp.nvec, size_t(64));
     if (grid == 0) grid = 1;
     if (grid > kMaxGrid) return DCCL_INVALID_ARGUMENT;  // one tile per block (the XCD map is over the grid)
     void* args[] = {&sl, &ph, &r, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&tune_phased_kernel<K, MODE>), grid, args, st, 64,
-                  (MODE & 16) ? multi_lds(K) : 0);
+                  lds != 0 ? lds : (MODE & 16) ? multi_lds(K) : 0);
 }
 template <int MODE>
-int tune_phased_mode(SendList sl, PhaseList ph, int k, unsigned char* r, Split sp, hipStream_t st) {
+int tune_phased_mode(SendList sl, PhaseList ph, int k, unsigned char* r, Split sp, hipStream_t st, size_t lds) {
     switch (k) {
-    case 1: return tune_phased_k<1, MODE>(sl, ph, r, sp, st);
-    case 2: return tune_phased_k<2, MODE>(sl, ph, r, sp, st);
-    case 3: return tune_phased_k<3, MODE>(sl, ph, r, sp, st);
-    case 4: return tune_phased_k<4, MODE>(sl, ph, r, sp, st);
-    case 5: return tune_phased_k<5, MODE>(sl, ph, r, sp, st);
-    case 6: return tune_phased_k<6, MODE>(sl, ph, r, sp, st);
-    case 7: return tune_phased_k<7, MODE>(sl, ph, r, sp, st);
-    case 8: return tune_phased_k<8, MODE>(sl, ph, r, sp, st);
+    case 1: return tune_phased_k<1, MODE>(sl, ph, r, sp, st, lds);
+    case 2: return tune_phased_k<2, MODE>(sl, ph, r, sp, st, lds);
+    case 3: return tune_phased_k<3, MODE>(sl, ph, r, sp, st, lds);
+    case 4: return tune_phased_k<4, MODE>(sl, ph, r, sp, st, lds);
+    case 5: return tune_phased_k<5, MODE>(sl, ph, r, sp, st, lds);
+    case 6: return tune_phased_k<6, MODE>(sl, ph, r, sp, st, lds);
+    case 7: return tune_phased_k<7, MODE>(sl, ph, r, sp, st, lds);
+    case 8: return tune_phased_k<8, MODE>(sl, ph, r, sp, st, lds);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
 }  // namespace
 
 extern "C" int dccl_tune_phased_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
-                                        void* stream) {
+                                        size_t lds_bytes, void* stream) {
+    if (lds_bytes > (64u << 10)) return DCCL_INVALID_ARGUMENT;
     if (sends == nullptr || recv == nullptr) return DCCL_INVALID_ARGUMENT;
     const uintptr_t ar = reinterpret_cast<uintptr_t>(recv);
     if (ar & 3) return DCCL_INVALID_ARGUMENT;
@@ -758,16 +760,16 @@ extern "C" int dccl_tune_phased_f32_sum(const void* const* sends, int nsend, voi
     auto r = static_cast<unsigned char*>(recv);
     const auto st = static_cast<hipStream_t>(stream);
     switch (variant) {
-    case 0: return tune_phased_mode<0>(sl, ph, nsend, r, sp, st);
-    case 1: return tune_phased_mode<1>(sl, ph, nsend, r, sp, st);
-    case 2: return tune_phased_mode<2>(sl, ph, nsend, r, sp, st);
-    case 3: return tune_phased_mode<3>(sl, ph, nsend, r, sp, st);
-    case 4: return tune_phased_mode<4>(sl, ph, nsend, r, sp, st);
-    case 8: return tune_phased_mode<8>(sl, ph, nsend, r, sp, st);
-    case 9: return tune_phased_mode<9>(sl, ph, nsend, r, sp, st);
-    case 24: return tune_phased_mode<24>(sl, ph, nsend, r, sp, st);
-    case 25: return tune_phased_mode<25>(sl, ph, nsend, r, sp, st);
-    case 16: return tune_phased_mode<16>(sl, ph, nsend, r, sp, st);
+    case 0: return tune_phased_mode<0>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 1: return tune_phased_mode<1>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 2: return tune_phased_mode<2>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 3: return tune_phased_mode<3>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 4: return tune_phased_mode<4>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 8: return tune_phased_mode<8>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 9: return tune_phased_mode<9>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 24: return tune_phased_mode<24>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 25: return tune_phased_mode<25>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 16: return tune_phased_mode<16>(sl, ph, nsend, r, sp, st, lds_bytes);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }

@@ -27,7 +27,8 @@ def _load():
                                             c_void_p]),
         "dccl_tune_chain_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_void_p, c_size_t, c_size_t,
                                             c_void_p]),
-        "dccl_tune_phased_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_void_p]),
+        "dccl_tune_phased_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int, c_size_t,
+                                             c_void_p]),
         "dccl_tune_chain_phased_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_void_p, c_size_t,
                                                    c_int, c_void_p]),
         "dccl_tune_phased_walk_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_size_t, c_int,
