@@ -19,7 +19,7 @@ import dccl_amd  # noqa: E402
 from tools import tune_lib  # noqa: E402
 from tools.bench_suite import PEAK, time_launches  # noqa: E402
 
-VARIANTS = (0, 1, 16, 24, 25)  # the lane-exchange forms; 2-3 (unaligned loads) lost 3-8 points at every k (round 2)
+VARIANTS = (0, 1, 32, 64)  # the lane-exchange forms; 2-3 (unaligned loads) lost 3-8 points at every k (round 2)
 
 
 def main():

@@ -637,6 +637,8 @@ extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t
 //   3 = 2 with consecutive tiles on one XCD;
 //   8 every operand's loads issued before the first shift (ld_phased_issue / ld_phased_finish); 9 = 8 with
 //     consecutive tiles on one XCD; 16 / 24 / 25 = 0 / 8 / 9 under the k-way kernel's wave caps (multi_lds);
+//   32: 0 with each source's first line and lane 63's neighbour vector loaded through the caches; 64: 0 with
+//     every source load cached;
 //   lds_bytes != 0: that much unused dynamic LDS per one-wave block instead (an explicit wave cap).
 //   4 the shipped shape in the group-interleaved XCD order (xcd_group_tile: 8 consecutive tiles per XCD
 //     within each group of 64 blocks, the groups in order).
@@ -669,11 +671,36 @@ __device__ __forceinline__ u32x4 ld_phased_finish(const PhasedLoad& x, unsigned 
     }
 }
 
+// ld_phased with cached loads: C = 1 only lanes 0-7 (the tile's first line, the one the previous tile's
+// lane 63 also reads) and lane 63's neighbour vector; C = 2 every load.
+template <int C>
+__device__ __forceinline__ u32x4 ld_phased_cached(const unsigned char* body, unsigned p, size_t v, size_t nvec) {
+    u32x4 lo = {0u, 0u, 0u, 0u};
+    const u32x4* va = reinterpret_cast<const u32x4*>(body - p);
+    const unsigned lane = threadIdx.x & 63;
+    if (p != 0 ? v <= nvec : v < nvec) {
+        if (C == 2 || lane < 8) lo = va[v];
+        else lo = __builtin_nontemporal_load(va + v);
+    }
+    if (p == 0) return lo;
+    u32x4 ex = {0u, 0u, 0u, 0u};
+    if (lane == 63 && v < nvec) ex = va[v + 1];
+    const u32x4 hi = from_next_lane_or(lo, ex);
+    const unsigned b = p & 3;
+    switch (p >> 2) {
+    case 0: return funnel16<0>(lo, hi, b);
+    case 1: return funnel16<1>(lo, hi, b);
+    case 2: return funnel16<2>(lo, hi, b);
+    default: return funnel16<3>(lo, hi, b);
+    }
+}
+
 template <int K, int MODE>
 __global__ __launch_bounds__(64) void tune_phased_kernel(SendList sends, PhaseList ph, unsigned char* __restrict__ recv,
                                                          size_t head, size_t nvec, size_t tail) {
     constexpr bool XCD = (MODE & 1) != 0, UNALIGNED = (MODE & 2) != 0, GROUP = (MODE & 4) != 0,
                    FIRST = (MODE & 8) != 0;  // MODE & 16: the k-way kernel's wave caps (launch side)
+    constexpr int CACHE = (MODE >> 5) & 3;  // 1: each source's first line (lanes 0-7) cached; 2: every source load cached
     const size_t off = head * sizeof(float);
     u32x4* vr = reinterpret_cast<u32x4*>(recv + off);
     const size_t ntiles = (nvec + 63) / 64;
@@ -698,7 +725,8 @@ __global__ __launch_bounds__(64) void tune_phased_kernel(SendList sends, PhaseLi
                 s[k] = u32x4{0u, 0u, 0u, 0u};
                 if (v < nvec) s[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_u*>(sends.p[k] + off) + v);
             } else {
-                s[k] = ld_phased(sends.p[k] + off, ph.p[k], v, nvec);
+                if constexpr (CACHE == 0) s[k] = ld_phased(sends.p[k] + off, ph.p[k], v, nvec);
+                else s[k] = ld_phased_cached<CACHE>(sends.p[k] + off, ph.p[k], v, nvec);
             }
         }
         if (v < nvec) {
@@ -770,6 +798,8 @@ extern "C" int dccl_tune_phased_f32_sum(const void* const* sends, int nsend, voi
     case 24: return tune_phased_mode<24>(sl, ph, nsend, r, sp, st, lds_bytes);
     case 25: return tune_phased_mode<25>(sl, ph, nsend, r, sp, st, lds_bytes);
     case 16: return tune_phased_mode<16>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 32: return tune_phased_mode<32>(sl, ph, nsend, r, sp, st, lds_bytes);
+    case 64: return tune_phased_mode<64>(sl, ph, nsend, r, sp, st, lds_bytes);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
