@@ -130,26 +130,24 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
     if (nsend == 1) return reduce_typed<T, OP>(sends[0], recv, count, stream);
     SendList sl{};
     const uintptr_t ar = reinterpret_cast<uintptr_t>(recv);
-    bool vec_ok = (ar % sizeof(T)) == 0, elem_ok = vec_ok;
+    bool vec_ok = (ar % sizeof(T)) == 0;
     for (int k = 0; k < nsend; ++k) {
         sl.p[k] = static_cast<const unsigned char*>(sends[k]);
-        const uintptr_t a = reinterpret_cast<uintptr_t>(sends[k]);
-        if (a % sizeof(T)) elem_ok = vec_ok = false;
-        if ((a ^ ar) & 15) vec_ok = false;
+        if ((reinterpret_cast<uintptr_t>(sends[k]) ^ ar) & 15) vec_ok = false;
     }
     auto r = static_cast<unsigned char*>(recv);
-    if (elem_ok && !vec_ok) {  // element-aligned sources at other 16-B phases: the phased kernel
+    if (ar % sizeof(T)) {  // recv not element-aligned: 16-B accesses at its own address, sources at any phase
+        if constexpr (sizeof(T) > 1) {
+            PhaseList ph{};
+            for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], 0);
+            return multi_unaligned_typed<T, OP>(sl, ph, nsend, r, count, stream);
+        }
+    }
+    if (!vec_ok) {  // an element-aligned recv and sources at other 16-B (or byte) phases: the phased kernel
         const Split sp = split_for_vectors<T>(ar, count, recv_align());
         PhaseList ph{};
         for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(T));
         return multi_phased_typed<T, OP>(sl, ph, nsend, r, sp, stream);
-    }
-    if (!vec_ok) {
-        const size_t grid = ceil_div(count, size_t(kBlock));
-        void* args[] = {&sl, &nsend, &r, &count};
-        const void* fn = elem_ok ? reinterpret_cast<const void*>(&reduce_multi_scalar_kernel<T, OP, true>)
-                                 : reinterpret_cast<const void*>(&reduce_multi_scalar_kernel<T, OP, false>);
-        return launch(fn, grid, args, stream);
     }
     const Split sp = split_for_vectors<T>(ar, count, recv_align());
     if (any_straddles(sl, nsend, sp.head * sizeof(T)))
@@ -216,28 +214,27 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
     if (nsend == 1 && own == dst) return reduce_typed<T, OP>(sends[0], dst, count, stream);
     SendList sl{};
     const uintptr_t ad = reinterpret_cast<uintptr_t>(dst), ao = reinterpret_cast<uintptr_t>(own);
-    bool elem_ok = ((ad | ao) % sizeof(T)) == 0, vec_ok = elem_ok && ((ad ^ ao) & 15) == 0;
+    bool vec_ok = (ad % sizeof(T)) == 0 && ((ad ^ ao) & 15) == 0;
     for (int k = 0; k < nsend; ++k) {
         sl.p[k] = static_cast<const unsigned char*>(sends[k]);
-        const uintptr_t a = reinterpret_cast<uintptr_t>(sends[k]);
-        if (a % sizeof(T)) elem_ok = vec_ok = false;
-        if ((a ^ ad) & 15) vec_ok = false;
+        if ((reinterpret_cast<uintptr_t>(sends[k]) ^ ad) & 15) vec_ok = false;
     }
     const auto o = static_cast<const unsigned char*>(own);
     auto d = static_cast<unsigned char*>(dst);
-    if (elem_ok && !vec_ok) {  // element-aligned operands at other 16-B phases than dst's: the phased kernel
+    if (ad % sizeof(T)) {  // dst not element-aligned: 16-B accesses at its own address, operands at any phase
+        if constexpr (sizeof(T) > 1) {
+            PhaseList ph{};
+            for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], 0);
+            ph.p[nsend] = phase_word(o, 0);
+            return chain_unaligned_typed<T, OP>(sl, ph, nsend, o, d, count, stream);
+        }
+    }
+    if (!vec_ok) {  // an element-aligned dst and operands at other 16-B (or byte) phases: the phased kernel
         const Split sp = split_for_vectors<T>(ad, count, recv_align());
         PhaseList ph{};
         for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(T));
         ph.p[nsend] = phase_word(o, sp.head * sizeof(T));
         return chain_phased_typed<T, OP>(sl, ph, nsend, o, d, sp, stream);
-    }
-    if (!vec_ok) {
-        const size_t grid = ceil_div(count, size_t(kBlock));
-        void* args[] = {&sl, &nsend, const_cast<const unsigned char**>(&o), &d, &count};
-        const void* fn = elem_ok ? reinterpret_cast<const void*>(&reduce_chain_scalar_kernel<T, OP, true>)
-                                 : reinterpret_cast<const void*>(&reduce_chain_scalar_kernel<T, OP, false>);
-        return launch(fn, grid, args, stream);
     }
     const Split sp = split_for_vectors<T>(ad, count, recv_align());
     if (any_straddles(sl, nsend, sp.head * sizeof(T)))

@@ -315,18 +315,6 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_multi_vec_kernel(SendList sen
     }
 }
 
-template <typename T, int OP, bool ALIGNED>
-__global__ __launch_bounds__(kBlock) void reduce_multi_scalar_kernel(SendList sends, int nsend,
-                                                                     unsigned char* __restrict__ recv,
-                                                                     size_t count) {
-    const size_t stride = size_t(gridDim.x) * kBlock;
-    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < count; i += stride) {
-        T acc = ld_elem<T, ALIGNED>(recv, i);
-        for (int k = 0; k < nsend; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, ALIGNED>(sends.p[k], i));
-        st_elem<T, ALIGNED>(recv, i, acc);
-    }
-}
-
 // ---------------------------------------------------------------------------------
 // Chain kernel: the association order of the reference's ring reduce-scatter for one chunk,
 // in one pass over all contributions:
@@ -369,32 +357,21 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sen
     }
 }
 
-template <typename T, int OP, bool ALIGNED>
-__global__ __launch_bounds__(kBlock) void reduce_chain_scalar_kernel(SendList sends, int nsend,
-                                                                     const unsigned char* own, unsigned char* dst,
-                                                                     size_t count) {
-    const size_t stride = size_t(gridDim.x) * kBlock;
-    for (size_t i = size_t(blockIdx.x) * kBlock + threadIdx.x; i < count; i += stride) {
-        T acc = ld_elem<T, ALIGNED>(sends.p[0], i);
-        for (int k = 1; k < nsend; ++k) acc = Combine<T, OP>::apply(ld_elem<T, ALIGNED>(sends.p[k], i), acc);
-        st_elem<T, ALIGNED>(dst, i, Combine<T, OP>::apply(ld_elem<T, ALIGNED>(own, i), acc));
-    }
-}
-
 // ---------------------------------------------------------------------------------
-// Phased k-way and chain kernels: element-aligned sources whose 16-B phases differ from the
-// destination's (DCCL chunks of sizes that are not a multiple of 16 B, read from peers or
-// scratchpads at other phases).  Operand j's body starts p_j bytes (ph.p[j], 0 <= p_j < 16) past
-// a 16-B boundary A_j.  An operand with p_j != 0 is read the shifted kernel's way: every lane
-// loads the ALIGNED vector A_j[v] (non-temporal), lane 63 also loads A_j[v+1] (through the
-// caches), the other lanes take it from their right-hand neighbour (ds_bpermute), and the 32
-// bytes are funnel-shifted by p_j.  An operand with p_j == 0 is a plain vector load.
+// Phased k-way and chain kernels: an element-aligned destination and operands whose 16-B phases differ
+// from it (DCCL chunks of sizes that are not a multiple of 16 B, read from peers or scratchpads at
+// other phases; operands need not even be element-aligned).  Operand j's body starts p_j bytes
+// (ph.p[j], 0 <= p_j < 16) past a 16-B boundary A_j.  An operand with p_j != 0 is read the shifted
+// kernel's way: every lane loads the ALIGNED vector A_j[v] (non-temporal), lane 63 also loads A_j[v+1]
+// (through the caches), the other lanes take it from their right-hand neighbour (DPP wave shift), and
+// the 32 bytes are funnel-shifted by p_j (v_alignbyte_b32, any byte count).  An operand with p_j == 0 is
+// a plain vector load.  The head / tail scalars read operands bytewise (any alignment).
 // Measured on MI355X (tools/bench_suite.py --parts phased, profiles/r1_s5_phased_probe.json): one
 // operand at a time with a uniform branch on its phase, and no occupancy cap, beat issuing every
 // operand's loads before the first shift (branch-free selects) and the k-way kernel's wave caps:
-// 74-79 % of HBM peak for k = 1..7 against 45-61 %.  The per-operand load -> bpermute -> shift
-// chain needs the full 32 waves per CU to hide its latency.
-// One-wave blocks and a per-tile loop uniform per wave: every lane reaches the bpermutes.
+// 74-79 % of HBM peak for k = 1..7 against 45-61 %; round 2 re-measured loads-first forms, caps and
+// tile orders.
+// One-wave blocks and a per-tile loop uniform per wave: every lane reaches the lane exchange.
 // ---------------------------------------------------------------------------------
 struct PhaseList { unsigned p[9]; };
 
@@ -472,7 +449,7 @@ __global__ __launch_bounds__(64) void reduce_multi_phased_kernel(SendList sends,
             const size_t i = j < head ? j : head + nvec * Pack<T>::N + (j - head);
             T acc = ld_elem<T, true>(recv, i);
 #pragma unroll
-            for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, true>(sends.p[k], i));
+            for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, false>(sends.p[k], i));
             st_elem<T, true>(recv, i, acc);
         }
     }
@@ -502,12 +479,75 @@ __global__ __launch_bounds__(64) void reduce_chain_phased_kernel(SendList sends,
     if (blockIdx.x == 0) {
         for (size_t j = threadIdx.x; j < head + tail; j += blockDim.x) {
             const size_t i = j < head ? j : head + nvec * Pack<T>::N + (j - head);
-            T acc = ld_elem<T, true>(sends.p[0], i);
+            T acc = ld_elem<T, false>(sends.p[0], i);
 #pragma unroll
-            for (int k = 1; k < K; ++k) acc = Combine<T, OP>::apply(ld_elem<T, true>(sends.p[k], i), acc);
-            st_elem<T, true>(dst, i, Combine<T, OP>::apply(ld_elem<T, true>(own, i), acc));
+            for (int k = 1; k < K; ++k) acc = Combine<T, OP>::apply(ld_elem<T, false>(sends.p[k], i), acc);
+            st_elem<T, true>(dst, i, Combine<T, OP>::apply(ld_elem<T, false>(own, i), acc));
         }
     }
+}
+
+// ---------------------------------------------------------------------------------
+// k-way and chain combines into a destination that is not element-aligned (reduce_unaligned_kernel's
+// scheme for K operands): lane i's window is the 16 bytes of elements [V i, V i + V) at the destination's
+// own address (one unaligned 16-B load and store, gfx950), every operand read through ld_phased at its
+// own byte phase.  Consecutive tiles on one XCD, grid a multiple of 8.  A window and the bytes lane i
+// reads for it through ld_phased belong to lane i alone, so own may alias dst.  The tail (< V elements)
+// is block 0's, element by element.
+// ---------------------------------------------------------------------------------
+template <typename T, int OP, int K>
+__global__ __launch_bounds__(64) void reduce_multi_unaligned_kernel(SendList sends, PhaseList ph,
+                                                                    unsigned char* __restrict__ recv, size_t nvec,
+                                                                    size_t count) {
+    const size_t g = gridDim.x;
+    for (size_t t = size_t(blockIdx.x % 8) * (g / 8) + blockIdx.x / 8; t * 64 < nvec; t += g) {
+        const size_t i = t * 64 + threadIdx.x;
+        u32x4 s[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k], ph.p[k], i, nvec);
+        if (i < nvec) {
+            u32x4_u* pr = reinterpret_cast<u32x4_u*>(recv + 16 * i);
+            u32x4 acc = __builtin_nontemporal_load(pr);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, s[k]);
+            __builtin_nontemporal_store(acc, pr);
+        }
+    }
+    if (blockIdx.x == 0)
+        for (size_t j = nvec * Pack<T>::N + threadIdx.x; j < count; j += 64) {
+            T acc = ld_elem<T, false>(recv, j);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, false>(sends.p[k], j));
+            st_elem<T, false>(recv, j, acc);
+        }
+}
+
+// Chain order as reduce_chain_vec_kernel; ph.p[K] is own's phase.
+template <typename T, int OP, int K>
+__global__ __launch_bounds__(64) void reduce_chain_unaligned_kernel(SendList sends, PhaseList ph,
+                                                                    const unsigned char* own, unsigned char* dst,
+                                                                    size_t nvec, size_t count) {
+    const size_t g = gridDim.x;
+    for (size_t t = size_t(blockIdx.x % 8) * (g / 8) + blockIdx.x / 8; t * 64 < nvec; t += g) {
+        const size_t i = t * 64 + threadIdx.x;
+        u32x4 s[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k], ph.p[k], i, nvec);
+        const u32x4 o = ld_phased(own, ph.p[K], i, nvec);
+        if (i < nvec) {
+            u32x4 acc = s[0];
+#pragma unroll
+            for (int k = 1; k < K; ++k) acc = combine16<T, OP>(s[k], acc);
+            __builtin_nontemporal_store(combine16<T, OP>(o, acc), reinterpret_cast<u32x4_u*>(dst + 16 * i));
+        }
+    }
+    if (blockIdx.x == 0)
+        for (size_t j = nvec * Pack<T>::N + threadIdx.x; j < count; j += 64) {
+            T acc = ld_elem<T, false>(sends.p[0], j);
+#pragma unroll
+            for (int k = 1; k < K; ++k) acc = Combine<T, OP>::apply(ld_elem<T, false>(sends.p[k], j), acc);
+            st_elem<T, false>(dst, j, Combine<T, OP>::apply(ld_elem<T, false>(own, j), acc));
+        }
 }
 
 // ---------------------------------------------------------------------------------
@@ -601,5 +641,13 @@ int chain_straddle_typed(SendList sl, int nsend, const unsigned char* own, unsig
 template <typename T, int OP>
 int chain_phased_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp,
                        hipStream_t stream);
+// k-way (2 <= nsend <= 8) and chain (1 <= nsend <= 8) combines into a destination that is not
+// element-aligned, instantiated for every (T, OP) in unaligned_multi.hip.  ph.p[k] = sends[k] & 15
+// (and ph.p[nsend] = own & 15 for the chain).
+template <typename T, int OP>
+int multi_unaligned_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, size_t count, hipStream_t stream);
+template <typename T, int OP>
+int chain_unaligned_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d,
+                          size_t count, hipStream_t stream);
 
 }  // namespace dccl_amd

@@ -1,0 +1,88 @@
+// dccl_amd/csrc/unaligned_multi.hip — the k-way and chain combines into a destination that is not
+// element-aligned (reduce_multi_unaligned_kernel / reduce_chain_unaligned_kernel in reduce_kernels.hpp).
+// Instantiated for every (T, OP) with sizeof(T) > 1 (a one-byte element is always aligned), in a
+// translation unit of its own, so the build compiles it beside local_reduce.hip.
+#include <hip/hip_runtime.h>
+
+#include "dispatch.hpp"
+#include "reduce_kernels.hpp"
+
+namespace dccl_amd {
+namespace {
+
+// A grid that is a multiple of 8 (the kernels' XCD tile map); kMaxGrid is one.
+size_t unaligned_grid(size_t nvec) {
+    const size_t g = ceil_div(ceil_div(nvec, size_t(64)), size_t(8)) * 8;
+    return g == 0 ? 8 : g;
+}
+
+template <typename T, int OP, int K>
+int launch_multi(SendList sl, PhaseList ph, unsigned char* r, size_t count, hipStream_t stream) {
+    size_t nvec = count / Pack<T>::N;
+    void* args[] = {&sl, &ph, &r, &nvec, &count};
+    return launch(reinterpret_cast<const void*>(&reduce_multi_unaligned_kernel<T, OP, K>), unaligned_grid(nvec), args,
+                  stream, 64);
+}
+
+template <typename T, int OP, int K>
+int launch_chain(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, size_t count,
+                 hipStream_t stream) {
+    size_t nvec = count / Pack<T>::N;
+    void* args[] = {&sl, &ph, &own, &d, &nvec, &count};
+    return launch(reinterpret_cast<const void*>(&reduce_chain_unaligned_kernel<T, OP, K>), unaligned_grid(nvec), args,
+                  stream, 64);
+}
+
+}  // namespace
+
+template <typename T, int OP>
+int multi_unaligned_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, size_t count, hipStream_t stream) {
+    switch (nsend) {
+    case 2: return launch_multi<T, OP, 2>(sl, ph, r, count, stream);
+    case 3: return launch_multi<T, OP, 3>(sl, ph, r, count, stream);
+    case 4: return launch_multi<T, OP, 4>(sl, ph, r, count, stream);
+    case 5: return launch_multi<T, OP, 5>(sl, ph, r, count, stream);
+    case 6: return launch_multi<T, OP, 6>(sl, ph, r, count, stream);
+    case 7: return launch_multi<T, OP, 7>(sl, ph, r, count, stream);
+    case 8: return launch_multi<T, OP, 8>(sl, ph, r, count, stream);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+
+template <typename T, int OP>
+int chain_unaligned_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d,
+                          size_t count, hipStream_t stream) {
+    switch (nsend) {
+    case 1: return launch_chain<T, OP, 1>(sl, ph, own, d, count, stream);
+    case 2: return launch_chain<T, OP, 2>(sl, ph, own, d, count, stream);
+    case 3: return launch_chain<T, OP, 3>(sl, ph, own, d, count, stream);
+    case 4: return launch_chain<T, OP, 4>(sl, ph, own, d, count, stream);
+    case 5: return launch_chain<T, OP, 5>(sl, ph, own, d, count, stream);
+    case 6: return launch_chain<T, OP, 6>(sl, ph, own, d, count, stream);
+    case 7: return launch_chain<T, OP, 7>(sl, ph, own, d, count, stream);
+    case 8: return launch_chain<T, OP, 8>(sl, ph, own, d, count, stream);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+
+#define DCCL_UNALIGNED_INST_OP(T, OP)                                                                             \
+    template int multi_unaligned_typed<T, OP>(SendList, PhaseList, int, unsigned char*, size_t, hipStream_t);      \
+    template int chain_unaligned_typed<T, OP>(SendList, PhaseList, int, const unsigned char*, unsigned char*, size_t, \
+                                              hipStream_t);
+#define DCCL_UNALIGNED_INST(T)              \
+    DCCL_UNALIGNED_INST_OP(T, kSum)         \
+    DCCL_UNALIGNED_INST_OP(T, kProd)        \
+    DCCL_UNALIGNED_INST_OP(T, kMax)         \
+    DCCL_UNALIGNED_INST_OP(T, kMin)
+DCCL_UNALIGNED_INST(int32_t)
+DCCL_UNALIGNED_INST(uint32_t)
+DCCL_UNALIGNED_INST(int64_t)
+DCCL_UNALIGNED_INST(uint64_t)
+DCCL_UNALIGNED_INST(f16_bits)
+DCCL_UNALIGNED_INST(float)
+DCCL_UNALIGNED_INST(double)
+DCCL_UNALIGNED_INST(bf16_bits)
+#undef DCCL_UNALIGNED_INST
+#undef DCCL_UNALIGNED_INST_OP
+
+}  // namespace dccl_amd

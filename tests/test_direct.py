@@ -160,6 +160,44 @@ def test_chain_mixed_phases(gpu, dt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dt", [2, 4, 6, 7, 8, 9])
+def test_chain_byte_offsets(gpu, dt):
+    """Sends and own at any byte address (phased chain kernel with byte phases) into a dst that is
+    element-aligned or not (reduce_chain_unaligned_kernel), separate and in place (own == dst at a byte
+    offset), against the ring-order oracle; nothing outside dst written."""
+    import dccl_amd
+    from tests.test_gpu_parity import rand_inputs, dev_bytes, host_of
+    from tests.test_oracle import fp_equal
+    import torch
+    rng = np.random.default_rng(1500 + dt)
+    esz = dccl_amd.size_of_type(dt)
+    per_tile = 64 * (16 // esz)
+    for k, n in ((1, 3), (2, per_tile - 1), (3, per_tile + 5), (4, 4099), (6, 2 * per_tile + 1), (8, 20001)):
+        for dst_mis in (False, True):
+            op = int(rng.integers(0, 4))
+            arrs = [rand_inputs(rng, dt, n)[0] for _ in range(k + 1)]
+            sends, own = arrs[:k], arrs[k]
+            want = chain_expected(sends, own, dt, op)
+            offs = [int(rng.integers(0, 64)) for _ in range(k + 1)]
+            offs[0] = offs[0] // esz * esz + 1
+            doff = int(rng.integers(0, 64 // esz)) * esz + (int(rng.integers(1, esz)) if dst_mis else 0)
+            dev = [dev_bytes(a, o) for a, o in zip(sends, offs)]
+            t_own, p_own = dev_bytes(own, offs[k])
+            t_dst, p_dst = dev_bytes(np.zeros_like(own), doff)
+            assert dccl_amd.local_reduce_chain([d[1] for d in dev], p_own, p_dst, dt, n, op) == 0
+            torch.cuda.synchronize()
+            assert fp_equal(host_of(t_dst, doff, own), want, dt), (op, k, n, offs, doff)
+            nb = n * esz
+            assert not t_dst[:doff].any() and not t_dst[doff + nb:].any(), (k, n, offs, doff)
+            assert host_of(t_own, offs[k], own).tobytes() == own.tobytes()
+            # in place: own == dst at a byte offset of its own
+            t_in, p_in = dev_bytes(own, doff)
+            assert dccl_amd.local_reduce_chain([d[1] for d in dev], p_in, p_in, dt, n, op) == 0
+            torch.cuda.synchronize()
+            assert fp_equal(host_of(t_in, doff, own), want, dt), (op, k, n, offs, doff, "in place")
+
+
+@pytest.mark.gpu
 def test_copy_multi(gpu):
     import torch
     import dccl_amd

@@ -298,6 +298,37 @@ def test_multi_mixed_phases(dccl, k):
             assert fp_equal(host_of(tr, roff, r), want, dt), (k, dt, n, op, offs, roff)
 
 
+@pytest.mark.parametrize("k", [2, 3, 5, 8])
+def test_multi_byte_offsets(dccl, k):
+    """Sources at any byte address (phased kernel with byte phases, sources' head / tail read bytewise) and
+    recv at any byte address (reduce_multi_unaligned_kernel when recv is not element-aligned): every dtype
+    wider than a byte, sizes around a tile, against the sequential oracle; nothing outside recv written."""
+    rng = np.random.default_rng(1300 + k)
+    for dt in [2, 3, 4, 5, 6, 7, 8, 9]:
+        esz = int(oracle.NP_DTYPES[dt]().itemsize)
+        per_tile = 64 * (16 // esz)
+        for n in (1, 16 // esz + 1, per_tile - 1, per_tile + 3, 2 * per_tile + 5, 40001):
+            for recv_mis in (False, True):
+                op = int(rng.integers(0, 4))
+                sends = [rand_inputs(rng, dt, n)[0] for _ in range(k)]
+                _, r = rand_inputs(rng, dt, n)
+                offs = [int(rng.integers(0, 64)) for _ in range(k)]
+                offs[0] = offs[0] // esz * esz + 1  # at least one source not element-aligned
+                roff = int(rng.integers(0, 64 // esz)) * esz
+                if recv_mis:
+                    roff += int(rng.integers(1, esz))
+                holders = [dev_bytes(x, o) for x, o in zip(sends, offs)]
+                tr, pr = dev_bytes(r, roff)
+                assert dccl.local_reduce_multi([h[1] for h in holders], pr, dt, n, op, 0) == 0
+                torch.cuda.synchronize()
+                want = r
+                for x in sends:
+                    want = expected(x, want, dt, op)
+                assert fp_equal(host_of(tr, roff, r), want, dt), (k, dt, n, op, offs, roff)
+                nb = n * esz
+                assert not tr[:roff].any() and not tr[roff + nb:].any(), (k, dt, n, offs, roff)
+
+
 # ----------------------------------------------------------------------------- host path
 @pytest.mark.parametrize("zero_copy", ["default", "0"])
 @pytest.mark.parametrize("pinned", ["none", "both", "send"])

@@ -4,7 +4,8 @@ and one from tools/build_ab.sh) loaded side by side (RTLD_LOCAL), timed interlea
 fp32 Sum, 1 GiB per operand:
   pairwise   aligned, send off its lines, send at another 16-B phase, send at a byte offset, recv not
              element-aligned (bench.py's pooled layout, displaced);
-  phased     k-way (k = 4) and chain (k = 7) with every source 4 B off the destination's 16-B phase;
+  phased     k-way (k = 4) and chain (k = 7) with every source 4 B off the destination's 16-B phase, and
+             with sources or the destination not element-aligned;
   misaligned the shape variants of the misaligned-recv kernel through the tuning library (--tune).
     python tools/ab_combine.py LIB_A LIB_B [--rounds 7] [--tune] [--out f.json]
 """
@@ -73,6 +74,16 @@ def main():
                   lambda lib: lib.dccl_local_reduce_multi(arr4, 4, recv0, 7, n, 0, st)))
     cases.append(("chain k=7, sources +4 B (phased)", 9,
                   lambda lib: lib.dccl_local_reduce_chain(arr7, 7, recv0, recv0, 7, n, 0, st)))
+    spb = [q - 4 + 1 for q in sp]  # sources at +1 B: not element-aligned
+    arr4b = (ctypes.c_void_p * 4)(*spb[:4])
+    arr7b = (ctypes.c_void_p * 7)(*spb[:7])
+    cases.append(("k-way k=4, sources +1 B", 6, lambda lib: lib.dccl_local_reduce_multi(arr4b, 4, recv0, 7, n, 0, st)))
+    cases.append(("k-way k=4, sources +4 B, recv +2 B", 6,
+                  lambda lib: lib.dccl_local_reduce_multi(arr4, 4, recv0 + 2, 7, n, 0, st)))
+    cases.append(("chain k=7, sources +1 B", 9,
+                  lambda lib: lib.dccl_local_reduce_chain(arr7b, 7, recv0, recv0, 7, n, 0, st)))
+    cases.append(("chain k=4, sources +4 B, own = dst +2 B", 6,
+                  lambda lib: lib.dccl_local_reduce_chain(arr4, 4, recv0 + 2, recv0 + 2, 7, n, 0, st)))
     rows = []
     if a.tune_only:
         a.tune, cases = True, []

@@ -17,7 +17,8 @@ for f in comm algorithms bootstrap dccl_api direct host_staged rccl_transport; d
   objs+=("$out/$f.o")
 done
 # the kernel translation units are reused from the normal build (their host side is launchers only)
-lr=("$root/build/obj/local_reduce.hip.o" "$root/build/obj/phased_multi.hip.o" "$root/build/obj/phased_chain.hip.o")
+lr=("$root/build/obj/local_reduce.hip.o" "$root/build/obj/phased_multi.hip.o" "$root/build/obj/phased_chain.hip.o"
+    "$root/build/obj/unaligned_multi.hip.o")
 for o in "${lr[@]}"; do [[ -f "$o" ]] || python "$root/dccl_amd/build.py" > /dev/null; done
 "$HIPCC" "${flags[@]}" -c "$root/tools/dccl_cli.cpp" -o "$out/cli.o"
 "$HIPCC" --offload-arch=gfx950 -Xarch_host "-fsanitize=$kind" "$out/cli.o" "${objs[@]}" "${lr[@]}" -o "$out/dccl_cli" -pthread -ldl
