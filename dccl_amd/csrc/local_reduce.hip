@@ -186,7 +186,7 @@ __global__ __launch_bounds__(64) void copy_multi_kernel(CopyList cl, int npairs,
     const size_t nvec = (bytes - head) / 16;
     const unsigned p = unsigned((reinterpret_cast<uintptr_t>(s) + head) & 15);  // uniform per block
     u32x4* vd = reinterpret_cast<u32x4*>(d + head);
-    for (size_t t = x; t * 64 < nvec; t += gx) {  // uniform per wave: every lane reaches the bpermutes
+    for (size_t t = x; t * 64 < nvec; t += gx) {  // uniform per wave: every lane reaches the lane exchange
         const size_t v = t * 64 + threadIdx.x;
         const u32x4 val = ld_phased(s + head, p, v, nvec);
         if (v < nvec) __builtin_nontemporal_store(val, vd + v);

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_vec_kernel(const unsigned cha
 // that is not a multiple of 16 B lands here.  recv is walked in aligned 16-B vectors from
 // recv + head; the matching send bytes start p bytes (0 < p < 16, a multiple of sizeof(T)) past
 // the 16-B boundary A.  Every lane loads the ALIGNED send vector A[v], takes A[v+1] from its
-// right-hand neighbour (ds_bpermute; lane 63 loads it itself, issued with the other loads), and
+// right-hand neighbour (DPP wave shift; lane 63 loads it itself, issued with the other loads), and
 // funnel-shifts the 32 bytes by p (v_alignbyte_b32), so every access stays a 16-B vector.
 // A[nvec] is loaded although only its first p bytes belong to send: an aligned 16-B load never
 // leaves the page of its first byte, which is send's.
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
     const size_t bid = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     const unsigned q = p >> 2, b = p & 3;
     const bool last_lane = threadIdx.x == 63;
-    for (size_t t = bid; t < ntiles; t += gridDim.x) {  // uniform per wave: every lane reaches the bpermute
+    for (size_t t = bid; t < ntiles; t += gridDim.x) {  // uniform per wave: every lane reaches the lane exchange
         const size_t v = t * 64 + threadIdx.x;
         u32x4 lo = {0u, 0u, 0u, 0u}, ex = {0u, 0u, 0u, 0u}, r = {0u, 0u, 0u, 0u};
         if (v <= nvec) lo = ld16<(POLICY & kNtSend) != 0>(va + v);
