@@ -278,7 +278,7 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_multi_vec_kernel(SendList sen
                                                                     size_t head, size_t nvec, size_t tail) {
     u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
     const size_t ntiles = (nvec + C::TILE - 1) / C::TILE;
-    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (size_t t = C::XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; t < ntiles; t += gridDim.x) {
         const size_t base = t * C::TILE + threadIdx.x;
         u32x4 r[C::UNROLL], s[K][C::UNROLL];
 #pragma unroll
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sen
     const u32x4* vo = reinterpret_cast<const u32x4*>(own + off);
     u32x4* vd = reinterpret_cast<u32x4*>(dst + off);
     const size_t ntiles = (nvec + C::TILE - 1) / C::TILE;
-    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (size_t t = C::XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; t < ntiles; t += gridDim.x) {
         const size_t i = t * C::TILE + threadIdx.x;
         if (i < nvec) {
             u32x4 s[K];

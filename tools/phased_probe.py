@@ -25,6 +25,9 @@ VARIANTS = (0, 1, 32, 64)  # the lane-exchange forms; 2-3 (unaligned loads) lost
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--straddle", action="store_true",
+                   help="in-phase sources off recv's 128-B lines: tune_multi variants 0, 8, 9, 10 under the k-way caps")
+    p.add_argument("--common-phase", action="store_true", help="--straddle: every source at the same line offset")
     p.add_argument("--caps", action="store_true", help="wave-cap sweep of the loads-first variants (8, 9)")
     p.add_argument("--walk", action="store_true", help="the walking variants (dccl_tune_phased_walk_f32_sum) instead")
     p.add_argument("--chain", action="store_true", help="also the phased chain kernel, XCD order off / on")
@@ -34,7 +37,7 @@ def main():
     nbytes = 1 << 30
     n = nbytes // 4 - 64
     recv = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    srcs = torch.empty(8 * (nbytes + 4096), dtype=torch.uint8, device="cuda")
+    srcs = torch.empty(8 * (nbytes + 4096) + 256, dtype=torch.uint8, device="cuda")
     dccl_amd.check(dccl_amd.synth_fill(recv.data_ptr(), 7, nbytes // 4, 0, 0xDCC1, 1, st), "synth")
     rows = []
     if a.walk:
@@ -42,6 +45,9 @@ def main():
         return finish(a, rows)
     if a.caps:
         caps(a, recv, srcs, n, nbytes, st, rows)
+        return finish(a, rows)
+    if a.straddle:
+        straddle(a, recv, srcs, n, nbytes, st, rows)
         return finish(a, rows)
     for k, phase in ((1, 4), (2, 4), (3, 4), (4, 4), (5, 4), (6, 4), (7, 4), (8, 4)):
         sp = [srcs.data_ptr() + j * (nbytes + 4096) + phase for j in range(k)]
@@ -81,6 +87,33 @@ def finish(a, rows):
     if a.out:
         with open(a.out, "w") as f:
             json.dump(rows, f, indent=1)
+
+
+VSTRADDLE = (0, 8, 11, 12, 13)
+
+
+def straddle(a, recv, srcs, n, nbytes, st, rows):
+    """Sources 16-B aligned but off recv's 128-B lines (+16, +48, +80 ... B), k = 1..8, the k-way kernel under
+    the shipped wave caps in four shapes: 0 all non-temporal, 8 sources cached (shipped), 9 / 10 the same
+    with each XCD's tiles one contiguous range."""
+    waves = [32, 32, 18, 13, 13, 11, 11, 10, 9]  # kMultiWaves in dccl_amd/csrc/reduce_kernels.hpp
+    for k in range(1, 9):
+        sp = [srcs.data_ptr() + j * (nbytes + 4096) + (16 if a.common_phase else 16 * (2 * j + 1)) for j in range(k)]
+        for j, q in enumerate(sp):
+            dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
+        arr = (ctypes.c_void_p * k)(*sp)
+        lds = 0 if waves[k] >= 32 else ((160 << 10) // waves[k] + 255) // 256 * 256
+        t = {v: [] for v in VSTRADDLE}
+        for _ in range(a.rounds):
+            for v in VSTRADDLE:
+                fn = lambda v=v: dccl_amd.check(tune_lib.lib.dccl_tune_multi_f32_sum(
+                    arr, k, recv.data_ptr(), n, v, lds, st), "multi straddle")
+                t[v].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+        for v in VSTRADDLE:
+            ms = statistics.median(t[v])
+            rows.append({"k": k, "source_offsets": "16" if a.common_phase else "16 (2j+1)", "multi_variant": v, "ms": round(ms, 4),
+                         "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
+            print(json.dumps(rows[-1]), flush=True)
 
 
 def caps(a, recv, srcs, n, nbytes, st, rows):

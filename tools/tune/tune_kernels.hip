@@ -166,7 +166,10 @@ extern "C" int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count
 // Tuning only: k-way fp32 Sum (dccl_local_reduce_multi's kernel) with an explicit shape.
 // Variant v: 0 = shipped (64 threads, 1 vector, all nt), 1 = 64 threads x 2 vectors,
 // 2 = 256 threads x 1 vector, 3 = only send loads nt, 4 = 64 threads x 4 vectors,
-// 5/6/7 = staged: recv + s0 first, then the other sends 1/2/3 at a time (aligned operands only); `lds_bytes` of
+// 5/6/7 = staged: recv + s0 first, then the other sends 1/2/3 at a time (aligned operands only); 8 = sources
+// through the caches (the shipped line-straddle shape), 9 / 10 = 0 / 8 with each XCD's tiles one contiguous
+// range (xcd_remap); 11 / 12 / 13 = 0 / 8 / 3 with the head scalars aligning sends[0] to its 128-B line
+// instead of recv (recv straddles its lines, the sources sharing sends[0]'s line phase do not); `lds_bytes` of
 // unused dynamic LDS per block caps the resident blocks per CU (160 KiB / lds_bytes).
 // ---------------------------------------------------------------------------------
 namespace {
@@ -223,6 +226,9 @@ int tune_multi_k(int variant, SendList sl, unsigned char* r, Split sp, hipStream
     case 5: return tune_multi_staged<K, 1>(sl, r, sp, st, lds);
     case 6: return tune_multi_staged<K, 2>(sl, r, sp, st, lds);
     case 7: return tune_multi_staged<K, 3>(sl, r, sp, st, lds);
+    case 8: return tune_multi_launch<K, VecCfg<64, 1, 6, false, 1>>(sl, r, sp, st, lds);
+    case 9: return tune_multi_launch<K, VecCfg<64, 1, 7, true, 1>>(sl, r, sp, st, lds);
+    case 10: return tune_multi_launch<K, VecCfg<64, 1, 6, true, 1>>(sl, r, sp, st, lds);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
@@ -241,7 +247,10 @@ extern "C" int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void
     }
     if (ar & 3) return DCCL_INVALID_ARGUMENT;
     if (count == 0) return DCCL_SUCCESS;
-    const Split sp = split_for_vectors<float>(ar, count, 128);  // recv line-aligned, as the shipped launch
+    // recv line-aligned, as the shipped launch; variants 11-13: sends[0] line-aligned instead (recv straddles)
+    const uintptr_t anchor = variant >= 11 ? reinterpret_cast<uintptr_t>(sends[0]) : ar;
+    const Split sp = split_for_vectors<float>(anchor, count, 128);
+    if (variant >= 11) variant = variant == 11 ? 0 : variant == 12 ? 8 : 3;
     auto r = static_cast<unsigned char*>(recv);
     const auto st = static_cast<hipStream_t>(stream);
     switch (nsend) {
