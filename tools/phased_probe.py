@@ -89,7 +89,7 @@ def finish(a, rows):
             json.dump(rows, f, indent=1)
 
 
-VSTRADDLE = (0, 8, 11, 12, 13)
+VSTRADDLE = (0, 8, 14)
 
 
 def straddle(a, recv, srcs, n, nbytes, st, rows):

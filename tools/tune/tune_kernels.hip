@@ -169,7 +169,8 @@ extern "C" int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count
 // 5/6/7 = staged: recv + s0 first, then the other sends 1/2/3 at a time (aligned operands only); 8 = sources
 // through the caches (the shipped line-straddle shape), 9 / 10 = 0 / 8 with each XCD's tiles one contiguous
 // range (xcd_remap); 11 / 12 / 13 = 0 / 8 / 3 with the head scalars aligning sends[0] to its 128-B line
-// instead of recv (recv straddles its lines, the sources sharing sends[0]'s line phase do not); `lds_bytes` of
+// instead of recv (recv straddles its lines, the sources sharing sends[0]'s line phase do not); 14 = sources
+// cached only in the tile's two partial lines (tune_multi_edge_cached_kernel); `lds_bytes` of
 // unused dynamic LDS per block caps the resident blocks per CU (160 KiB / lds_bytes).
 // ---------------------------------------------------------------------------------
 namespace {
@@ -215,6 +216,54 @@ int tune_multi_launch(SendList sl, unsigned char* r, Split sp, hipStream_t strea
     return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<float, kSum, K, C>), grid, args, stream,
                   C::BLOCK, lds);
 }
+// Line-straddling in-phase sources: only the lanes whose vectors lie in a source's first or last (partial)
+// 128-B line of the tile, the lines the neighbouring tiles share, load through the caches; the rest
+// non-temporal.  One-wave blocks, one vector per lane, recv and store non-temporal.
+template <int K>
+__global__ __launch_bounds__(64) void tune_multi_edge_cached_kernel(SendList sends, unsigned char* __restrict__ recv,
+                                                                    size_t head, size_t nvec, size_t tail) {
+    u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(float));
+    const size_t ntiles = (nvec + 63) / 64;
+    const unsigned lane = threadIdx.x & 63;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t i = t * 64 + lane;
+        u32x4 s[K];
+        u32x4 r = {0u, 0u, 0u, 0u};
+        if (i < nvec) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const u32x4* p = reinterpret_cast<const u32x4*>(sends.p[k] + head * sizeof(float)) + i;
+                const unsigned lo = unsigned(reinterpret_cast<uintptr_t>(p - lane) & 127) / 16;  // tile's line phase
+                const bool edge = lane < (8 - lo) % 8 || lane >= 64 - lo;
+                if (lo != 0 && edge) s[k] = *p;
+                else s[k] = __builtin_nontemporal_load(p);
+            }
+            r = __builtin_nontemporal_load(vr + i);
+        }
+        if (i < nvec) {
+            u32x4 acc = r;
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = combine16<float, kSum>(acc, s[k]);
+            __builtin_nontemporal_store(acc, vr + i);
+        }
+    }
+    if (blockIdx.x == 0)
+        for (size_t j = threadIdx.x; j < head + tail; j += 64) {
+            const size_t e = j < head ? j : head + nvec * 4 + (j - head);
+            float acc = ld_elem<float, true>(recv, e);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = Combine<float, kSum>::apply(acc, ld_elem<float, true>(sends.p[k], e));
+            st_elem<float, true>(recv, e, acc);
+        }
+}
+template <int K>
+int tune_multi_edge_cached(SendList sl, unsigned char* r, Split sp, hipStream_t st, size_t lds) {
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0) grid = 1;
+    void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&tune_multi_edge_cached_kernel<K>), grid, args, st, 64, lds);
+}
+
 template <int K>
 int tune_multi_k(int variant, SendList sl, unsigned char* r, Split sp, hipStream_t st, size_t lds) {
     switch (variant) {
@@ -229,6 +278,7 @@ int tune_multi_k(int variant, SendList sl, unsigned char* r, Split sp, hipStream
     case 8: return tune_multi_launch<K, VecCfg<64, 1, 6, false, 1>>(sl, r, sp, st, lds);
     case 9: return tune_multi_launch<K, VecCfg<64, 1, 7, true, 1>>(sl, r, sp, st, lds);
     case 10: return tune_multi_launch<K, VecCfg<64, 1, 6, true, 1>>(sl, r, sp, st, lds);
+    case 14: return tune_multi_edge_cached<K>(sl, r, sp, st, lds);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
