@@ -229,17 +229,22 @@ def test_all_16bit_patterns(dccl, dt):
             assert fp_equal(out, expected(s, r_all, dt, op), dt), (dt, op, hex(int(p)))
 
 
-def test_aliasing_send_is_recv(dccl):
-    rng = np.random.default_rng(5)
+@pytest.mark.parametrize("off", [0, 1, 3, 6, 16])
+def test_aliasing_send_is_recv(dccl, off):
+    """send == recv (allowed by the boundary), element-aligned or not: every kernel's lane only uses the
+    bytes of its own elements, so in-place doubling / squaring is exact across tiles and waves."""
+    rng = np.random.default_rng(5 + off)
     for dt in ALL_DTYPES:
-        s, _ = rand_inputs(rng, dt, 10007)
-        t, p = dev_bytes(s)
-        for op in OPS:
-            assert dccl.local_reduce(p, p, dt, s.size, op, 0) == 0
-            torch.cuda.synchronize()
-            got = host_of(t, 0, s)
-            assert fp_equal(got, expected(s, s, dt, op), dt)
-            s = got.copy()
+        for n in (10007, 200003):
+            s, _ = rand_inputs(rng, dt, n)
+            t, p = dev_bytes(s, off)
+            for op in OPS:
+                assert dccl.local_reduce(p, p, dt, s.size, op, 0) == 0
+                torch.cuda.synchronize()
+                got = host_of(t, off, s)
+                assert fp_equal(got, expected(s, s, dt, op), dt), (dt, n, op, off)
+                s = got.copy()
+            assert not t[:off].any() and not t[off + s.nbytes:].any()
 
 
 def test_stream_ordering(dccl):
