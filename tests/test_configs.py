@@ -9,6 +9,9 @@ C5  one 16 GiB-per-operand fp32 Sum buffer split into 1, 2, 4 and 8 contiguous 2
     slice, all 16 GiB, with oracle.synth + oracle.expected_reduce (as tests/test_synth.py checks C3);
     the 1-, 2- and 4-shard results must then equal the 8-shard result bit for bit on the device, and
     each of their shard boundaries is also compared with the oracle directly.
+Beyond one grid  17 GiB per operand (more tiles than the 2^24-block grid cap, so every kernel's grid-stride
+    loop runs): the aligned, shifted and misaligned-recv combines, the whole result checked on the device
+    against the synthetic inputs regenerated per 1 GiB slice.
 Straddle  in-phase k-way and chain sources off the destination's 128-B line grid (multi_straddle_typed,
     chain_straddle_typed; advisor r1): sources at 16-B multiples that are not 128-B multiples, the
     destination at another line offset, odd counts, k = 1..8, every dtype, against the sequential and
@@ -149,3 +152,40 @@ def test_recv_misaligned_large_against_oracle(gpu, dt, roff, soff):
     assert got.tobytes() == oracle.combine(s, r, dt, op).tobytes()
     nb = n * esz
     assert not tr[:roff].any() and not tr[roff + nb:].any()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("soff,roff", [(0, 0), (4, 0), (0, 1)], ids=["aligned", "send_phase4", "recv_plus1"])
+def test_beyond_max_grid_17gib(gpu, soff, roff):
+    """fp32 Sum over 17 GiB per operand: 2^24 one-wave blocks cover 16 GiB, so the grid-stride loop of the
+    vector kernel (aligned), the shifted kernel (send 4 B off phase) and reduce_unaligned_kernel (recv 1 B
+    off) all run a second pass.  Operands are written slice by slice from the counter-based generator
+    (dccl_synth_fill_range into an aligned slice, then a byte copy to the operand's offset); the result is
+    compared bit for bit with recv + send recomputed by torch per 1 GiB slice; the bytes around recv stay."""
+    import dccl_amd
+    total = 17 * (GIB // 4)
+    piece = GIB // 4
+    nb = 4 * total
+    send = torch.zeros(nb + 4096, dtype=torch.uint8, device="cuda")
+    recv = torch.zeros(nb + 4096, dtype=torch.uint8, device="cuda")
+    a = torch.empty(piece, dtype=torch.float32, device="cuda")
+    b = torch.empty(piece, dtype=torch.float32, device="cuda")
+    for first in range(0, total, piece):
+        m = min(piece, total - first)
+        assert dccl_amd.synth_fill_range(a.data_ptr(), 7, m, 0, SEED, 60, first) == 0
+        assert dccl_amd.synth_fill_range(b.data_ptr(), 7, m, 0, SEED, 61, first) == 0
+        send[soff + 4 * first:soff + 4 * (first + m)].copy_(a[:m].view(torch.uint8))
+        recv[roff + 4 * first:roff + 4 * (first + m)].copy_(b[:m].view(torch.uint8))
+    assert dccl_amd.local_reduce(send.data_ptr() + soff, recv.data_ptr() + roff, 7, total, 0) == 0
+    torch.cuda.synchronize()
+    got = torch.empty(piece, dtype=torch.float32, device="cuda")
+    for first in range(0, total, piece):
+        m = min(piece, total - first)
+        assert dccl_amd.synth_fill_range(a.data_ptr(), 7, m, 0, SEED, 60, first) == 0
+        assert dccl_amd.synth_fill_range(b.data_ptr(), 7, m, 0, SEED, 61, first) == 0
+        got[:m].view(torch.uint8).copy_(recv[roff + 4 * first:roff + 4 * (first + m)])
+        want = b[:m] + a[:m]
+        assert torch.equal(got[:m].view(torch.int32), want.view(torch.int32)), (soff, roff, first)
+    assert not recv[:roff].any() and not recv[roff + nb:].any()
+    del send, recv, a, b, got
+    torch.cuda.empty_cache()
