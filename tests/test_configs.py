@@ -189,3 +189,45 @@ def test_beyond_max_grid_17gib(gpu, soff, roff):
     assert not recv[:roff].any() and not recv[roff + nb:].any()
     del send, recv, a, b, got
     torch.cuda.empty_cache()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kind,soff,roff", [("multi", 0, 0), ("multi", 4, 0), ("multi", 0, 2), ("chain", 0, 0),
+                                            ("chain", 4, 0), ("chain", 0, 2)])
+def test_kway_chain_beyond_max_grid_17gib(gpu, kind, soff, roff):
+    """The k-way (k = 2) and chain (k = 2, separate dst) combines over 17 GiB per operand, past the grid cap:
+    in phase (vector kernels), sources 4 B off phase (phased kernels), destination 2 B off (unaligned
+    kernels).  Checked bit for bit per 1 GiB slice against torch on the regenerated inputs, in the
+    kernels' association order (k-way: (recv + s0) + s1; chain: own + (s1 + s0))."""
+    import dccl_amd
+    total = 17 * (GIB // 4)
+    piece = GIB // 4
+    nb = 4 * total
+    bufs = [torch.zeros(nb + 4096, dtype=torch.uint8, device="cuda") for _ in range(3)]  # s0, s1, recv / own
+    dst = torch.zeros(nb + 4096, dtype=torch.uint8, device="cuda") if kind == "chain" else None
+    offs = [soff, soff, roff if kind == "multi" else 0]
+    tmp = torch.empty(piece, dtype=torch.float32, device="cuda")
+    for first in range(0, total, piece):
+        m = min(piece, total - first)
+        for j, (buf, off) in enumerate(zip(bufs, offs)):
+            assert dccl_amd.synth_fill_range(tmp.data_ptr(), 7, m, 0, SEED, 70 + j, first) == 0
+            buf[off + 4 * first:off + 4 * (first + m)].copy_(tmp[:m].view(torch.uint8))
+    ptrs = [b.data_ptr() + o for b, o in zip(bufs, offs)]
+    if kind == "multi":
+        assert dccl_amd.local_reduce_multi(ptrs[:2], ptrs[2], 7, total, 0, 0) == 0
+        out, ooff = bufs[2], roff
+    else:
+        assert dccl_amd.local_reduce_chain(ptrs[:2], ptrs[2], dst.data_ptr() + roff, 7, total, 0) == 0
+        out, ooff = dst, roff
+    torch.cuda.synchronize()
+    v = [torch.empty(piece, dtype=torch.float32, device="cuda") for _ in range(3)]
+    for first in range(0, total, piece):
+        m = min(piece, total - first)
+        for j in range(3):
+            assert dccl_amd.synth_fill_range(v[j].data_ptr(), 7, m, 0, SEED, 70 + j, first) == 0
+        want = (v[2][:m] + v[0][:m]) + v[1][:m] if kind == "multi" else v[2][:m] + (v[1][:m] + v[0][:m])
+        tmp[:m].view(torch.uint8).copy_(out[ooff + 4 * first:ooff + 4 * (first + m)])
+        assert torch.equal(tmp[:m].view(torch.int32), want.view(torch.int32)), (kind, soff, roff, first)
+    assert not out[:ooff].any() and not out[ooff + nb:].any()
+    del bufs, dst, tmp, v, out
+    torch.cuda.empty_cache()
