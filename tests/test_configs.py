@@ -231,3 +231,27 @@ def test_kway_chain_beyond_max_grid_17gib(gpu, kind, soff, roff):
     assert not out[:ooff].any() and not out[ooff + nb:].any()
     del bufs, dst, tmp, v, out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.slow
+def test_host_staged_count_beyond_2_32(gpu):
+    """Host-resident operands (DCCL's RDMA buffers) with more than 2^32 elements: int8 Sum over 4.5 GiB of
+    pageable memory through the host-staged path (the reference caps its host scratchpad at 4 GiB and keeps
+    slice sizes in uint32, SURVEY.md A.3 #8-9), checked slice by slice against the oracle."""
+    import dccl_amd
+    n = 4 * GIB + GIB // 2  # int8: elements == bytes > 2^32
+    s = oracle.synth(n, 0, 0, SEED, 80)
+    r = oracle.synth(n, 0, 0, SEED, 81)
+    assert dccl_amd.local_reduce_host(s.ctypes.data, r.ctypes.data, 0, n, 0) == 0
+    piece = GIB // 4
+
+    def one(a):
+        b = min(n, a + piece)
+        want = oracle.synth(b - a, 0, 0, SEED, 81, a)
+        assert oracle.expected_reduce(s[a:b], want, 0, 0) == 0
+        return None if np.array_equal(r[a:b], want) else (a, b)
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        bad = [x for x in ex.map(one, range(0, n, piece)) if x is not None]
+    assert not bad, bad[:3]
+    assert np.array_equal(s[-4096:], oracle.synth(4096, 0, 0, SEED, 80, n - 4096))  # send untouched
