@@ -28,7 +28,7 @@ int launch_straddle(SendList sl, unsigned char* r, Split sp, hipStream_t stream)
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, StraddleKwayCfg>), grid, args, stream, 64,
-                  multi_lds(K));
+                  straddle_lds(K));
 }
 
 }  // namespace

@@ -567,6 +567,23 @@ inline constexpr int kChainWaves[9] = {32, 32, 24, 20, 16, 13, 11, 10, 9};
 constexpr size_t chain_lds(int k) {
     return kChainWaves[k] >= 32 ? 0 : (kLdsPerCu / kChainWaves[k] + 255) / 256 * 256;
 }
+// Caps of the line-straddling launches (in-phase sources off recv's 128-B lines, loaded through the
+// caches): swept on their own in round 2 (tools/phased_probe.py --straddle-caps, 1 GiB fp32 Sum, sources
+// at 16 (2j+1) B, profiles/r2_kway_straddle_caps.json).  The straddling loads want fewer waves than
+// line-aligned ones from k = 4 (k-way) / k = 3 (chain); past the best cap the rate falls off a cliff of
+// 5 points (k-way k = 6: 79.3 % at 10 waves, 74.1 % at 11; k = 7: 78.6 % at 9, 74.0 % at 10), so each
+// value sits inside its plateau.  Nominal counts: the LDS rounding makes 8 and 9 (and 16 and 18) the same
+// occupancy.  A/B against the k-way caps on one box (profiles/r2_kway_straddle_caps_ab.json): k-way k = 6
+// 74.1 -> 79.0 %, k = 7 73.6 -> 78.8 %, k = 8 74.8 -> 75.9 %; chain k = 3 79.6 -> 81.3 %, k = 4 77.3 -> 80.2 %
+// (k-way k = 4 keeps 13: 79.4 % against 78.9 % at 11).
+inline constexpr int kStraddleWaves[9] = {32, 32, 18, 13, 13, 11, 9, 9, 7};
+constexpr size_t straddle_lds(int k) {
+    return kStraddleWaves[k] >= 32 ? 0 : (kLdsPerCu / kStraddleWaves[k] + 255) / 256 * 256;
+}
+inline constexpr int kChainStraddleWaves[9] = {32, 32, 24, 18, 13, 13, 11, 10, 9};
+constexpr size_t chain_straddle_lds(int k) {
+    return kChainStraddleWaves[k] >= 32 ? 0 : (kLdsPerCu / kChainStraddleWaves[k] + 255) / 256 * 256;
+}
 
 constexpr size_t kMaxGrid = size_t(1) << 24;  // grid-stride beyond this (2^24 x 64 threads)
 

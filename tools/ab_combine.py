@@ -58,7 +58,7 @@ def main():
         dccl_amd.check(dccl_amd.synth_fill(base + off, 7, nbytes // 4, 0, 0xDCC1, bid, st), "synth")
     recv0, send0 = base, base + nbytes + 4096
     # phased k-way / chain: eight 1 GiB sources at +4 B, recv / own aligned
-    srcs = torch.empty(8 * (nbytes + 4096), dtype=torch.uint8, device="cuda")
+    srcs = torch.empty(8 * (nbytes + 4096) + 512, dtype=torch.uint8, device="cuda")
     sp = [srcs.data_ptr() + j * (nbytes + 4096) + 4 for j in range(8)]
     for j, q in enumerate(sp):
         dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
@@ -74,6 +74,14 @@ def main():
                   lambda lib: lib.dccl_local_reduce_multi(arr4, 4, recv0, 7, n, 0, st)))
     cases.append(("chain k=7, sources +4 B (phased)", 9,
                   lambda lib: lib.dccl_local_reduce_chain(arr7, 7, recv0, recv0, 7, n, 0, st)))
+    sps = [q - 4 + 16 * (2 * j + 1) for j, q in enumerate(sp)]  # in phase, off recv's 128-B lines
+    arrs = {k: (ctypes.c_void_p * k)(*sps[:k]) for k in (3, 4, 6, 7, 8)}
+    for k in (4, 6, 7, 8):
+        cases.append((f"k-way k={k}, sources off recv's lines (straddle)", k + 2,
+                      lambda lib, k=k: lib.dccl_local_reduce_multi(arrs[k], k, recv0, 7, n, 0, st)))
+    for k in (3, 4):
+        cases.append((f"chain k={k}, sources off recv's lines (straddle)", k + 2,
+                      lambda lib, k=k: lib.dccl_local_reduce_chain(arrs[k], k, recv0, recv0, 7, n, 0, st)))
     spb = [q - 4 + 1 for q in sp]  # sources at +1 B: not element-aligned
     arr4b = (ctypes.c_void_p * 4)(*spb[:4])
     arr7b = (ctypes.c_void_p * 7)(*spb[:7])

@@ -27,6 +27,8 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--straddle", action="store_true",
                    help="in-phase sources off recv's 128-B lines: tune_multi variants 0, 8, 9, 10 under the k-way caps")
+    p.add_argument("--straddle-caps", action="store_true",
+                   help="line-straddling sources, k = 5-8: wave-cap sweep of the shipped straddle shape (variant 8)")
     p.add_argument("--common-phase", action="store_true", help="--straddle: every source at the same line offset")
     p.add_argument("--caps", action="store_true", help="wave-cap sweep of the loads-first variants (8, 9)")
     p.add_argument("--walk", action="store_true", help="the walking variants (dccl_tune_phased_walk_f32_sum) instead")
@@ -45,6 +47,9 @@ def main():
         return finish(a, rows)
     if a.caps:
         caps(a, recv, srcs, n, nbytes, st, rows)
+        return finish(a, rows)
+    if a.straddle_caps:
+        straddle_caps(a, recv, srcs, n, nbytes, st, rows)
         return finish(a, rows)
     if a.straddle:
         straddle(a, recv, srcs, n, nbytes, st, rows)
@@ -90,6 +95,38 @@ def finish(a, rows):
 
 
 VSTRADDLE = (0, 8, 14)
+
+
+def straddle_caps(a, recv, srcs, n, nbytes, st, rows):
+    """The shipped line-straddle k-way and chain shapes (sources cached) under explicit wave caps
+    (STRADDLE_WAVES, STRADDLE_K); the chain runs in place (own = dst = recv)."""
+    ks = tuple(int(x) for x in os.environ.get("STRADDLE_K", "5,6,7,8").split(","))
+    for k in ks:
+        sp = [srcs.data_ptr() + j * (nbytes + 4096) + 16 * (2 * j + 1) for j in range(k)]
+        for j, q in enumerate(sp):
+            dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
+        arr = (ctypes.c_void_p * k)(*sp)
+        waves = tuple(int(x) for x in os.environ.get("STRADDLE_WAVES", "9,11,13,16,20,24,32").split(","))
+        t = {w: [] for w in waves}
+        for _ in range(a.rounds):
+            for w in waves:
+                lds = 0 if w >= 32 else ((160 << 10) // w + 255) // 256 * 256
+                fn = lambda lds=lds: dccl_amd.check(tune_lib.lib.dccl_tune_multi_f32_sum(
+                    arr, k, recv.data_ptr(), n, 8, lds, st), "multi straddle")
+                t[w].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+        tc = {w: [] for w in waves}
+        for _ in range(a.rounds):
+            for w in waves:
+                lds = 0 if w >= 32 else ((160 << 10) // w + 255) // 256 * 256
+                fn = lambda lds=lds: dccl_amd.check(tune_lib.lib.dccl_tune_chain_policy_f32_sum(
+                    arr, k, recv.data_ptr(), recv.data_ptr(), n, lds, 6, st), "chain straddle")
+                tc[w].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+        for w in waves:
+            for what, tt in (("multi", t), ("chain", tc)):
+                ms = statistics.median(tt[w])
+                rows.append({"what": what, "k": k, "waves": w, "ms": round(ms, 4),
+                             "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
+                print(json.dumps(rows[-1]), flush=True)
 
 
 def straddle(a, recv, srcs, n, nbytes, st, rows):

@@ -66,6 +66,10 @@ int dccl_tune_chain_phased_f32_sum(const void* const* sends, int nsend, const vo
 int dccl_tune_phased_walk_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
                                   void* stream);
 
+/* the chain kernel with cache policy 7 (all non-temporal) or 6 (sources cached) and an explicit wave cap */
+int dccl_tune_chain_policy_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
+                                   size_t lds_bytes, int policy, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -320,9 +320,9 @@ extern "C" int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void
 // cap: `lds_bytes` of unused dynamic LDS per one-wave block (0 = 32 waves per CU).
 // ---------------------------------------------------------------------------------
 namespace {
-template <int K>
+template <int K, int POLICY = 7>
 int tune_chain_k(SendList sl, const unsigned char* own, unsigned char* d, Split sp, hipStream_t st, size_t lds) {
-    using C = VecCfg<64, 1, 7, false, 1>;
+    using C = VecCfg<64, 1, POLICY, false, 1>;
     size_t grid = ceil_div(sp.nvec, C::TILE);
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
@@ -332,6 +332,14 @@ int tune_chain_k(SendList sl, const unsigned char* own, unsigned char* d, Split 
 
 extern "C" int dccl_tune_chain_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
                                        size_t lds_bytes, void* stream) {
+    return dccl_tune_chain_policy_f32_sum(sends, nsend, own, dst, count, lds_bytes, 7, stream);
+}
+
+// policy 7: every access non-temporal (the in-phase launch); 6: sources through the caches (the
+// line-straddle launch's shape).
+extern "C" int dccl_tune_chain_policy_f32_sum(const void* const* sends, int nsend, const void* own, void* dst,
+                                              size_t count, size_t lds_bytes, int policy, void* stream) {
+    if (policy != 6 && policy != 7) return DCCL_INVALID_ARGUMENT;
     if (lds_bytes > (64u << 10)) return DCCL_INVALID_ARGUMENT;
     if (nsend < 1 || nsend > 8 || sends == nullptr || own == nullptr || dst == nullptr) return DCCL_INVALID_ARGUMENT;
     SendList sl{};
@@ -347,6 +355,18 @@ extern "C" int dccl_tune_chain_f32_sum(const void* const* sends, int nsend, cons
     const auto o = static_cast<const unsigned char*>(own);
     auto d = static_cast<unsigned char*>(dst);
     const auto st = static_cast<hipStream_t>(stream);
+    if (policy == 6) {
+        switch (nsend) {
+        case 1: return tune_chain_k<1, 6>(sl, o, d, sp, st, lds_bytes);
+        case 2: return tune_chain_k<2, 6>(sl, o, d, sp, st, lds_bytes);
+        case 3: return tune_chain_k<3, 6>(sl, o, d, sp, st, lds_bytes);
+        case 4: return tune_chain_k<4, 6>(sl, o, d, sp, st, lds_bytes);
+        case 5: return tune_chain_k<5, 6>(sl, o, d, sp, st, lds_bytes);
+        case 6: return tune_chain_k<6, 6>(sl, o, d, sp, st, lds_bytes);
+        case 7: return tune_chain_k<7, 6>(sl, o, d, sp, st, lds_bytes);
+        default: return tune_chain_k<8, 6>(sl, o, d, sp, st, lds_bytes);
+        }
+    }
     switch (nsend) {
     case 1: return tune_chain_k<1>(sl, o, d, sp, st, lds_bytes);
     case 2: return tune_chain_k<2>(sl, o, d, sp, st, lds_bytes);
