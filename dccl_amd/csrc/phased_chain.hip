@@ -16,7 +16,11 @@ int launch_phased(SendList sl, PhaseList ph, const unsigned char* own, unsigned 
     size_t grid = ceil_div(sp.nvec, size_t(64));
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &ph, &own, &d, &sp.head, &sp.nvec, &sp.tail};
-    // No occupancy cap, unlike the k-way kernel (reduce_kernels.hpp, "Phased k-way and chain kernels").
+    // the per-operand form uncapped (with the XCD order up to kPhasedXcdMaxK), or the loads-first form under
+    // its own cap (kChainPhasedFirstWaves, reduce_kernels.hpp)
+    if constexpr (kChainPhasedFirstWaves[K] != 0)
+        return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K, false, true>), grid, args,
+                      stream, 64, waves_lds(kChainPhasedFirstWaves[K]));
     return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K, (K <= kPhasedXcdMaxK)>), grid, args, stream, 64);
 }
 

@@ -375,12 +375,53 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sen
 // ---------------------------------------------------------------------------------
 struct PhaseList { unsigned p[9]; };
 
+// ld_phased in two halves, so a kernel can issue every operand's loads before it uses any of them (one wait
+// for all of them instead of one round trip per operand): ld_phased_issue starts the loads,
+// ld_phased_finish does the lane exchange and the shift.  All 64 lanes call both (p is uniform).
+struct PhasedLoad {
+    u32x4 lo, ex;
+};
+__device__ __forceinline__ PhasedLoad ld_phased_issue(const unsigned char* body, unsigned p, size_t v, size_t nvec) {
+    // one load path for every phase (no uniform branch between two operands' loads): with p == 0, va is
+    // the body itself and vector nvec is not read
+    PhasedLoad x{{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+    const u32x4* va = reinterpret_cast<const u32x4*>(body - p);
+    if (p != 0 ? v <= nvec : v < nvec) x.lo = __builtin_nontemporal_load(va + v);  // A[nvec]: the last p bytes
+    if (p != 0 && (threadIdx.x & 63) == 63 && v < nvec) x.ex = va[v + 1];
+    return x;
+}
+__device__ __forceinline__ u32x4 ld_phased_finish(const PhasedLoad& x, unsigned p) {
+    if (p == 0) return x.lo;
+    const u32x4 hi = from_next_lane_or(x.lo, x.ex);
+    const unsigned b = p & 3;
+    switch (p >> 2) {  // uniform
+    case 0: return funnel16<0>(x.lo, hi, b);
+    case 1: return funnel16<1>(x.lo, hi, b);
+    case 2: return funnel16<2>(x.lo, hi, b);
+    default: return funnel16<3>(x.lo, hi, b);
+    }
+}
+
 // XCD: consecutive tiles on one XCD (xcd_remap), so the vector lane 63 reads past its tile and the
 // next tile's first line meet in one L2.  It pays while few operands share the L2.  1 GiB fp32 Sum,
 // sources 4 B off phase, on two boxes (tools/phased_probe.py, profiles/r2_phased_xcd_*.json), points of
 // HBM peak gained: k-way k = 2 +2.1..+4.0, k = 3 +2.1..+2.5, k = 4 +0.6..+1.7, k = 5 -0.2..+0.8,
 // k = 7 -2.2..-5.1; the chain kernel (in place) within 0.5 points of the same at every k.
 inline constexpr int kPhasedXcdMaxK = 4;
+// From k = 5 (k-way) / k = 4 (chain) the phased kernels take the loads-first form (every operand's loads
+// issued before the first shift, ld_phased_issue / ld_phased_finish) under a wave cap of their own
+// (0 = the per-operand form above, uncapped).  Without a cap the loads-first form loses (too many streams
+// in flight), with a cap of 11-13 waves it wins: 1 GiB fp32 Sum, sources 4 B off phase
+// (tools/phased_probe.py --prod-caps, profiles/r2_phased_first_caps.json): k-way k = 5 76.4 -> 78.8 %,
+// k = 7 77.4 -> 78.8 %, k = 8 72.7 -> 78.4 %; chain k = 4 77.7 -> 79.5 %, k = 5 77.1 -> 80.1 %, k = 7
+// 73.6 -> 78.5 %, k = 8 72.0 -> 78.1 %; A/B of the two builds on another box
+// (profiles/r2_phased_first_ab.json): k-way k = 5 76.8 -> 78.7 %, k = 8 74.1 -> 78.8 %; chain k = 4
+// 78.2 -> 79.1 %, k = 7 74.8 -> 79.0 %, k = 8 73.6 -> 79.3 %.  k = 6 stays on the per-operand form (the
+// two measurements disagree in sign, within a point), and so do k <= 4 (k-way) / k <= 3 (chain), where
+// the per-operand form with the XCD order is ahead.
+inline constexpr int kPhasedFirstWaves[9] = {0, 0, 0, 0, 0, 13, 0, 12, 11};
+inline constexpr int kChainPhasedFirstWaves[9] = {0, 0, 0, 0, 13, 13, 0, 11, 11};
+constexpr size_t waves_lds(int waves) { return waves >= 32 ? 0 : ((160u << 10) / waves + 255) / 256 * 256; }
 
 // The 16 body bytes of vector v (zero for v >= nvec) of an operand whose body starts at `body`,
 // phase p.  All 64 lanes must call it (p is uniform).
@@ -425,7 +466,7 @@ __global__ __launch_bounds__(64) void reduce_unaligned_kernel(const unsigned cha
             st_elem<T, false>(recv, j, Combine<T, OP>::apply(ld_elem<T, false>(recv, j), ld_elem<T, false>(send, j)));
 }
 
-template <typename T, int OP, int K, bool XCD>
+template <typename T, int OP, int K, bool XCD, bool FIRST = false>
 __global__ __launch_bounds__(64) void reduce_multi_phased_kernel(SendList sends, PhaseList ph,
                                                                  unsigned char* __restrict__ recv, size_t head,
                                                                  size_t nvec, size_t tail) {
@@ -434,6 +475,17 @@ __global__ __launch_bounds__(64) void reduce_multi_phased_kernel(SendList sends,
     const size_t ntiles = (nvec + 63) / 64;
     for (size_t t = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; t < ntiles; t += gridDim.x) {
         const size_t v = t * 64 + threadIdx.x;
+        if constexpr (FIRST) {  // recv, then every source's loads, then the shifts and combines
+            u32x4 acc = {0u, 0u, 0u, 0u};
+            if (v < nvec) acc = ld16<true>(vr + v);
+            PhasedLoad x[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[k] = ld_phased_issue(sends.p[k] + off, ph.p[k], v, nvec);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, ld_phased_finish(x[k], ph.p[k]));
+            if (v < nvec) __builtin_nontemporal_store(acc, vr + v);
+            continue;
+        }
         u32x4 s[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k] + off, ph.p[k], v, nvec);
@@ -456,7 +508,7 @@ __global__ __launch_bounds__(64) void reduce_multi_phased_kernel(SendList sends,
 }
 
 // Chain order as reduce_chain_vec_kernel; ph.p[K] is own's phase.
-template <typename T, int OP, int K, bool XCD>
+template <typename T, int OP, int K, bool XCD, bool FIRST = false>
 __global__ __launch_bounds__(64) void reduce_chain_phased_kernel(SendList sends, PhaseList ph,
                                                                  const unsigned char* own, unsigned char* dst,
                                                                  size_t head, size_t nvec, size_t tail) {
@@ -465,6 +517,18 @@ __global__ __launch_bounds__(64) void reduce_chain_phased_kernel(SendList sends,
     const size_t ntiles = (nvec + 63) / 64;
     for (size_t t = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; t < ntiles; t += gridDim.x) {
         const size_t v = t * 64 + threadIdx.x;
+        if constexpr (FIRST) {  // every operand's loads, then the shifts and combines in chain order
+            PhasedLoad x[K + 1];
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[k] = ld_phased_issue(sends.p[k] + off, ph.p[k], v, nvec);
+            x[K] = ld_phased_issue(own + off, ph.p[K], v, nvec);
+            u32x4 acc = ld_phased_finish(x[0], ph.p[0]);
+#pragma unroll
+            for (int k = 1; k < K; ++k) acc = combine16<T, OP>(ld_phased_finish(x[k], ph.p[k]), acc);
+            const u32x4 o = ld_phased_finish(x[K], ph.p[K]);
+            if (v < nvec) __builtin_nontemporal_store(combine16<T, OP>(o, acc), vd + v);
+            continue;
+        }
         u32x4 s[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k] + off, ph.p[k], v, nvec);

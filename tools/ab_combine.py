@@ -74,6 +74,14 @@ def main():
                   lambda lib: lib.dccl_local_reduce_multi(arr4, 4, recv0, 7, n, 0, st)))
     cases.append(("chain k=7, sources +4 B (phased)", 9,
                   lambda lib: lib.dccl_local_reduce_chain(arr7, 7, recv0, recv0, 7, n, 0, st)))
+    arrp = {k: (ctypes.c_void_p * k)(*sp[:k]) for k in (5, 6, 8)}
+    for k in (5, 6, 8):
+        cases.append((f"k-way k={k}, sources +4 B (phased)", k + 2,
+                      lambda lib, k=k: lib.dccl_local_reduce_multi(arrp[k], k, recv0, 7, n, 0, st)))
+    arr4p = (ctypes.c_void_p * 4)(*sp[:4])
+    for k, arr in ((4, arr4p), (6, arrp[6]), (8, arrp[8])):
+        cases.append((f"chain k={k}, sources +4 B (phased)", k + 2,
+                      lambda lib, k=k, arr=arr: lib.dccl_local_reduce_chain(arr, k, recv0, recv0, 7, n, 0, st)))
     sps = [q - 4 + 16 * (2 * j + 1) for j, q in enumerate(sp)]  # in phase, off recv's 128-B lines
     arrs = {k: (ctypes.c_void_p * k)(*sps[:k]) for k in (3, 4, 6, 7, 8)}
     for k in (4, 6, 7, 8):

@@ -27,6 +27,8 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--straddle", action="store_true",
                    help="in-phase sources off recv's 128-B lines: tune_multi variants 0, 8, 9, 10 under the k-way caps")
+    p.add_argument("--prod-caps", action="store_true",
+                   help="the shipped phased k-way and chain kernels: shipped form vs loads-first under wave caps")
     p.add_argument("--straddle-caps", action="store_true",
                    help="line-straddling sources, k = 5-8: wave-cap sweep of the shipped straddle shape (variant 8)")
     p.add_argument("--common-phase", action="store_true", help="--straddle: every source at the same line offset")
@@ -47,6 +49,9 @@ def main():
         return finish(a, rows)
     if a.caps:
         caps(a, recv, srcs, n, nbytes, st, rows)
+        return finish(a, rows)
+    if a.prod_caps:
+        prod_caps(a, recv, srcs, n, nbytes, st, rows)
         return finish(a, rows)
     if a.straddle_caps:
         straddle_caps(a, recv, srcs, n, nbytes, st, rows)
@@ -95,6 +100,34 @@ def finish(a, rows):
 
 
 VSTRADDLE = (0, 8, 14)
+
+
+def prod_caps(a, recv, srcs, n, nbytes, st, rows):
+    """The shipped phased kernels (dccl_tune_phased_prod_f32_sum), k-way and chain (in place), sources +4 B:
+    the shipped form (first 0, its XCD rule, no cap) against the loads-first form under wave caps PHASED_WAVES,
+    for k in PHASED_K."""
+    ws = tuple(int(x) for x in os.environ.get("PHASED_WAVES", "9,10,11,12,13,14,16").split(","))
+    for k in tuple(int(x) for x in os.environ.get("PHASED_K", "3,4,5,6,7,8").split(",")):
+        sp = [srcs.data_ptr() + j * (nbytes + 4096) + 4 for j in range(k)]
+        for j, q in enumerate(sp):
+            dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
+        arr = (ctypes.c_void_p * k)(*sp)
+        configs = [(0, 32)] + [(1, w) for w in ws]
+        for what in ("multi", "chain"):
+            own = None if what == "multi" else recv.data_ptr()
+            t = {c: [] for c in configs}
+            for _ in range(a.rounds):
+                for f, w in configs:
+                    lds = 0 if w >= 32 else ((160 << 10) // w + 255) // 256 * 256
+                    x = int(k <= 4) if f == 0 else 0
+                    fn = lambda f=f, lds=lds, x=x: dccl_amd.check(tune_lib.lib.dccl_tune_phased_prod_f32_sum(
+                        arr, k, own, recv.data_ptr(), n, f, x, lds, st), "phased prod")
+                    t[(f, w)].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+            for f, w in configs:
+                ms = statistics.median(t[(f, w)])
+                rows.append({"what": what, "k": k, "first": f, "waves": w, "ms": round(ms, 4),
+                             "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
+                print(json.dumps(rows[-1]), flush=True)
 
 
 def straddle_caps(a, recv, srcs, n, nbytes, st, rows):
@@ -156,8 +189,9 @@ def straddle(a, recv, srcs, n, nbytes, st, rows):
 def caps(a, recv, srcs, n, nbytes, st, rows):
     """Variants 0 (shipped, uncapped), 8 (loads first) and 9 (loads first, XCD order) under explicit wave caps
     (unused dynamic LDS per one-wave block: 160 KiB / waves), k = 2, 4, 7, sources +4 B."""
-    configs = [(0, 0)] + [(v, w) for v in (8, 9) for w in (32, 24, 20, 16, 13, 11)]
-    for k in (2, 4, 7):
+    ws = tuple(int(x) for x in os.environ.get("PHASED_WAVES", "32,24,20,16,13,11").split(","))
+    configs = [(0, 0)] + [(v, w) for v in (8, 9) for w in ws]
+    for k in tuple(int(x) for x in os.environ.get("PHASED_K", "2,4,7").split(",")):
         sp = [srcs.data_ptr() + j * (nbytes + 4096) + 4 for j in range(k)]
         for j, q in enumerate(sp):
             dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")

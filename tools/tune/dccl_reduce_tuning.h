@@ -70,6 +70,10 @@ int dccl_tune_phased_walk_f32_sum(const void* const* sends, int nsend, void* rec
 int dccl_tune_chain_policy_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
                                    size_t lds_bytes, int policy, void* stream);
 
+/* the shipped phased k-way (own NULL) / chain kernels: loads-first form, XCD order and wave cap chosen at run time */
+int dccl_tune_phased_prod_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
+                                  int first, int xcd, size_t lds_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

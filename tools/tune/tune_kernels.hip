@@ -723,33 +723,6 @@ extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t
 //     within each group of 64 blocks, the groups in order).
 // ---------------------------------------------------------------------------------
 namespace {
-// Tuning only: ld_phased in two halves, so a kernel can issue every operand's loads before it uses any of them (one
-// wait for all of them instead of one round trip per operand): ld_phased_issue starts the loads,
-// ld_phased_finish does the lane exchange and the shift.  All 64 lanes call both (p is uniform).
-struct PhasedLoad {
-    u32x4 lo, ex;
-};
-__device__ __forceinline__ PhasedLoad ld_phased_issue(const unsigned char* body, unsigned p, size_t v, size_t nvec) {
-    // one load path for every phase (no uniform branch between two operands' loads): with p == 0, va is
-    // the body itself and vector nvec is not read
-    PhasedLoad x{{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
-    const u32x4* va = reinterpret_cast<const u32x4*>(body - p);
-    if (p != 0 ? v <= nvec : v < nvec) x.lo = __builtin_nontemporal_load(va + v);  // A[nvec]: the last p bytes
-    if (p != 0 && (threadIdx.x & 63) == 63 && v < nvec) x.ex = va[v + 1];
-    return x;
-}
-__device__ __forceinline__ u32x4 ld_phased_finish(const PhasedLoad& x, unsigned p) {
-    if (p == 0) return x.lo;
-    const u32x4 hi = from_next_lane_or(x.lo, x.ex);
-    const unsigned b = p & 3;
-    switch (p >> 2) {  // uniform
-    case 0: return funnel16<0>(x.lo, hi, b);
-    case 1: return funnel16<1>(x.lo, hi, b);
-    case 2: return funnel16<2>(x.lo, hi, b);
-    default: return funnel16<3>(x.lo, hi, b);
-    }
-}
-
 // ld_phased with cached loads: C = 1 only lanes 0-7 (the tile's first line, the one the previous tile's
 // lane 63 also reads) and lane 63's neighbour vector; C = 2 every load.
 template <int C>
@@ -1060,4 +1033,60 @@ extern "C" int dccl_tune_phased_walk_f32_sum(const void* const* sends, int nsend
     case 7: return tune_phased_walk_u<2, 2>(sl, ph, nsend, r, sp, st);
     default: return tune_phased_walk_u<4, 2>(sl, ph, nsend, r, sp, st);
     }
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning only: the shipped phased k-way (own == nullptr, recv = dst) and chain kernels with the loads-first
+// form (first), the XCD tile order (xcd) and an explicit wave cap (lds_bytes) chosen at run time.
+// ---------------------------------------------------------------------------------
+namespace {
+template <int K, bool X, bool F>
+int tune_phased_prod_k(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, Split sp, hipStream_t st,
+                       size_t lds) {
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0) grid = 1;
+    if (own == nullptr) {
+        void* args[] = {&sl, &ph, &d, &sp.head, &sp.nvec, &sp.tail};
+        return launch(reinterpret_cast<const void*>(&reduce_multi_phased_kernel<float, kSum, K, X, F>), grid, args, st,
+                      64, lds);
+    }
+    void* args[] = {&sl, &ph, &own, &d, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<float, kSum, K, X, F>), grid, args, st, 64,
+                  lds);
+}
+template <bool X, bool F>
+int tune_phased_prod_xf(SendList sl, PhaseList ph, int k, const unsigned char* own, unsigned char* d, Split sp,
+                        hipStream_t st, size_t lds) {
+    switch (k) {
+    case 2: return tune_phased_prod_k<2, X, F>(sl, ph, own, d, sp, st, lds);
+    case 3: return tune_phased_prod_k<3, X, F>(sl, ph, own, d, sp, st, lds);
+    case 4: return tune_phased_prod_k<4, X, F>(sl, ph, own, d, sp, st, lds);
+    case 5: return tune_phased_prod_k<5, X, F>(sl, ph, own, d, sp, st, lds);
+    case 6: return tune_phased_prod_k<6, X, F>(sl, ph, own, d, sp, st, lds);
+    case 7: return tune_phased_prod_k<7, X, F>(sl, ph, own, d, sp, st, lds);
+    case 8: return tune_phased_prod_k<8, X, F>(sl, ph, own, d, sp, st, lds);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
+}  // namespace
+
+extern "C" int dccl_tune_phased_prod_f32_sum(const void* const* sends, int nsend, const void* own, void* dst,
+                                             size_t count, int first, int xcd, size_t lds_bytes, void* stream) {
+    if (sends == nullptr || dst == nullptr || nsend < 2 || nsend > 8 || lds_bytes > (64u << 10))
+        return DCCL_INVALID_ARGUMENT;
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(dst);
+    if (ad & 3) return DCCL_INVALID_ARGUMENT;
+    SendList sl{};
+    for (int k = 0; k < nsend; ++k) sl.p[k] = static_cast<const unsigned char*>(sends[k]);
+    const Split sp = split_for_vectors<float>(ad, count, 128);
+    PhaseList ph{};
+    for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(float));
+    const auto o = static_cast<const unsigned char*>(own);
+    if (o != nullptr) ph.p[nsend] = phase_word(o, sp.head * sizeof(float));
+    auto d = static_cast<unsigned char*>(dst);
+    const auto st = static_cast<hipStream_t>(stream);
+    if (xcd) return first ? tune_phased_prod_xf<true, true>(sl, ph, nsend, o, d, sp, st, lds_bytes)
+                          : tune_phased_prod_xf<true, false>(sl, ph, nsend, o, d, sp, st, lds_bytes);
+    return first ? tune_phased_prod_xf<false, true>(sl, ph, nsend, o, d, sp, st, lds_bytes)
+                 : tune_phased_prod_xf<false, false>(sl, ph, nsend, o, d, sp, st, lds_bytes);
 }
