@@ -369,8 +369,9 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sen
 // Measured on MI355X (tools/bench_suite.py --parts phased, profiles/r1_s5_phased_probe.json): one
 // operand at a time with a uniform branch on its phase, and no occupancy cap, beat issuing every
 // operand's loads before the first shift (branch-free selects) and the k-way kernel's wave caps:
-// 74-79 % of HBM peak for k = 1..7 against 45-61 %; round 2 re-measured loads-first forms, caps and
-// tile orders.
+// 74-79 % of HBM peak for k = 1..7 against 45-61 %.  Round 2: the loads-first form with the same
+// uniform-branch shifts, under caps of its own, wins from k = 5 (k-way) / k = 4 (chain); see
+// kPhasedFirstWaves below and DESIGN.md §12.
 // One-wave blocks and a per-tile loop uniform per wave: every lane reaches the lane exchange.
 // ---------------------------------------------------------------------------------
 struct PhaseList { unsigned p[9]; };
