@@ -80,7 +80,8 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
         unsigned p = unsigned(as & 15);
         void* args[] = {const_cast<unsigned char**>(&s), &p, const_cast<unsigned char**>(&r),
                         const_cast<size_t*>(&nvec), &count};
-        return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<T, OP>), grid, args, stream, 64);
+        return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<T, OP>), grid, args, stream, 64,
+                      waves_lds(kUnalignedWaves));
     }
     if (as % sizeof(T)) {  // an element-aligned recv and a send at any byte address: the shifted kernel
         const Split sp = split_for_vectors<T>(ar, count, align);

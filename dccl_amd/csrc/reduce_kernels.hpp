@@ -261,7 +261,8 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
 // reads it (aligned loads, lane exchange, funnel shift by its own phase): unaligned send loads as well
 // cost a further 7-10 points.  A 1 KiB tile spans 9 lines of recv, one shared with the next tile;
 // consecutive tiles go to one XCD (blocks are dealt round-robin over the 8 XCDs), so the shared lines meet
-// in one L2.  1 GiB fp32 Sum on MI355X, recv + 1 B: 76.4-76.7 % of HBM peak, against 74.6-74.8 % with
+// in one L2.  1 GiB fp32 Sum on MI355X, recv + 1 B: 76.4-76.7 % of HBM peak uncapped (78.4-78.8 % under the
+// kUnalignedWaves cap), against 74.6-74.8 % with
 // consecutive tiles on different XCDs and 72-73 % for a byte-gather kernel; a two-pass form writing every
 // recv vector whole from one wave reached 74-75.5 % (tools/tune/, profiles/r2_misaligned_ab.json).  The
 // tail (< V elements) is block 0's, element by element.  Kernel: after ld_phased below.
@@ -423,6 +424,9 @@ inline constexpr int kPhasedXcdMaxK = 4;
 inline constexpr int kPhasedFirstWaves[9] = {0, 0, 0, 0, 0, 13, 0, 12, 11};
 inline constexpr int kChainPhasedFirstWaves[9] = {0, 0, 0, 0, 13, 13, 0, 11, 11};
 constexpr size_t waves_lds(int waves) { return waves >= 32 ? 0 : ((160u << 10) / waves + 255) / 256 * 256; }
+// reduce_unaligned_kernel's wave cap: 1 GiB fp32 Sum, recv + 1 B, 76.7 % uncapped, 78.0 % at 26 waves,
+// 78.8 % at 24 and 22, 76.1 % at 20 (a cliff), both operand layouts (profiles/r2_misaligned_caps.json).
+inline constexpr int kUnalignedWaves = 24;
 
 // The 16 body bytes of vector v (zero for v >= nvec) of an operand whose body starts at `body`,
 // phase p.  All 64 lanes must call it (p is uniform).
@@ -694,14 +698,15 @@ int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t s
 // Element-aligned operands with different 16-B phases (or an element-aligned recv and a send at any byte
 // address, SEND_ALIGNED false): the shifted vector kernel.
 template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true>
-int launch_shift(const unsigned char* s, unsigned char* r, size_t count, hipStream_t stream, size_t align = 16) {
+int launch_shift(const unsigned char* s, unsigned char* r, size_t count, hipStream_t stream, size_t align = 16,
+                 size_t lds_bytes = 0) {
     Split sp = split_for_vectors<T>(reinterpret_cast<uintptr_t>(r), count, align);
     unsigned p = unsigned((reinterpret_cast<uintptr_t>(s) + sp.head * sizeof(T)) & 15);
     size_t grid = ceil_div(sp.nvec, size_t(64));
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&s, &r, &sp.head, &sp.nvec, &sp.tail, &p};
     return launch(reinterpret_cast<const void*>(&reduce_shift_kernel<T, OP, POLICY, XCD, TAG, SEND_ALIGNED>), grid,
-                  args, stream, 64);
+                  args, stream, 64, lds_bytes);
 }
 
 // 16-B phase of an operand whose body starts `off` bytes in (see PhaseList).

@@ -74,6 +74,9 @@ int dccl_tune_chain_policy_f32_sum(const void* const* sends, int nsend, const vo
 int dccl_tune_phased_prod_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
                                   int first, int xcd, size_t lds_bytes, void* stream);
 
+/* the shipped shifted-kernel dispatch under an explicit wave cap (lds_bytes of unused LDS per block) */
+int dccl_tune_shift_caps_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -494,7 +494,7 @@ extern "C" int dccl_tune_write_probe(int variant, void* recv, size_t count_f32, 
 // and block order.
 // ---------------------------------------------------------------------------------
 namespace {
-using ShiftFn = int (*)(const unsigned char*, unsigned char*, size_t, hipStream_t, size_t);
+using ShiftFn = int (*)(const unsigned char*, unsigned char*, size_t, hipStream_t, size_t, size_t);
 struct ShiftEntry { int policy, xcd; ShiftFn fn; };
 #define DCCL_SV(P, X) ShiftEntry{P, X, &launch_shift<float, kSum, P, X, 1>}
 const ShiftEntry kShift[] = {DCCL_SV(7, false), DCCL_SV(15, false), DCCL_SV(6, false), DCCL_SV(7, true),
@@ -513,7 +513,7 @@ extern "C" int dccl_tune_shift_f32_sum(const void* send, void* recv, size_t coun
     if (xcd) *xcd = kShift[variant].xcd;
     if (count == 0) return DCCL_SUCCESS;
     return kShift[variant].fn(static_cast<const unsigned char*>(send), static_cast<unsigned char*>(recv), count,
-                              static_cast<hipStream_t>(stream), tune_align());
+                              static_cast<hipStream_t>(stream), tune_align(), 0);
 }
 
 // ---------------------------------------------------------------------------------
@@ -701,6 +701,17 @@ extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t
     case 15: return tune_unaligned_walk<kNtStore, 1, true>(s, r, count, st);
     case 16: return tune_unaligned_walk<kNtSend | kNtRecv | kNtStore, 1, true>(s, r, count, st);
     case 17: return tune_unaligned_walk<kNtStore, 64, false>(s, r, count, st);
+    case 20: case 21: case 22: case 23: case 24: case 25: {  // the shipped kernel, capped at 26/22/20/16/13/24 waves
+        const int waves[] = {26, 22, 20, 16, 13, 24};
+        const size_t lds = ((160u << 10) / waves[variant - 20] + 255) / 256 * 256;
+        const size_t nvec = count / 4;
+        size_t grid = ceil_div(ceil_div(nvec, size_t(64)), size_t(8)) * 8;
+        unsigned p = unsigned(reinterpret_cast<uintptr_t>(send) & 15);
+        size_t cnt = count;
+        size_t nv = nvec;
+        void* args[] = {const_cast<unsigned char**>(&s), &p, const_cast<unsigned char**>(&r), &nv, &cnt};
+        return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<float, kSum>), grid, args, st, 64, lds);
+    }
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
@@ -1089,4 +1100,22 @@ extern "C" int dccl_tune_phased_prod_f32_sum(const void* const* sends, int nsend
                           : tune_phased_prod_xf<true, false>(sl, ph, nsend, o, d, sp, st, lds_bytes);
     return first ? tune_phased_prod_xf<false, true>(sl, ph, nsend, o, d, sp, st, lds_bytes)
                  : tune_phased_prod_xf<false, false>(sl, ph, nsend, o, d, sp, st, lds_bytes);
+}
+
+// Tuning only: the shipped shifted-kernel dispatch for an element-aligned recv and a send at another phase
+// (or byte offset), under a wave cap of `lds_bytes` of unused dynamic LDS per block (0 = uncapped).
+extern "C" int dccl_tune_shift_caps_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes, void* stream) {
+    const auto s = static_cast<const unsigned char*>(send);
+    const auto r = static_cast<unsigned char*>(recv);
+    const auto st = static_cast<hipStream_t>(stream);
+    const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
+    if ((ar & 3) || ((as ^ ar) & 15) == 0 || lds_bytes > (64u << 10)) return DCCL_INVALID_ARGUMENT;
+    const Split sp = split_for_vectors<float>(ar, count, 128);
+    const uintptr_t a = (as + sp.head * sizeof(float)) & ~uintptr_t(15);
+    constexpr int kP = kNtSend | kNtRecv | kNtStore, kPs = kNtRecv | kNtStore;
+    if (as & 3)
+        return (a & 127) ? launch_shift<float, kSum, kPs, false, 0, false>(s, r, count, st, 128, lds_bytes)
+                         : launch_shift<float, kSum, kP, false, 0, false>(s, r, count, st, 128, lds_bytes);
+    return (a & 127) ? launch_shift<float, kSum, kPs, false>(s, r, count, st, 128, lds_bytes)
+                     : launch_shift<float, kSum, kP, false>(s, r, count, st, 128, lds_bytes);
 }
