@@ -363,6 +363,36 @@ def test_host_staged(dccl, pinned, zero_copy, monkeypatch):
             assert s2.tobytes() == s.tobytes()
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_staged_byte_offsets(dccl, pinned):
+    """Host operands that are not element-aligned: registered (the zero-copy kernel reads them through their
+    device alias at the same byte offsets, so the shifted / misaligned-recv kernels run over PCIe) and
+    pageable (bounced into aligned staging slots); sizes on both sides of the zero-copy limit."""
+    rng = np.random.default_rng(402)
+    for dt, n in [(7, 1000), (7, (16 << 20) // 4 + 3), (8, 4099), (6, (1 << 20) + 1), (4, 3 * (16 << 20) // 8 + 7)]:
+        esz = np.dtype(oracle.NP_DTYPES[dt]).itemsize
+        for soff, roff in ((1, 0), (0, 1), (3, esz // 2 + 1)):
+            s, r = rand_inputs(rng, dt, n)
+            op = int(rng.integers(0, 4))
+            want = expected(s, r, dt, op)
+            sb = np.zeros(s.nbytes + 64, dtype=np.uint8)
+            rb = np.zeros(r.nbytes + 64, dtype=np.uint8)
+            sb[soff:soff + s.nbytes] = s.view(np.uint8)
+            rb[roff:roff + r.nbytes] = r.view(np.uint8)
+            regs = [sb, rb] if pinned else []
+            for x in regs:
+                assert dccl.register_host_memory(x.ctypes.data, x.nbytes) == 0
+            try:
+                assert dccl.local_reduce_host(sb.ctypes.data + soff, rb.ctypes.data + roff, dt, n, op) == 0
+            finally:
+                for x in regs:
+                    dccl.deregister_host_memory(x.ctypes.data)
+            got = rb[roff:roff + r.nbytes].view(r.dtype)
+            assert fp_equal(got, want, dt), (pinned, dt, n, op, soff, roff)
+            assert not rb[:roff].any() and not rb[roff + r.nbytes:].any()
+            assert sb[soff:soff + s.nbytes].tobytes() == s.tobytes()
+
+
 @pytest.mark.parametrize("threads", ["1", "3", "8"])
 def test_host_staged_copy_threads(dccl, threads, monkeypatch):
     """Pageable bounce copies split over DCCL_HOST_COPY_THREADS threads: odd byte counts, every slice
