@@ -153,16 +153,7 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
     const Split sp = split_for_vectors<T>(ar, count, recv_align());
     if (any_straddles(sl, nsend, sp.head * sizeof(T)))
         return multi_straddle_typed<T, OP>(sl, nsend, r, sp, stream);
-    switch (nsend) {
-    case 2: return launch_multi_vec<T, OP, 2>(sl, r, sp, stream);
-    case 3: return launch_multi_vec<T, OP, 3>(sl, r, sp, stream);
-    case 4: return launch_multi_vec<T, OP, 4>(sl, r, sp, stream);
-    case 5: return launch_multi_vec<T, OP, 5>(sl, r, sp, stream);
-    case 6: return launch_multi_vec<T, OP, 6>(sl, r, sp, stream);
-    case 7: return launch_multi_vec<T, OP, 7>(sl, r, sp, stream);
-    case 8: return launch_multi_vec<T, OP, 8>(sl, r, sp, stream);
-    default: return DCCL_INVALID_ARGUMENT;
-    }
+    return with_k<2, 8>(nsend, [&](auto K) { return launch_multi_vec<T, OP, K.value>(sl, r, sp, stream); });
 }
 
 // ---------------------------------------------------------------------------------
@@ -240,17 +231,7 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
     const Split sp = split_for_vectors<T>(ad, count, recv_align());
     if (any_straddles(sl, nsend, sp.head * sizeof(T)))
         return chain_straddle_typed<T, OP>(sl, nsend, o, d, sp, stream);
-    switch (nsend) {
-    case 1: return launch_chain_vec<T, OP, 1>(sl, o, d, sp, stream);
-    case 2: return launch_chain_vec<T, OP, 2>(sl, o, d, sp, stream);
-    case 3: return launch_chain_vec<T, OP, 3>(sl, o, d, sp, stream);
-    case 4: return launch_chain_vec<T, OP, 4>(sl, o, d, sp, stream);
-    case 5: return launch_chain_vec<T, OP, 5>(sl, o, d, sp, stream);
-    case 6: return launch_chain_vec<T, OP, 6>(sl, o, d, sp, stream);
-    case 7: return launch_chain_vec<T, OP, 7>(sl, o, d, sp, stream);
-    case 8: return launch_chain_vec<T, OP, 8>(sl, o, d, sp, stream);
-    default: return DCCL_INVALID_ARGUMENT;
-    }
+    return with_k<1, 8>(nsend, [&](auto K) { return launch_chain_vec<T, OP, K.value>(sl, o, d, sp, stream); });
 }
 
 struct ReduceChainFn {

@@ -40,32 +40,12 @@ int launch_straddle(SendList sl, const unsigned char* own, unsigned char* d, Spl
 
 template <typename T, int OP>
 int chain_phased_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream) {
-    switch (nsend) {
-    case 1: return launch_phased<T, OP, 1>(sl, ph, own, d, sp, stream);
-    case 2: return launch_phased<T, OP, 2>(sl, ph, own, d, sp, stream);
-    case 3: return launch_phased<T, OP, 3>(sl, ph, own, d, sp, stream);
-    case 4: return launch_phased<T, OP, 4>(sl, ph, own, d, sp, stream);
-    case 5: return launch_phased<T, OP, 5>(sl, ph, own, d, sp, stream);
-    case 6: return launch_phased<T, OP, 6>(sl, ph, own, d, sp, stream);
-    case 7: return launch_phased<T, OP, 7>(sl, ph, own, d, sp, stream);
-    case 8: return launch_phased<T, OP, 8>(sl, ph, own, d, sp, stream);
-    default: return DCCL_INVALID_ARGUMENT;
-    }
+    return with_k<1, 8>(nsend, [&](auto K) { return launch_phased<T, OP, K.value>(sl, ph, own, d, sp, stream); });
 }
 
 template <typename T, int OP>
 int chain_straddle_typed(SendList sl, int nsend, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream) {
-    switch (nsend) {
-    case 1: return launch_straddle<T, OP, 1>(sl, own, d, sp, stream);
-    case 2: return launch_straddle<T, OP, 2>(sl, own, d, sp, stream);
-    case 3: return launch_straddle<T, OP, 3>(sl, own, d, sp, stream);
-    case 4: return launch_straddle<T, OP, 4>(sl, own, d, sp, stream);
-    case 5: return launch_straddle<T, OP, 5>(sl, own, d, sp, stream);
-    case 6: return launch_straddle<T, OP, 6>(sl, own, d, sp, stream);
-    case 7: return launch_straddle<T, OP, 7>(sl, own, d, sp, stream);
-    case 8: return launch_straddle<T, OP, 8>(sl, own, d, sp, stream);
-    default: return DCCL_INVALID_ARGUMENT;
-    }
+    return with_k<1, 8>(nsend, [&](auto K) { return launch_straddle<T, OP, K.value>(sl, own, d, sp, stream); });
 }
 
 #define DCCL_PHASED_INST(T)                                                       \

@@ -39,30 +39,12 @@ int launch_straddle(SendList sl, unsigned char* r, Split sp, hipStream_t stream)
 
 template <typename T, int OP>
 int multi_phased_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, Split sp, hipStream_t stream) {
-    switch (nsend) {
-    case 2: return launch_phased<T, OP, 2>(sl, ph, r, sp, stream);
-    case 3: return launch_phased<T, OP, 3>(sl, ph, r, sp, stream);
-    case 4: return launch_phased<T, OP, 4>(sl, ph, r, sp, stream);
-    case 5: return launch_phased<T, OP, 5>(sl, ph, r, sp, stream);
-    case 6: return launch_phased<T, OP, 6>(sl, ph, r, sp, stream);
-    case 7: return launch_phased<T, OP, 7>(sl, ph, r, sp, stream);
-    case 8: return launch_phased<T, OP, 8>(sl, ph, r, sp, stream);
-    default: return DCCL_INVALID_ARGUMENT;
-    }
+    return with_k<2, 8>(nsend, [&](auto K) { return launch_phased<T, OP, K.value>(sl, ph, r, sp, stream); });
 }
 
 template <typename T, int OP>
 int multi_straddle_typed(SendList sl, int nsend, unsigned char* r, Split sp, hipStream_t stream) {
-    switch (nsend) {
-    case 2: return launch_straddle<T, OP, 2>(sl, r, sp, stream);
-    case 3: return launch_straddle<T, OP, 3>(sl, r, sp, stream);
-    case 4: return launch_straddle<T, OP, 4>(sl, r, sp, stream);
-    case 5: return launch_straddle<T, OP, 5>(sl, r, sp, stream);
-    case 6: return launch_straddle<T, OP, 6>(sl, r, sp, stream);
-    case 7: return launch_straddle<T, OP, 7>(sl, r, sp, stream);
-    case 8: return launch_straddle<T, OP, 8>(sl, r, sp, stream);
-    default: return DCCL_INVALID_ARGUMENT;
-    }
+    return with_k<2, 8>(nsend, [&](auto K) { return launch_straddle<T, OP, K.value>(sl, r, sp, stream); });
 }
 
 #define DCCL_PHASED_INST(T)                                                       \

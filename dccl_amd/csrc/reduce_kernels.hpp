@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <cstddef>
 #include <cstdint>
 
@@ -666,6 +668,20 @@ inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream, 
 }
 
 inline size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }
+
+// Runtime source count -> compile-time K: f(std::integral_constant<int, K>{}) for k in [LO, HI],
+// DCCL_INVALID_ARGUMENT outside it.
+template <int LO, int HI, typename F>
+int with_k(int k, F&& f) {
+    if constexpr (LO > HI) {
+        (void)k;
+        (void)f;
+        return DCCL_INVALID_ARGUMENT;
+    } else {
+        if (k == LO) return f(std::integral_constant<int, LO>{});
+        return with_k<LO + 1, HI>(k, static_cast<F&&>(f));
+    }
+}
 
 struct Split {
     size_t head, nvec, tail;

@@ -37,32 +37,13 @@ int launch_chain(SendList sl, PhaseList ph, const unsigned char* own, unsigned c
 
 template <typename T, int OP>
 int multi_unaligned_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, size_t count, hipStream_t stream) {
-    switch (nsend) {
-    case 2: return launch_multi<T, OP, 2>(sl, ph, r, count, stream);
-    case 3: return launch_multi<T, OP, 3>(sl, ph, r, count, stream);
-    case 4: return launch_multi<T, OP, 4>(sl, ph, r, count, stream);
-    case 5: return launch_multi<T, OP, 5>(sl, ph, r, count, stream);
-    case 6: return launch_multi<T, OP, 6>(sl, ph, r, count, stream);
-    case 7: return launch_multi<T, OP, 7>(sl, ph, r, count, stream);
-    case 8: return launch_multi<T, OP, 8>(sl, ph, r, count, stream);
-    default: return DCCL_INVALID_ARGUMENT;
-    }
+    return with_k<2, 8>(nsend, [&](auto K) { return launch_multi<T, OP, K.value>(sl, ph, r, count, stream); });
 }
 
 template <typename T, int OP>
 int chain_unaligned_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d,
                           size_t count, hipStream_t stream) {
-    switch (nsend) {
-    case 1: return launch_chain<T, OP, 1>(sl, ph, own, d, count, stream);
-    case 2: return launch_chain<T, OP, 2>(sl, ph, own, d, count, stream);
-    case 3: return launch_chain<T, OP, 3>(sl, ph, own, d, count, stream);
-    case 4: return launch_chain<T, OP, 4>(sl, ph, own, d, count, stream);
-    case 5: return launch_chain<T, OP, 5>(sl, ph, own, d, count, stream);
-    case 6: return launch_chain<T, OP, 6>(sl, ph, own, d, count, stream);
-    case 7: return launch_chain<T, OP, 7>(sl, ph, own, d, count, stream);
-    case 8: return launch_chain<T, OP, 8>(sl, ph, own, d, count, stream);
-    default: return DCCL_INVALID_ARGUMENT;
-    }
+    return with_k<1, 8>(nsend, [&](auto K) { return launch_chain<T, OP, K.value>(sl, ph, own, d, count, stream); });
 }
 
 #define DCCL_UNALIGNED_INST_OP(T, OP)                                                                             \
