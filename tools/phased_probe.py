@@ -27,6 +27,8 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--straddle", action="store_true",
                    help="in-phase sources off recv's 128-B lines: tune_multi variants 0, 8, 9, 10 under the k-way caps")
+    p.add_argument("--swap", action="store_true",
+                   help="sources sharing one phase: tiles on the sources' 16-B grid (recv accessed unaligned)")
     p.add_argument("--prod-caps", action="store_true",
                    help="the shipped phased k-way and chain kernels: shipped form vs loads-first under wave caps")
     p.add_argument("--straddle-caps", action="store_true",
@@ -52,6 +54,9 @@ def main():
         return finish(a, rows)
     if a.prod_caps:
         prod_caps(a, recv, srcs, n, nbytes, st, rows)
+        return finish(a, rows)
+    if a.swap:
+        swap_tiling(a, recv, srcs, n, nbytes, st, rows)
         return finish(a, rows)
     if a.straddle_caps:
         straddle_caps(a, recv, srcs, n, nbytes, st, rows)
@@ -100,6 +105,41 @@ def finish(a, rows):
 
 
 VSTRADDLE = (0, 8, 14)
+
+
+def swap_tiling(a, recv, srcs, n, nbytes, st, rows):
+    """Every source at +4 B, recv 128-B aligned: the shipped phased dispatch (dccl_local_reduce_multi /
+    _chain) against the unaligned kernels started 3 elements in, so the sources' vectors are aligned and recv
+    is the operand accessed at an unaligned address (the 3 head elements are not timed), under wave caps
+    PHASED_WAVES."""
+    ws = tuple(int(x) for x in os.environ.get("PHASED_WAVES", "32,28,24,20,16,13").split(","))
+    for k in tuple(int(x) for x in os.environ.get("PHASED_K", "2,3,4,5,6,7,8").split(",")):
+        sp = [srcs.data_ptr() + j * (nbytes + 4096) + 4 for j in range(k)]
+        for j, q in enumerate(sp):
+            dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
+        arr = (ctypes.c_void_p * k)(*sp)
+        arr_sw = (ctypes.c_void_p * k)(*[q + 12 for q in sp])
+        r0 = recv.data_ptr()
+        for what in ("multi", "chain"):
+            t = {"shipped": []}
+            t.update({w: [] for w in ws})
+            for _ in range(a.rounds):
+                if what == "multi":
+                    f0 = lambda: dccl_amd.check(dccl_amd.local_reduce_multi(sp, r0, 7, n, 0, st), "multi")
+                else:
+                    f0 = lambda: dccl_amd.check(dccl_amd.local_reduce_chain(sp, r0, r0, 7, n, 0, st), "chain")
+                t["shipped"].append(time_launches([f0], rounds=1, min_ms=20.0)[0])
+                for w in ws:
+                    lds = 0 if w >= 32 else ((160 << 10) // w + 255) // 256 * 256
+                    own = None if what == "multi" else r0 + 12
+                    fn = lambda lds=lds, own=own: dccl_amd.check(tune_lib.lib.dccl_tune_unaligned_kway_f32_sum(
+                        arr_sw, k, own, r0 + 12, n - 3, lds, st), "swap")
+                    t[w].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+            for key, v in t.items():
+                ms = statistics.median(v)
+                rows.append({"what": what, "k": k, "tiling": "shipped" if key == "shipped" else f"swap@{key}",
+                             "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
+                print(json.dumps(rows[-1]), flush=True)
 
 
 def prod_caps(a, recv, srcs, n, nbytes, st, rows):

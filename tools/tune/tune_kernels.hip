@@ -1119,3 +1119,42 @@ extern "C" int dccl_tune_shift_caps_f32_sum(const void* send, void* recv, size_t
     return (a & 127) ? launch_shift<float, kSum, kPs, false>(s, r, count, st, 128, lds_bytes)
                      : launch_shift<float, kSum, kP, false>(s, r, count, st, 128, lds_bytes);
 }
+
+// ---------------------------------------------------------------------------------
+// Tuning only: the shipped unaligned k-way (own == nullptr) and chain kernels called directly on any
+// operands (the product calls them only for a destination that is not element-aligned), under an
+// explicit wave cap: used to try "sources aligned, destination at another phase" tilings.
+// ---------------------------------------------------------------------------------
+namespace {
+template <int K>
+int tune_unaligned_kway_k(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, size_t count,
+                          hipStream_t st, size_t lds) {
+    size_t nvec = count / 4;
+    const size_t grid = ceil_div(ceil_div(nvec, size_t(64)), size_t(8)) * 8;
+    if (own == nullptr) {
+        void* args[] = {&sl, &ph, &d, &nvec, &count};
+        return launch(reinterpret_cast<const void*>(&reduce_multi_unaligned_kernel<float, kSum, K>), grid, args, st,
+                      64, lds);
+    }
+    void* args[] = {&sl, &ph, &own, &d, &nvec, &count};
+    return launch(reinterpret_cast<const void*>(&reduce_chain_unaligned_kernel<float, kSum, K>), grid, args, st, 64,
+                  lds);
+}
+}  // namespace
+
+extern "C" int dccl_tune_unaligned_kway_f32_sum(const void* const* sends, int nsend, const void* own, void* dst,
+                                                size_t count, size_t lds_bytes, void* stream) {
+    if (sends == nullptr || dst == nullptr || nsend < 2 || nsend > 8 || lds_bytes > (64u << 10))
+        return DCCL_INVALID_ARGUMENT;
+    SendList sl{};
+    PhaseList ph{};
+    for (int k = 0; k < nsend; ++k) {
+        sl.p[k] = static_cast<const unsigned char*>(sends[k]);
+        ph.p[k] = phase_word(sl.p[k], 0);
+    }
+    const auto o = static_cast<const unsigned char*>(own);
+    if (o != nullptr) ph.p[nsend] = phase_word(o, 0);
+    auto d = static_cast<unsigned char*>(dst);
+    const auto st = static_cast<hipStream_t>(stream);
+    return with_k<2, 8>(nsend, [&](auto K) { return tune_unaligned_kway_k<K.value>(sl, ph, o, d, count, st, lds_bytes); });
+}
