@@ -562,3 +562,52 @@ def test_graph_capture_replay(dccl):
         g.replay()
     torch.cuda.synchronize()
     assert torch.all(r == 20.0)
+
+
+def test_graph_capture_every_kernel_family(dccl):
+    """Every launch path enqueues kernels only (no allocation, no host synchronisation), so each can be
+    captured in one HIP graph and replayed: the pairwise combine with send off phase (shifted kernel) and
+    with recv off its elements (unaligned kernel, wave-capped launch), the k-way combine with sources in
+    phase, off phase (phased kernels, both forms) and at byte offsets into a misaligned recv, and the chain.
+    Integer Sum, so r after R replays is exactly r0 + R * (sum of the sources) per capture."""
+    n = (1 << 18) + 5
+    rng = np.random.default_rng(77)
+    st = torch.cuda.Stream()
+
+    def buf(vals, off):
+        t = torch.zeros(n * 4 + 64, dtype=torch.uint8, device="cuda")
+        t[off:off + n * 4].copy_(torch.from_numpy(vals.view(np.uint8).copy()))
+        return t, t.data_ptr() + off
+
+    srcs = [rng.integers(-1000, 1000, n, dtype=np.int32) for _ in range(8)]
+    cases = [("shift", [4], 0), ("unaligned", [0], 1), ("kway_inphase", [0, 0, 0], 0),
+             ("kway_phased_small", [4, 8, 12], 0), ("kway_phased_first", [4] * 5, 0),
+             ("kway_bytes", [1, 2, 3, 5], 2), ("chain", [4] * 7, 0)]
+    for name, soffs, roff in cases:
+        hold = [buf(srcs[j], o) for j, o in enumerate(soffs)]
+        r0 = rng.integers(-1000, 1000, n, dtype=np.int32)
+        tr, pr = buf(r0, roff)
+        ptrs = [h[1] for h in hold]
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(st):
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=st):
+                if name in ("shift", "unaligned"):
+                    assert dccl.local_reduce(ptrs[0], pr, 2, n, 0, st.cuda_stream) == 0
+                elif name == "chain":  # in place: dst = own + (s6 + ... + s0)
+                    assert dccl.local_reduce_chain(ptrs, pr, pr, 2, n, 0, st.cuda_stream) == 0
+                else:
+                    assert dccl.local_reduce_multi(ptrs, pr, 2, n, 0, st.cuda_stream) == 0
+        torch.cuda.synchronize()
+        tr[roff:roff + n * 4].copy_(torch.from_numpy(r0.view(np.uint8).copy()))  # capture does not execute
+        torch.cuda.synchronize()
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        total = np.zeros(n, dtype=np.int64)
+        for j in range(len(soffs)):
+            total += srcs[j]
+        want = (r0.astype(np.int64) + 3 * total).astype(np.int32)
+        got = tr[roff:roff + n * 4].cpu().numpy().view(np.int32)
+        assert np.array_equal(got, want), name
+        del g
