@@ -543,6 +543,57 @@ def test_misaligned_reference_wrong_build_correct(dccl):
         assert got.tobytes() == correct.tobytes(), i
 
 
+def test_concurrent_threads_and_streams(dccl):
+    """Reentrancy (SURVEY §8(b) threading): 6 host threads, each with its own stream, run the device combine
+    (pairwise at several alignments, k-way, chain) and the host-staged combine concurrently on their own
+    buffers, 20 times each; every result matches the sequential expectation."""
+    import threading
+    errors = []
+
+    def worker(seed):
+        try:
+            torch.cuda.set_device(0)
+            rng = np.random.default_rng(900 + seed)
+            st = torch.cuda.Stream()
+            n = 100_003 + seed
+            for it in range(20):
+                dt = [2, 7, 9, 4][(seed + it) % 4]
+                op = int(rng.integers(0, 4))
+                s, r = rand_inputs(rng, dt, n)
+                soff, roff = [(0, 0), (4, 0), (1, 0), (0, 2)][it % 4]
+                if dt == 4:
+                    soff, roff = soff * 2, 0
+                if dt == 9 and roff:
+                    roff = 1
+                ts, ps = dev_bytes(s, soff)
+                tr, pr = dev_bytes(r, roff)
+                torch.cuda.current_stream().synchronize()  # the operand copies ran on this thread's default stream
+                with torch.cuda.stream(st):
+                    if it % 5 == 4:  # the host-staged path on this thread's own staging resources
+                        s2, r2 = s.copy(), r.copy()
+                        assert dccl.local_reduce_host(s2.ctypes.data, r2.ctypes.data, dt, n, op) == 0
+                        assert fp_equal(r2, expected(s, r, dt, op), dt), ("host", seed, it)
+                        continue
+                    if it % 3 == 2:
+                        assert dccl.local_reduce_multi([ps, ps], pr, dt, n, op, st.cuda_stream) == 0
+                        want = expected(s, expected(s, r, dt, op), dt, op)
+                    else:
+                        assert dccl.local_reduce(ps, pr, dt, n, op, st.cuda_stream) == 0
+                        want = expected(s, r, dt, op)
+                    st.synchronize()
+                assert fp_equal(host_of(tr, roff, r), want, dt), (seed, it, dt, op, soff, roff)
+        except Exception as e:  # surfaced in the test thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(6)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(120)
+    assert not any(t.is_alive() for t in threads), "a worker hung"
+    assert not errors, errors[:2]
+
+
 def test_graph_capture_replay(dccl):
     """dccl_local_reduce only enqueues a kernel on the given stream, so it can be captured in a HIP
     graph (torch.cuda.graph) and replayed; each replay applies the combine once more."""
