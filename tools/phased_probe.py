@@ -174,8 +174,9 @@ def straddle_caps(a, recv, srcs, n, nbytes, st, rows):
     """The shipped line-straddle k-way and chain shapes (sources cached) under explicit wave caps
     (STRADDLE_WAVES, STRADDLE_K); the chain runs in place (own = dst = recv)."""
     ks = tuple(int(x) for x in os.environ.get("STRADDLE_K", "5,6,7,8").split(","))
+    variant = int(os.environ.get("STRADDLE_VARIANT", "8"))  # 8: shipped shape; 11: head aligned to sends[0]
     for k in ks:
-        sp = [srcs.data_ptr() + j * (nbytes + 4096) + 16 * (2 * j + 1) for j in range(k)]
+        sp = [srcs.data_ptr() + j * (nbytes + 4096) + (16 if a.common_phase else 16 * (2 * j + 1)) for j in range(k)]
         for j, q in enumerate(sp):
             dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
         arr = (ctypes.c_void_p * k)(*sp)
@@ -185,7 +186,7 @@ def straddle_caps(a, recv, srcs, n, nbytes, st, rows):
             for w in waves:
                 lds = 0 if w >= 32 else ((160 << 10) // w + 255) // 256 * 256
                 fn = lambda lds=lds: dccl_amd.check(tune_lib.lib.dccl_tune_multi_f32_sum(
-                    arr, k, recv.data_ptr(), n, 8, lds, st), "multi straddle")
+                    arr, k, recv.data_ptr(), n, variant, lds, st), "multi straddle")
                 t[w].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
         tc = {w: [] for w in waves}
         for _ in range(a.rounds):
@@ -197,7 +198,8 @@ def straddle_caps(a, recv, srcs, n, nbytes, st, rows):
         for w in waves:
             for what, tt in (("multi", t), ("chain", tc)):
                 ms = statistics.median(tt[w])
-                rows.append({"what": what, "k": k, "waves": w, "ms": round(ms, 4),
+                rows.append({"what": what, "k": k, "waves": w, "variant": variant if what == "multi" else 6,
+                             "ms": round(ms, 4),
                              "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
                 print(json.dumps(rows[-1]), flush=True)
 
