@@ -533,7 +533,9 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
         t = (time.perf_counter() - t0) / iters
         out["rccl_allreduce"] = {"ms": round(t * 1e3, 3),
                                  "busbw_gb_s": round(2 * (world - 1) / world * count * 4 / t / 1e9, 1),
-                                 "note": "RCCL's own all_reduce, informational: its combine is RCCL's"}
+                                 "backend": dist.get_backend(),
+                                 "note": "the torch.distributed backend's own all_reduce (RCCL when the backend is "
+                                         "nccl), informational: its combine is the backend's"}
         out["dccl_allgather"] = allgather_compare(comms, world, rank, dev, st, count, iters)
         # BASELINE C5's exchange step at its own size (the reduced shards of DCCL_BENCH_C5_GIB GiB of fp32,
         # moved as int32): the direct IPC all-gather beside RCCL's (the single-link ring is left out here)
