@@ -2,7 +2,7 @@
 
 For k = 1..8 sends of --mib MiB fp32 and two operand placements (separate allocations; one pool
 with a 4 KiB x (j+1) stagger between operand j and j+1), times each variant of
-dccl_tune_multi_f32_sum (include/dccl/dccl_reduce_tuning.h) and the shipped entry point.
+dccl_tune_multi_f32_sum (tools/tune/dccl_reduce_tuning.h) and the shipped entry point.
 Algorithmic bytes per launch: (k + 2) * operand bytes.  Use 1 GiB operands (--mib 1024) for decisions:
 at 256 MiB a recv buffer written with the default cache policy partly survives in the 256 MiB
 Infinity Cache between back-to-back launches, which flatters variants 3 (profiles/r1_tune_multi_*.json).

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B the fp32-Sum combine kernel variants in ONE process, interleaved rounds (MI355X).
 
-Variants (include/dccl/dccl_reduce_tuning.h):
+Variants (tools/tune/dccl_reduce_tuning.h):
   * template variants: block threads x UNROLL x cache policy (nt send / nt recv / nt store)
     x XCD-contiguous remap, one block per tile or a persistent grid;
   * asm flavours: one-wave blocks with explicit sc0/sc1/nt bits on loads and stores;
