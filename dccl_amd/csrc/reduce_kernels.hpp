@@ -263,11 +263,11 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
 // reads it (aligned loads, lane exchange, funnel shift by its own phase): unaligned send loads as well
 // cost a further 7-10 points.  A 1 KiB tile spans 9 lines of recv, one shared with the next tile;
 // consecutive tiles go to one XCD (blocks are dealt round-robin over the 8 XCDs), so the shared lines meet
-// in one L2.  1 GiB fp32 Sum on MI355X, recv + 1 B: 76.4-76.7 % of HBM peak uncapped (78.4-78.8 % under the
-// kUnalignedWaves cap), against 74.6-74.8 % with
-// consecutive tiles on different XCDs and 72-73 % for a byte-gather kernel; a two-pass form writing every
-// recv vector whole from one wave reached 74-75.5 % (tools/tune/, profiles/r2_misaligned_ab.json).  The
-// tail (< V elements) is block 0's, element by element.  Kernel: after ld_phased below.
+// in one L2.  1 GiB fp32 Sum on MI355X, recv + 1 B: 78.4-78.8 % of HBM peak under the kUnalignedWaves cap
+// (76.4-76.7 % uncapped), against 74.6-74.8 % with consecutive tiles on different XCDs and 72-73 % for a
+// byte-gather kernel; a two-pass form writing every recv vector whole from one wave reached 74-75.5 %
+// (tools/tune/, profiles/r2_misaligned_ab.json, r2_misaligned_caps.json).  The tail (< V elements) is
+// block 0's, element by element.  Kernel: after ld_phased below.
 // ---------------------------------------------------------------------------------
 typedef u32x4 u32x4_u __attribute__((aligned(1)));
 
