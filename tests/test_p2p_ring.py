@@ -13,6 +13,7 @@ The GPU side of the same branch (real combine, the dccl_api glue) is tests/test_
 """
 import json
 import os
+import shutil
 import subprocess
 
 import numpy as np
@@ -33,15 +34,19 @@ SEED = 0xDCC1
 def harness():
     deps = SRCS + [os.path.join(ROOT, "dccl_amd", "csrc", f) for f in ("algorithms.hpp", "comm.hpp", "dispatch.hpp")]
     if not os.path.exists(HARNESS) or os.path.getmtime(HARNESS) < max(os.path.getmtime(p) for p in deps):
-        os.makedirs(OUT, exist_ok=True)
+        # Per-process scratch directory and an atomic rename: pytest-xdist workers may build at once.
+        tmp = os.path.join(OUT, f"tmp.{os.getpid()}")
+        os.makedirs(tmp, exist_ok=True)
         hip = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-O1", "-Wall",
                f"-I{ROOT}/include", f"-I{ROOT}/dccl_amd/csrc"]
-        subprocess.run(hip + ["-c", SRCS[0], "-o", f"{OUT}/harness.o"], check=True)
-        subprocess.run(hip + ["-c", SRCS[1], "-o", f"{OUT}/algorithms.o"], check=True)
-        subprocess.run(["gcc", "-std=c11", "-O2", "-fPIC", "-c", SRCS[2], "-o", f"{OUT}/oracle_host_reduce.o"],
+        subprocess.run(hip + ["-c", SRCS[0], "-o", f"{tmp}/harness.o"], check=True)
+        subprocess.run(hip + ["-c", SRCS[1], "-o", f"{tmp}/algorithms.o"], check=True)
+        subprocess.run(["gcc", "-std=c11", "-O2", "-fPIC", "-c", SRCS[2], "-o", f"{tmp}/oracle_host_reduce.o"],
                        check=True)
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", f"{OUT}/harness.o", f"{OUT}/algorithms.o",
-                        f"{OUT}/oracle_host_reduce.o", "-o", HARNESS, "-pthread"], check=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", f"{tmp}/harness.o", f"{tmp}/algorithms.o",
+                        f"{tmp}/oracle_host_reduce.o", "-o", f"{tmp}/ring_p2p_harness", "-pthread"], check=True)
+        os.replace(f"{tmp}/ring_p2p_harness", HARNESS)
+        shutil.rmtree(tmp, ignore_errors=True)
     return HARNESS
 
 
