@@ -54,18 +54,39 @@ size_t recv_align() {
     }();
     return v;
 }
-// Optional occupancy cap: DCCL_REDUCE_LDS_CAP bytes of (unused) dynamic LDS per one-wave block
-// (e.g. 7168 admits 22 blocks per CU instead of 32).  Off by default: with operands in a friendly
-// physical placement the uncapped launch is 0.8 % faster (profiles/r1_occupancy_pooled_*.json);
-// with separately allocated operands in the slow placement mode a 22-wave cap gained 1.0-1.4 %
-// (profiles/r1_tune_occupancy*.json).  Read once per process.
-size_t occupancy_lds() {
+// Occupancy cap of the aligned pairwise launch, as bytes of (unused) dynamic LDS per one-wave block
+// (160 KiB / bytes resident waves per CU).  DCCL_REDUCE_LDS_CAP, read once per process, forces a value
+// (0 = uncapped).  Unset, the cap follows the operands' allocations:
+//   * both in ONE allocation (the bench's pooled pair): uncapped, 0.4-1.1 points faster than any cap;
+//   * in two allocations (DCCL's scratchpad + user chunk) of at least kSeparateCapBytes each: 22 waves
+//     per CU.  Paired A/B of the same pairs under every cap (tools/separate_cap_paired.py, 8 separate
+//     1 GiB pairs per run, profiles/r2_s61_separate_cap_paired*.json): median over pairs +0.6 to +1.0
+//     points at 1 GiB in four runs, +0.7 at 4 GiB, +0.5 at 512 MiB, but -0.8 at 256 MiB, hence the
+//     size floor.  Caps of 21-24 waves are equivalent; 20 and 26 lose.
+constexpr size_t kUnsetCap = ~size_t(0);
+constexpr size_t kSeparateCapBytes = size_t(1) << 30;
+constexpr size_t kSeparateLds = 7168;  // 22 waves per CU
+size_t forced_occupancy_lds() {
     static const size_t v = [] {
         const char* e = std::getenv("DCCL_REDUCE_LDS_CAP");
-        const unsigned long long x = e ? std::strtoull(e, nullptr, 10) : 0ull;
+        if (e == nullptr || *e == '\0') return kUnsetCap;
+        const unsigned long long x = std::strtoull(e, nullptr, 10);
         return static_cast<size_t>(x > (64ull << 10) ? (64ull << 10) : x);
     }();
     return v;
+}
+size_t pair_occupancy_lds(const void* send, const void* recv, size_t bytes) {
+    const size_t forced = forced_occupancy_lds();
+    if (forced != kUnsetCap) return forced;
+    if (bytes < kSeparateCapBytes) return 0;
+    hipDeviceptr_t bs = nullptr, br = nullptr;
+    size_t ls = 0, lr = 0;
+    if (hipMemGetAddressRange(&bs, &ls, const_cast<void*>(send)) != hipSuccess ||
+        hipMemGetAddressRange(&br, &lr, const_cast<void*>(recv)) != hipSuccess) {
+        (void)hipGetLastError();  // not runtime-allocated device memory: no cap, and no stale error left behind
+        return 0;
+    }
+    return bs == br ? 0 : kSeparateLds;
 }
 template <typename T, int OP>
 int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream) {
@@ -95,8 +116,11 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
         return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false>(s, r, count, stream, align)
                          : launch_shift<T, OP, ShiftPolicy, false>(s, r, count, stream, align);
     }
-    if ((as ^ ar) & 127) return launch_vec<T, OP, StraddleCfg>(s, r, sp, stream, 0, occupancy_lds());
-    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream, 0, occupancy_lds());
+    if ((as ^ ar) & 127) {
+        const size_t forced = forced_occupancy_lds();
+        return launch_vec<T, OP, StraddleCfg>(s, r, sp, stream, 0, forced == kUnsetCap ? 0 : forced);
+    }
+    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream, 0, pair_occupancy_lds(send, recv, count * sizeof(T)));
 }
 
 // k-way combine: every resident wave keeps k+1 16-B loads per lane in flight, so the resident waves
