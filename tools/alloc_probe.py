@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Allocation probe (tuning only): the shipped fp32 Sum combine over 1 GiB operands in bench.py's pooled
 layout (recv, then send 4 KiB past its end), with the pool allocated three ways: torch's caching
-allocator, hipMalloc, and hipExtMallocWithFlags(hipDeviceMallocContiguous).  Timed interleaved.
+allocator, hipMalloc, and hipExtMallocWithFlags with hipDeviceMallocContiguous, hipDeviceMallocUncached and
+hipDeviceMallocFinegrained (the last two change the memory type the caches and the Infinity Cache see).
+Timed interleaved.
     python tools/alloc_probe.py [--rounds 9] [--out f.json]
 """
 import argparse
@@ -30,7 +32,8 @@ def main():
     size = 2 * nbytes + 4096
     keep = torch.empty(size, dtype=torch.uint8, device="cuda")
     pools = {"torch": keep.data_ptr()}
-    for name, flags in (("hipMalloc", None), ("contiguous", 0x4), ("hipMalloc_2", None)):
+    for name, flags in (("hipMalloc", None), ("contiguous", 0x4), ("uncached", 0x3), ("finegrained", 0x1),
+                        ("hipMalloc_2", None)):
         ptr = ctypes.c_void_p()
         rc = hip.hipMalloc(ctypes.byref(ptr), ctypes.c_size_t(size)) if flags is None else \
             hip.hipExtMallocWithFlags(ctypes.byref(ptr), ctypes.c_size_t(size), ctypes.c_uint(flags))
