@@ -7,7 +7,7 @@ fp32 Sum, 1 GiB per operand:
   phased     k-way (k = 4) and chain (k = 7) with every source 4 B off the destination's 16-B phase, and
              with sources or the destination not element-aligned;
   misaligned the shape variants of the misaligned-recv kernel through the tuning library (--tune).
-    python tools/ab_combine.py LIB_A LIB_B [--rounds 7] [--tune] [--out f.json]
+    python tools/ab_combine.py LIB_A LIB_B [--rounds 7] [--tune | --tune-only [--vars 25,30] [--roffs 1,2]] [--out f.json]
 """
 import argparse
 import ctypes
@@ -46,8 +46,12 @@ def main():
     p.add_argument("--rounds", type=int, default=7)
     p.add_argument("--tune", action="store_true", help="also time the misaligned-recv shape variants")
     p.add_argument("--tune-only", action="store_true", help="only the misaligned-recv shape variants")
+    p.add_argument("--vars", default="", help="comma list of misaligned-recv tuning variants (default: VARS)")
+    p.add_argument("--roffs", default="1", help="comma list of recv byte offsets for the tuning variants")
     p.add_argument("--out", default="")
     a = p.parse_args()
+    tvars = [int(x) for x in a.vars.split(",")] if a.vars else VARS
+    roffs = [int(x) for x in a.roffs.split(",")]
     libs = [bind(x) for x in a.libs]
     st = torch.cuda.current_stream().cuda_stream
     nbytes = 1 << 30
@@ -121,13 +125,13 @@ def main():
         dccl_amd.check(dccl_amd.synth_fill(s2.data_ptr(), 7, nbytes // 4, 0, 0xDCC1, 3, st), "synth")
         dccl_amd.check(dccl_amd.synth_fill(r2.data_ptr(), 7, nbytes // 4, 0, 0xDCC1, 4, st), "synth")
         for layout, sb, rb in (("pooled", send0, recv0), ("separate", s2.data_ptr(), r2.data_ptr())):
-            for roff in (1,):
-                t = {v: [] for v in VARS}
+            for roff in roffs:
+                t = {v: [] for v in tvars}
                 for _ in range(a.rounds):
-                    for v in VARS:
+                    for v in tvars:
                         fn = lambda v=v: tune_lib.lib.dccl_tune_misaligned_f32_sum(sb, rb + roff, n, v, st)
                         t[v].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
-                for v in VARS:
+                for v in tvars:
                     ms = statistics.median(t[v])
                     rows.append({"lib": "tune", "case": f"{layout}: misaligned recv +{roff} variant {v}",
                                  "ms": round(ms, 4), "frac": round(3 * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
