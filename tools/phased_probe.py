@@ -34,6 +34,8 @@ def main():
     p.add_argument("--straddle-caps", action="store_true",
                    help="line-straddling sources, k = 5-8: wave-cap sweep of the shipped straddle shape (variant 8)")
     p.add_argument("--common-phase", action="store_true", help="--straddle: every source at the same line offset")
+    p.add_argument("--straddle-group", action="store_true",
+                   help="line-straddling sources: the shipped shape against the group-interleaved XCD order (15/16)")
     p.add_argument("--caps", action="store_true", help="wave-cap sweep of the loads-first variants (8, 9)")
     p.add_argument("--walk", action="store_true", help="the walking variants (dccl_tune_phased_walk_f32_sum) instead")
     p.add_argument("--chain", action="store_true", help="also the phased chain kernel, XCD order off / on")
@@ -60,6 +62,9 @@ def main():
         return finish(a, rows)
     if a.straddle_caps:
         straddle_caps(a, recv, srcs, n, nbytes, st, rows)
+        return finish(a, rows)
+    if a.straddle_group:
+        straddle_group(a, recv, srcs, n, nbytes, st, rows)
         return finish(a, rows)
     if a.straddle:
         straddle(a, recv, srcs, n, nbytes, st, rows)
@@ -202,6 +207,51 @@ def straddle_caps(a, recv, srcs, n, nbytes, st, rows):
                              "ms": round(ms, 4),
                              "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
                 print(json.dumps(rows[-1]), flush=True)
+
+
+STRADDLE_WAVES = [32, 32, 18, 13, 13, 11, 9, 9, 7]  # kStraddleWaves in dccl_amd/csrc/reduce_kernels.hpp
+
+
+def straddle_group(a, recv, srcs, n, nbytes, st, rows):
+    """Sources 16-B aligned but off recv's 128-B lines (+16 (2j+1) B), k in STRADDLE_K: the shipped straddle
+    shape (variant 8, sources cached, block order) at its shipped cap against the group-interleaved XCD order
+    (15: sources cached, 16: all non-temporal) under the caps STRADDLE_WAVES (32 = uncapped).  First checks
+    15 and 16 against the product entry point bit for bit on a small ragged size."""
+    m = 100_003
+    small = [srcs.data_ptr() + j * (nbytes + 4096) + 16 * (2 * j + 1) for j in range(8)]
+    for j, q in enumerate(small):
+        dccl_amd.check(dccl_amd.synth_fill(q, 7, m, 0, 0xDCC1, 10 + j, st), "synth")
+    for k in range(2, 9):
+        arr = (ctypes.c_void_p * k)(*small[:k])
+        ref = torch.empty(4 * m + 256, dtype=torch.uint8, device="cuda")
+        dccl_amd.check(dccl_amd.synth_fill(ref.data_ptr() + 128, 7, m, 0, 0xDCC1, 1, st), "synth")
+        base = ref.clone()
+        dccl_amd.check(dccl_amd.local_reduce_multi(small[:k], ref.data_ptr() + 128, 7, m, 0, st), "multi")
+        for v in (15, 16):
+            got = base.clone()
+            dccl_amd.check(tune_lib.lib.dccl_tune_multi_f32_sum(arr, k, got.data_ptr() + 128, m, v, 0, st), "v")
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref), (k, v)
+    print("group-order variants bit-exact against the product", flush=True)
+    ws = tuple(int(x) for x in os.environ.get("STRADDLE_WAVES", "32,20,16,13,11,9").split(","))
+    for k in tuple(int(x) for x in os.environ.get("STRADDLE_K", "4,5,6,7,8").split(",")):
+        sp = [srcs.data_ptr() + j * (nbytes + 4096) + 16 * (2 * j + 1) for j in range(k)]
+        for j, q in enumerate(sp):
+            dccl_amd.check(dccl_amd.synth_fill(q, 7, n, 0, 0xDCC1, 10 + j, st), "synth")
+        arr = (ctypes.c_void_p * k)(*sp)
+        configs = [(8, STRADDLE_WAVES[k])] + [(v, w) for v in (15, 16) for w in ws]
+        t = {c: [] for c in configs}
+        for _ in range(a.rounds):
+            for v, w in configs:
+                lds = 0 if w >= 32 else ((160 << 10) // w + 255) // 256 * 256
+                fn = lambda v=v, lds=lds: dccl_amd.check(tune_lib.lib.dccl_tune_multi_f32_sum(
+                    arr, k, recv.data_ptr(), n, v, lds, st), "multi straddle")
+                t[(v, w)].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
+        for v, w in configs:
+            ms = statistics.median(t[(v, w)])
+            rows.append({"k": k, "variant": v, "waves": w, "ms": round(ms, 4),
+                         "frac": round((k + 2) * n * 4 / (ms * 1e-3) / 1e9 / PEAK, 4)})
+            print(json.dumps(rows[-1]), flush=True)
 
 
 def straddle(a, recv, srcs, n, nbytes, st, rows):

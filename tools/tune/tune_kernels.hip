@@ -170,7 +170,8 @@ extern "C" int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count
 // through the caches (the shipped line-straddle shape), 9 / 10 = 0 / 8 with each XCD's tiles one contiguous
 // range (xcd_remap); 11 / 12 / 13 = 0 / 8 / 3 with the head scalars aligning sends[0] to its 128-B line
 // instead of recv (recv straddles its lines, the sources sharing sends[0]'s line phase do not); 14 = sources
-// cached only in the tile's two partial lines (tune_multi_edge_cached_kernel); `lds_bytes` of
+// cached only in the tile's two partial lines (tune_multi_edge_cached_kernel); 15 / 16 = 8 / 0 in the
+// group-interleaved XCD tile order (tune_multi_group_kernel); `lds_bytes` of
 // unused dynamic LDS per block caps the resident blocks per CU (160 KiB / lds_bytes).
 // ---------------------------------------------------------------------------------
 namespace {
@@ -264,6 +265,46 @@ int tune_multi_edge_cached(SendList sl, unsigned char* r, Split sp, hipStream_t 
     return launch(reinterpret_cast<const void*>(&tune_multi_edge_cached_kernel<K>), grid, args, st, 64, lds);
 }
 
+// The shipped k-way kernel with the group-interleaved XCD tile order (xcd_group_tile: within every group of 64
+// blocks, each XCD walks 8 consecutive tiles; the groups sweep the range in order, so the chip keeps one
+// front).  Tiles t and t+1 then share an L2 in 7 of 8 cases, so a line-straddling source's line that two
+// neighbouring tiles share is fetched from HBM once instead of twice (PMC: each straddling source reads
+// 1.125 x in block order).  P: cache policy bits (6: sources cached, 7: all non-temporal).
+template <int K, int P>
+__global__ __launch_bounds__(64) void tune_multi_group_kernel(SendList sends, unsigned char* __restrict__ recv,
+                                                              size_t head, size_t nvec, size_t tail) {
+    u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(float));
+    const size_t ntiles = (nvec + 63) / 64;
+    for (size_t t = xcd_group_tile(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+        const size_t i = t * 64 + threadIdx.x;
+        if (i < nvec) {
+            u32x4 s[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                s[k] = ld16<(P & kNtSend) != 0>(reinterpret_cast<const u32x4*>(sends.p[k] + head * sizeof(float)) + i);
+            u32x4 acc = ld16<(P & kNtRecv) != 0>(vr + i);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = combine16<float, kSum>(acc, s[k]);
+            __builtin_nontemporal_store(acc, vr + i);
+        }
+    }
+    if (blockIdx.x == 0)
+        for (size_t j = threadIdx.x; j < head + tail; j += 64) {
+            const size_t e = j < head ? j : head + nvec * 4 + (j - head);
+            float acc = ld_elem<float, true>(recv, e);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = Combine<float, kSum>::apply(acc, ld_elem<float, true>(sends.p[k], e));
+            st_elem<float, true>(recv, e, acc);
+        }
+}
+template <int K, int P>
+int tune_multi_group(SendList sl, unsigned char* r, Split sp, hipStream_t st, size_t lds) {
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0) grid = 1;
+    void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
+    return launch(reinterpret_cast<const void*>(&tune_multi_group_kernel<K, P>), grid, args, st, 64, lds);
+}
+
 template <int K>
 int tune_multi_k(int variant, SendList sl, unsigned char* r, Split sp, hipStream_t st, size_t lds) {
     switch (variant) {
@@ -279,6 +320,8 @@ int tune_multi_k(int variant, SendList sl, unsigned char* r, Split sp, hipStream
     case 9: return tune_multi_launch<K, VecCfg<64, 1, 7, true, 1>>(sl, r, sp, st, lds);
     case 10: return tune_multi_launch<K, VecCfg<64, 1, 6, true, 1>>(sl, r, sp, st, lds);
     case 14: return tune_multi_edge_cached<K>(sl, r, sp, st, lds);
+    case 15: return tune_multi_group<K, kNtRecv | kNtStore>(sl, r, sp, st, lds);
+    case 16: return tune_multi_group<K, kNtSend | kNtRecv | kNtStore>(sl, r, sp, st, lds);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
@@ -298,9 +341,10 @@ extern "C" int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void
     if (ar & 3) return DCCL_INVALID_ARGUMENT;
     if (count == 0) return DCCL_SUCCESS;
     // recv line-aligned, as the shipped launch; variants 11-13: sends[0] line-aligned instead (recv straddles)
-    const uintptr_t anchor = variant >= 11 ? reinterpret_cast<uintptr_t>(sends[0]) : ar;
+    const bool src_anchor = variant >= 11 && variant <= 13;
+    const uintptr_t anchor = src_anchor ? reinterpret_cast<uintptr_t>(sends[0]) : ar;
     const Split sp = split_for_vectors<float>(anchor, count, 128);
-    if (variant >= 11) variant = variant == 11 ? 0 : variant == 12 ? 8 : 3;
+    if (src_anchor) variant = variant == 11 ? 0 : variant == 12 ? 8 : 3;
     auto r = static_cast<unsigned char*>(recv);
     const auto st = static_cast<hipStream_t>(stream);
     switch (nsend) {
