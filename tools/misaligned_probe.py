@@ -20,6 +20,7 @@ def main():
     p.add_argument("--roff", type=int, default=1)
     p.add_argument("--soff", type=int, default=0)
     p.add_argument("--launches", type=int, default=5)
+    p.add_argument("--variant", type=int, default=-1, help="a tools/tune misaligned-recv variant instead of the product")
     a = p.parse_args()
     nbytes = 1 << 30
     n = nbytes // 4 - 64
@@ -29,7 +30,12 @@ def main():
     dccl_amd.check(dccl_amd.synth_fill(base, 7, nbytes // 4, 0, 0xDCC1, 1, st), "synth")
     dccl_amd.check(dccl_amd.synth_fill(base + nbytes + 4096, 7, nbytes // 4, 0, 0xDCC1, 2, st), "synth")
     for _ in range(a.launches):
-        dccl_amd.check(dccl_amd.local_reduce(base + nbytes + 4096 + a.soff, base + a.roff, 7, n, 0, st), "combine")
+        if a.variant >= 0:
+            from tools import tune_lib
+            dccl_amd.check(tune_lib.lib.dccl_tune_misaligned_f32_sum(base + nbytes + 4096 + a.soff, base + a.roff, n,
+                                                                     a.variant, st), "tune")
+        else:
+            dccl_amd.check(dccl_amd.local_reduce(base + nbytes + 4096 + a.soff, base + a.roff, 7, n, 0, st), "combine")
     torch.cuda.synchronize()
 
 

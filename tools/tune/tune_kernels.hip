@@ -752,6 +752,115 @@ int tune_unaligned_edge(const unsigned char* s, unsigned char* r, size_t count, 
     void* args[] = {const_cast<unsigned char**>(&s), &p, &r, &nv, &cnt};
     return launch(reinterpret_cast<const void*>(&tune_unaligned_edge_kernel<E>), grid, args, st, 64, waves_lds(waves));
 }
+// Aligned-vector form of the misaligned-recv combine (walks of W tiles per wave).  recv's body is walked in
+// ALIGNED 16-B vectors V_v (from the first 16-B boundary inside recv, Vstart); every element boundary then
+// falls inside a vector, c bytes before its end (c = (Vstart - recv) mod e, 1 <= c < e).  Lane l builds the
+// element-aligned 16 bytes X that start at the element straddling its vector's first byte (the last c bytes
+// of V_{v-1}, from the lane to its left, and the first 16 - c of V_v), the matching send bytes SX (aligned
+// send vectors, funnel shift by sigma), combines them, takes the next element-aligned result from the lane to
+// its right, and stores the 16 output bytes of V_v whole.  A wave walks W consecutive tiles, carrying lane
+// 63's original V into the next tile's lane 0, so a recv line is never written by two waves except at walk
+// edges: the element straddling a walk edge belongs to the walk on its left, which writes its e - c bytes past
+// the edge bytewise; the walk on the right writes its first vector without them.  Head elements (up to the
+// one straddling Vstart) and tail elements (after the one straddling Vend) are block 0's, element by element.
+__device__ __forceinline__ u32x4 funnel_at(u32x4 lo, u32x4 hi, unsigned k) {  // bytes [k, k + 16), k < 16
+    const unsigned b = k & 3;
+    switch (k >> 2) {  // uniform
+    case 0: return funnel16<0>(lo, hi, b);
+    case 1: return funnel16<1>(lo, hi, b);
+    case 2: return funnel16<2>(lo, hi, b);
+    default: return funnel16<3>(lo, hi, b);
+    }
+}
+__device__ __forceinline__ unsigned char byte_of(u32x4 x, unsigned k) {
+    const unsigned d[4] = {x.x, x.y, x.z, x.w};
+    return static_cast<unsigned char>(d[k >> 2] >> (8 * (k & 3)));
+}
+template <typename T, int OP, int W>
+__global__ __launch_bounds__(64) void tune_unaligned_walk_vec_kernel(
+    const unsigned char* __restrict__ send, unsigned char* __restrict__ recv, unsigned char* vbase,
+    const unsigned char* ubase, size_t nv, unsigned c, unsigned sigma, size_t js, size_t je, size_t count) {
+    constexpr unsigned e = sizeof(T);
+    const unsigned lane = threadIdx.x;
+    u32x4* vr = reinterpret_cast<u32x4*>(vbase);
+    const u32x4* vu = reinterpret_cast<const u32x4*>(ubase);
+    const u32x4 zero = {0u, 0u, 0u, 0u};
+    const size_t nwalks = (nv + 64 * W - 1) / (64 * W);
+    for (size_t w = blockIdx.x; w < nwalks; w += gridDim.x) {
+        const size_t w0 = w * 64 * W, w1 = w0 + 64 * W < nv ? w0 + 64 * W : nv;
+        u32x4 carry = zero;
+        for (int j = 0; j < W; ++j) {
+            const size_t t0 = w0 + size_t(64) * j;
+            if (t0 >= w1) break;  // uniform
+            const size_t v = t0 + lane;
+            const bool in = v < w1;
+            const bool last = in && (lane == 63 || v + 1 == w1);
+            u32x4 vc = zero, u0 = zero, vn = zero, x1 = zero, x2 = zero;
+            if (in) {
+                vc = __builtin_nontemporal_load(vr + v);
+                u0 = __builtin_nontemporal_load(vu + v);
+            }
+            if (last) {
+                vn = vr[v + 1];
+                x1 = vu[v + 1];
+                if (sigma + e > 16) x2 = vu[v + 2];
+            }
+            u32x4 u1 = from_next_lane_or(u0, x1);
+            if (last) u1 = x1;
+            const u32x4 vp = from_prev_lane_or(vc, carry);
+            const u32x4 ox = combine16<T, OP>(funnel_at(vp, vc, 16 - c), funnel_at(u0, u1, sigma));
+            u32x4 oys = zero;
+            if (last) oys = combine16<T, OP>(funnel_at(vc, vn, 16 - c), funnel_at(x1, x2, sigma));
+            u32x4 oy = from_next_lane_or(ox, oys);
+            if (last) oy = oys;
+            const u32x4 out = funnel_at(ox, oy, c);
+            carry.x = unsigned(__builtin_amdgcn_readlane(int(vc.x), 63));
+            carry.y = unsigned(__builtin_amdgcn_readlane(int(vc.y), 63));
+            carry.z = unsigned(__builtin_amdgcn_readlane(int(vc.z), 63));
+            carry.w = unsigned(__builtin_amdgcn_readlane(int(vc.w), 63));
+            if (in) {
+                unsigned char* pv = reinterpret_cast<unsigned char*>(vr + v);
+                if (j == 0 && lane == 0) {  // walk edge: the straddling element's first e - c bytes are the left walk's
+                    for (unsigned k = e - c; k < 16; ++k) pv[k] = byte_of(out, k);
+                } else {
+                    __builtin_nontemporal_store(out, vr + v);
+                }
+                if (v + 1 == w1)  // walk edge: this walk owns the element straddling it, e - c bytes past the edge
+                    for (unsigned k = c; k < e; ++k) pv[16 + k - c] = byte_of(oy, k);
+            }
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (size_t i = lane; i <= js; i += 64)
+            st_elem<T, false>(recv, i, Combine<T, OP>::apply(ld_elem<T, false>(recv, i), ld_elem<T, false>(send, i)));
+        for (size_t i = je + 1 + lane; i < count; i += 64)
+            st_elem<T, false>(recv, i, Combine<T, OP>::apply(ld_elem<T, false>(recv, i), ld_elem<T, false>(send, i)));
+    }
+}
+template <typename T, int OP, int W>
+int tune_unaligned_walk_vec(const unsigned char* s, unsigned char* r, size_t count, hipStream_t st, int waves) {
+    constexpr size_t e = sizeof(T);
+    const uintptr_t ar = reinterpret_cast<uintptr_t>(r), as = reinterpret_cast<uintptr_t>(s);
+    const uintptr_t vs = (ar + 15) & ~uintptr_t(15), endb = ar + e * count, ve = endb & ~uintptr_t(15);
+    size_t nv = 0, js = count - 1, je = count - 1;
+    unsigned c = 0, sigma = 0;
+    const unsigned char* ub = s;
+    if (ve > vs) {
+        nv = (ve - vs) / 16;
+        js = (vs - ar) / e;
+        je = (ve - ar) / e;
+        c = unsigned(vs - (ar + e * js));
+        const uintptr_t sw = as + e * js;
+        sigma = unsigned(sw & 15);
+        ub = reinterpret_cast<const unsigned char*>(sw - sigma);
+    }
+    unsigned char* vb = r + (vs - ar);
+    size_t grid = ceil_div(nv, size_t(64) * W);
+    if (grid == 0) grid = 1;
+    void* args[] = {const_cast<unsigned char**>(&s), &r, &vb, &ub, &nv, &c, &sigma, &js, &je, &count};
+    return launch(reinterpret_cast<const void*>(&tune_unaligned_walk_vec_kernel<T, OP, W>), grid, args, st, 64,
+                  waves_lds(waves));
+}
 }  // namespace
 // recv must not be element-aligned (fp32: an address that is not a multiple of 4).
 // ---------------------------------------------------------------------------------
@@ -801,6 +910,19 @@ extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t
     case 31: return tune_unaligned_edge<64>(s, r, count, st, 32);
     case 32: return tune_unaligned_edge<128>(s, r, count, st, 24);
     case 33: return tune_unaligned_edge<128>(s, r, count, st, 32);
+    // aligned-vector walks (tune_unaligned_walk_vec_kernel): 40-43 W = 4 / 8 / 16 / 32 uncapped, 44-47 the same
+    // at 24 waves, 48-49 W = 8 / 16 at 16 waves, 50 W = 1 (one tile per wave, walk edges at every tile)
+    case 40: return tune_unaligned_walk_vec<float, kSum, 4>(s, r, count, st, 32);
+    case 41: return tune_unaligned_walk_vec<float, kSum, 8>(s, r, count, st, 32);
+    case 42: return tune_unaligned_walk_vec<float, kSum, 16>(s, r, count, st, 32);
+    case 43: return tune_unaligned_walk_vec<float, kSum, 32>(s, r, count, st, 32);
+    case 44: return tune_unaligned_walk_vec<float, kSum, 4>(s, r, count, st, 24);
+    case 45: return tune_unaligned_walk_vec<float, kSum, 8>(s, r, count, st, 24);
+    case 46: return tune_unaligned_walk_vec<float, kSum, 16>(s, r, count, st, 24);
+    case 47: return tune_unaligned_walk_vec<float, kSum, 32>(s, r, count, st, 24);
+    case 48: return tune_unaligned_walk_vec<float, kSum, 8>(s, r, count, st, 16);
+    case 49: return tune_unaligned_walk_vec<float, kSum, 16>(s, r, count, st, 16);
+    case 50: return tune_unaligned_walk_vec<float, kSum, 1>(s, r, count, st, 32);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
