@@ -615,6 +615,39 @@ def test_graph_capture_replay(dccl):
     assert torch.all(r == 20.0)
 
 
+def test_separate_allocations_capped_launch_eager_and_graph(dccl):
+    """Operands of >= 1 GiB in two allocations take the aligned launch under the 22-wave cap, chosen from a
+    hipMemGetAddressRange lookup of both operands on every call (local_reduce.hip, pair_occupancy_lds).  The
+    lookup must neither disturb a HIP-graph capture nor leave an error behind: eager, captured and replayed
+    results are checked exactly (integer Sum), and torch's error state stays clean."""
+    n = (1 << 30) // 4 + 7
+    s = torch.full((n,), 3, dtype=torch.int32, device="cuda")
+    r = torch.full((n,), 5, dtype=torch.int32, device="cuda")
+    assert dccl.local_reduce(s.data_ptr(), r.data_ptr(), 2, n, 0, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert int(r[0]) == 8 and int(r[-1]) == 8 and bool(torch.all(r == 8))
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=st):
+            assert dccl.local_reduce(s.data_ptr(), r.data_ptr(), 2, n, 0, st.cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert bool(torch.all(r == 8))  # capture does not execute
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    assert bool(torch.all(r == 14))
+    del g
+    # the pooled layout (one allocation) of the same size runs uncapped, same result
+    pool = torch.full((2 * n + 1024,), 5, dtype=torch.int32, device="cuda")
+    pool[n + 1024:] = 3
+    assert dccl.local_reduce(pool.data_ptr() + (n + 1024) * 4, pool.data_ptr(), 2, n, 0,
+                             torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert bool(torch.all(pool[:n] == 8)) and bool(torch.all(pool[n:n + 1024] == 5))
+
+
 def test_graph_capture_every_kernel_family(dccl):
     """Every launch path enqueues kernels only (no allocation, no host synchronisation), so each can be
     captured in one HIP graph and replayed: the pairwise combine with send off phase (shifted kernel) and
