@@ -23,7 +23,7 @@ Rank 0 prints ONE JSON line:
                    process may use (rank 0, N=1); nproc and the CPU model are stated
 Extra keys: c3 (BASELINE C3: 4 ops x fp16/bf16/fp32/int32/int64 at 1 GiB, timed and sample-verified) and
 c4 (BASELINE C4: fp32 Sum size sweep 4 KiB - 4 GiB, 21 points, operand sets rotated below a 512 MiB working
-set, per-launch duration eager and graph-replayed, fraction of HBM peak), rank 0 at N=1; payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
+set, per-launch duration eager from Python and from a C++ loop, and graph-replayed, fraction of HBM peak), rank 0 at N=1; payload_gib_s, host_staged (H2D+combine+D2H rate for host-resident operands,
 rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately),
 c5 (BASELINE config C5 on every run: --c5-gib GiB per operand sharded over the N GPUs, strong scaling,
 combine time and, N>1, the RCCL all-gather of the reduced shards),
@@ -414,7 +414,7 @@ def config_c4(dev, stream) -> list:
     duration of back-to-back launches (HIP events on the launch stream, >= ~20 ms of launches), the HBM rate
     3*bytes/t against the 8 TB/s roofline and the payload GiB/s; up to 64 MiB eager launches are
     host-issue-bound, so the same rotation is also replayed from a HIP graph (graph_us_per_launch,
-    graph_frac)."""
+    graph_frac) and issued eagerly from a C++ loop (native_c4: native_eager_us_per_launch, native_eager_frac)."""
     out = []
     top = 4 << 30
     pool = torch.empty(2 * top + PAIR_GAP, dtype=torch.uint8, device=dev)
@@ -441,7 +441,35 @@ def config_c4(dev, stream) -> list:
         out.append(row)
     del pool
     torch.cuda.empty_cache()
+    native = native_c4()
+    for row in out:
+        row.update(native.get(row["bytes_per_operand"], {}))
+    if "error" in native and out:
+        out[0]["native_eager_error"] = native["error"]
     return out
+
+
+def native_c4(max_log2: int = 26) -> dict:
+    """C4 up to 2^max_log2 bytes per operand issued from a C++ loop (dccl_amd/bin/c4_native, the same rotation
+    over operand sets): the eager per-launch time a native caller such as DCCL's ring step loop sees, without
+    the Python/ctypes issue cost of the `us_per_launch` column.  Runs as a child process; any failure is
+    reported, never fatal."""
+    import subprocess
+    binary = os.path.join(ROOT, "dccl_amd", "bin", "c4_native")
+    if not os.path.exists(binary):
+        return {"error": "dccl_amd/bin/c4_native missing"}
+    try:
+        p = subprocess.run([binary, str(max_log2)], capture_output=True, text=True, timeout=180)
+    except subprocess.TimeoutExpired:
+        return {"error": "c4_native timed out"}
+    res = {}
+    for line in p.stdout.splitlines():
+        if line.startswith("{"):
+            d = json.loads(line)
+            res[d["bytes_per_operand"]] = {k: d[k] for k in ("native_eager_us_per_launch", "native_eager_frac")}
+    if p.returncode != 0:
+        res["error"] = f"c4_native exited with {p.returncode}: {p.stderr[-200:]}"
+    return res
 
 
 def run_with_watchdog(fn, seconds: float):

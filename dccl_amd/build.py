@@ -7,7 +7,7 @@ fp32/fp16 denormals (SURVEY.md §7 "Bit-exact semantics").
 
 Tools-only artefacts, never linked into the product library: the tuning variants
 (tools/tune/tune_kernels.hip -> tools/lib/libdccl_amd_tune.so), the dccl_cli harness and the
-plain-C ABI check (dccl_amd/bin/).
+plain-C ABI check, the PMC and native C4 workloads of bench.py (dccl_amd/bin/).
 
     python dccl_amd/build.py [--force]      (by path: importing the package loads the library)
 """
@@ -31,6 +31,8 @@ C_CHECK_SRC = os.path.join(ROOT, "tools", "c_abi_check.c")
 C_CHECK = os.path.join(BIN_DIR, "c_abi_check")
 PMC_SRC = os.path.join(ROOT, "tools", "pmc_combine.cpp")
 PMC_BIN = os.path.join(BIN_DIR, "pmc_combine")
+C4_SRC = os.path.join(ROOT, "tools", "c4_native.cpp")
+C4_BIN = os.path.join(BIN_DIR, "c4_native")
 TUNE_DIR = os.path.join(ROOT, "tools", "tune")
 TUNE_SRC = os.path.join(TUNE_DIR, "tune_kernels.hip")
 TUNE_LIB = os.path.join(ROOT, "tools", "lib", "libdccl_amd_tune.so")
@@ -98,6 +100,11 @@ def build(force: bool = False) -> str:
     if force or not os.path.exists(PMC_BIN) or os.path.getmtime(PMC_BIN) < max(os.path.getmtime(LIB),
                                                                                 os.path.getmtime(PMC_SRC)):
         subprocess.run([HIPCC, *COMMON, PMC_SRC, "-o", PMC_BIN, f"-L{OUT_DIR}", "-ldccl_amd",
+                        "-Wl,-rpath,$ORIGIN/../lib"], check=True)
+    # BASELINE C4's small sizes issued from a native loop (bench.py's c4 leg, `native_eager_us_per_launch`)
+    if force or not os.path.exists(C4_BIN) or os.path.getmtime(C4_BIN) < max(os.path.getmtime(LIB),
+                                                                              os.path.getmtime(C4_SRC)):
+        subprocess.run([HIPCC, *COMMON, C4_SRC, "-o", C4_BIN, f"-L{OUT_DIR}", "-ldccl_amd",
                         "-Wl,-rpath,$ORIGIN/../lib"], check=True)
     # a plain C11 consumer of the C-ABI headers (gcc, no C++ / HIP headers)
     if force or not os.path.exists(C_CHECK) or os.path.getmtime(C_CHECK) < max(

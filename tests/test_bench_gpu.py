@@ -98,3 +98,4 @@ def test_bench_single_gpu_line():
     sizes = [r["bytes_per_operand"] for r in res["c4"]]
     assert sizes == [1 << e for e in range(12, 33)] and all(r["us_per_launch"] > 0 for r in res["c4"])
     assert all(r["graph_us_per_launch"] > 0 for r in res["c4"] if r["bytes_per_operand"] <= 64 << 20)
+    assert all(r["native_eager_us_per_launch"] > 0 for r in res["c4"] if r["bytes_per_operand"] <= 64 << 20)
