@@ -276,8 +276,8 @@ def misaligned(results, mib=1024):
                              (8, 4, "8/4-B offsets (shifted vector kernel, recv realigned)"),
                              (1, 0, "send at a byte offset, recv aligned (shifted vector kernel, byte phase)"),
                              (3, 0, "send at a byte offset, recv aligned (shifted vector kernel, byte phase)"),
-                             (1, 1, "byte offsets, recv element-misaligned (byte-gather kernel)"),
-                             (0, 2, "recv element-misaligned (byte-gather kernel)")):
+                             (1, 1, "byte offsets, recv element-misaligned (reduce_unaligned_kernel: 16-B accesses at the displaced addresses)"),
+                             (0, 2, "recv element-misaligned (reduce_unaligned_kernel: 16-B accesses at the displaced addresses)")):
         fn = lambda soff=soff, roff=roff: dccl_amd.local_reduce(s.data_ptr() + soff, r.data_ptr() + roff, 7, n, 0, st)
         med, _ = time_launches([fn], rounds=5)
         gbs = 3 * n * 4 / (med * 1e-3) / 1e9
