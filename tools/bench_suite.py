@@ -262,7 +262,7 @@ def c1(results):
 def misaligned(results, mib=1024):
     """Operands off their 128-B lines (vector kernel), off the 16-B phase of each other (shifted vector
     kernel), a send off element alignment (shifted kernel, byte phase) or a recv off element alignment
-    (byte-gather kernel), fp32 Sum, 1 GiB."""
+    (reduce_unaligned_kernel), fp32 Sum, 1 GiB."""
     st = torch.cuda.current_stream().cuda_stream
     nbytes = mib << 20
     n = nbytes // 4 - 4
