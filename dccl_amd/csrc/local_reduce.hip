@@ -54,18 +54,26 @@ size_t recv_align() {
     }();
     return v;
 }
-// Occupancy cap of the aligned pairwise launch, as bytes of (unused) dynamic LDS per one-wave block
-// (160 KiB / bytes resident waves per CU).  DCCL_REDUCE_LDS_CAP, read once per process, forces a value
-// (0 = uncapped).  Unset, the cap follows the operands' allocations:
-//   * both in ONE allocation (the bench's pooled pair): uncapped, 0.4-1.1 points faster than any cap;
-//   * in two allocations (DCCL's scratchpad + user chunk) of at least kSeparateCapBytes each: 22 waves
-//     per CU.  Paired A/B of the same pairs under every cap (tools/separate_cap_paired.py, 8 separate
-//     1 GiB pairs per run, profiles/r2_s61_separate_cap_paired*.json): median over pairs +0.6 to +1.0
-//     points at 1 GiB in four runs, +0.7 at 4 GiB, +0.5 at 512 MiB, but -0.8 at 256 MiB, hence the
-//     size floor.  Caps of 21-24 waves are equivalent; 20 and 26 lose.
+// Occupancy caps of the pairwise launches, as bytes of (unused) dynamic LDS per one-wave block (160 KiB /
+// bytes resident waves per CU).  DCCL_REDUCE_LDS_CAP, read once per process, forces a value for the vector
+// and shifted kernels (0 = uncapped).  Unset, the cap follows the operands' allocations:
+//   * both in ONE allocation (the bench's pooled pair): uncapped;
+//   * in two allocations (DCCL's scratchpad + user chunk) of at least kSeparateCapBytes each: the aligned
+//     vector kernel at 22 waves per CU, the shifted kernel at 26.  Paired A/B of the same pairs under every cap
+//     (tools/separate_cap_paired.py, 6-8 separate pairs per run, profiles/r2_s61_separate_cap_*.json,
+//     r2_s66_separate_cap_shift*.json), median over pairs against uncapped:
+//       aligned, 22 waves: +0.6 to +1.0 points at 1 GiB (six runs, three boxes), +0.7 at 2 and 4 GiB, +0.5 at
+//         512 MiB, -0.8 at 256 MiB; 21-24 waves are equivalent, 20 and 26 lose; the pooled pair loses
+//         0.4-1.1 points under any cap, so it stays uncapped;
+//       shifted (send at another 16-B phase), 26 waves: +1.0 to +1.25 points at 1 and 2 GiB (four runs, send
+//         nt or cached), +0.9 at 512 MiB, -0.9 at 256 MiB and -1.3 at 128 MiB; 25-27 waves are equivalent,
+//         24 and below lose; the pooled pair moves by -0.3 to +1.0.
+//   The line-straddling vector launch (StraddleCfg) gains nothing from any cap (+0.0 median) and stays
+//   uncapped.
 constexpr size_t kUnsetCap = ~size_t(0);
-constexpr size_t kSeparateCapBytes = size_t(1) << 30;
-constexpr size_t kSeparateLds = 7168;  // 22 waves per CU
+constexpr size_t kSeparateCapBytes = size_t(512) << 20;
+constexpr size_t kSeparateLds = 7168;       // aligned vector kernel: 22 waves per CU
+constexpr size_t kSeparateShiftLds = 6144;  // shifted kernel: 26 waves per CU
 size_t forced_occupancy_lds() {
     static const size_t v = [] {
         const char* e = std::getenv("DCCL_REDUCE_LDS_CAP");
@@ -75,7 +83,9 @@ size_t forced_occupancy_lds() {
     }();
     return v;
 }
-size_t pair_occupancy_lds(const void* send, const void* recv, size_t bytes) {
+// `lds` when send and recv lie in two allocations of at least kSeparateCapBytes each, else 0 (or the forced
+// value): one hipMemGetAddressRange per operand, only for launches that large.
+size_t pair_occupancy_lds(const void* send, const void* recv, size_t bytes, size_t lds) {
     const size_t forced = forced_occupancy_lds();
     if (forced != kUnsetCap) return forced;
     if (bytes < kSeparateCapBytes) return 0;
@@ -86,7 +96,7 @@ size_t pair_occupancy_lds(const void* send, const void* recv, size_t bytes) {
         (void)hipGetLastError();  // not runtime-allocated device memory: no cap, and no stale error left behind
         return 0;
     }
-    return bs == br ? 0 : kSeparateLds;
+    return bs == br ? 0 : lds;
 }
 template <typename T, int OP>
 int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream) {
@@ -104,23 +114,26 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
         return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<T, OP>), grid, args, stream, 64,
                       waves_lds(kUnalignedWaves));
     }
+    const size_t bytes = count * sizeof(T);
     if (as % sizeof(T)) {  // an element-aligned recv and a send at any byte address: the shifted kernel
         const Split sp = split_for_vectors<T>(ar, count, align);
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);
-        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, false>(s, r, count, stream, align)
-                         : launch_shift<T, OP, ShiftPolicy, false, 0, false>(s, r, count, stream, align);
+        const size_t lds = pair_occupancy_lds(send, recv, bytes, kSeparateShiftLds);
+        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, false>(s, r, count, stream, align, lds)
+                         : launch_shift<T, OP, ShiftPolicy, false, 0, false>(s, r, count, stream, align, lds);
     }
     const Split sp = split_for_vectors<T>(ar, count, align);
     if ((as ^ ar) & 15) {
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);  // the shifted kernel's send vectors
-        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false>(s, r, count, stream, align)
-                         : launch_shift<T, OP, ShiftPolicy, false>(s, r, count, stream, align);
+        const size_t lds = pair_occupancy_lds(send, recv, bytes, kSeparateShiftLds);
+        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false>(s, r, count, stream, align, lds)
+                         : launch_shift<T, OP, ShiftPolicy, false>(s, r, count, stream, align, lds);
     }
     if ((as ^ ar) & 127) {
         const size_t forced = forced_occupancy_lds();
         return launch_vec<T, OP, StraddleCfg>(s, r, sp, stream, 0, forced == kUnsetCap ? 0 : forced);
     }
-    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream, 0, pair_occupancy_lds(send, recv, count * sizeof(T)));
+    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream, 0, pair_occupancy_lds(send, recv, bytes, kSeparateLds));
 }
 
 // k-way combine: every resident wave keeps k+1 16-B loads per lane in flight, so the resident waves

@@ -639,6 +639,11 @@ def test_separate_allocations_capped_launch_eager_and_graph(dccl):
     torch.cuda.synchronize()
     assert bool(torch.all(r == 14))
     del g
+    # the shifted kernel (send at another 16-B phase) takes its own cap in two allocations: send 4 B further
+    r.fill_(5)
+    assert dccl.local_reduce(s.data_ptr() + 4, r.data_ptr(), 2, n - 1, 0, torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert bool(torch.all(r[:n - 1] == 8)) and int(r[n - 1]) == 5
     # the pooled layout (one allocation) of the same size runs uncapped, same result
     pool = torch.full((2 * n + 1024,), 5, dtype=torch.int32, device="cuda")
     pool[n + 1024:] = 3

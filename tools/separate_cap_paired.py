@@ -9,7 +9,7 @@ one-wave block (160 KiB / lds resident waves per CU).  Per pair and cap: median 
 the 8 TB/s HBM peak; per cap: the change against uncapped for every pair.  Column `product`: the
 shipped entry point dccl_local_reduce on the same pairs (its own cap choice, local_reduce.hip).
 
-    python tools/separate_cap_paired.py [--pairs 8] [--mib 1024] [--rounds 5] [--iters 10] [--out f.json]
+    python tools/separate_cap_paired.py [--kind aligned|straddle|shift] [--pairs 8] [--mib 1024] [--rounds 5] [--iters 10] [--out f.json]
 """
 import argparse
 import json
@@ -24,7 +24,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import dccl_amd  # noqa: E402
 from tools import tune_lib  # noqa: E402
 
-CAPS = {32: 0, 26: 6144, 24: 6656, 22: 7168, 21: 7680, 20: 8192}  # waves per CU -> LDS bytes per block
+CAPS = {32: 0, 27: 5888, 26: 6144, 25: 6400, 24: 6656, 22: 7168, 21: 7680, 20: 8192}  # waves per CU -> LDS bytes per block
 
 
 def main():
@@ -34,9 +34,14 @@ def main():
     p.add_argument("--iters", type=int, default=10)
     p.add_argument("--out", default="")
     p.add_argument("--mib", type=int, default=1024, help="bytes per operand, MiB")
+    p.add_argument("--kind", default="aligned", choices=["aligned", "straddle", "shift", "shift_straddle"],
+                   help="aligned: send and recv on equal 128-B phases (DefaultCfg); straddle: send 16 B further "
+                        "(StraddleCfg, send loads cached); shift: send 4 B further (the shifted kernel); shift_straddle: "
+                        "send 20 B further (the shifted kernel with cached send loads)")
     a = p.parse_args()
     nb = a.mib << 20
-    n = nb // 4
+    soff = {"aligned": 0, "straddle": 16, "shift": 4, "shift_straddle": 20}[a.kind]
+    n = nb // 4 - (16 if soff else 0)
     st = torch.cuda.current_stream().cuda_stream
     pairs, keep = [], []
     for j in range(a.pairs):
@@ -51,9 +56,16 @@ def main():
         dccl_amd.check(dccl_amd.synth_fill(ps, 7, n, 0, 0xDCC1, 2, st), "synth")
         dccl_amd.check(dccl_amd.synth_fill(pr, 7, n, 0, 0xDCC1, 1, st), "synth")
     tune = tune_lib.lib.dccl_tune_reduce_f32_sum_lds
+    straddle_variant = next(v for v, inf in enumerate(tune_lib.tune_variants())
+                            if (inf["block"], inf["unroll"], inf["policy"], inf["xcd"]) == (64, 1, 6, 0))
 
     def fn(ps, pr, n, v, cap, lds, st):  # lds None: the product entry point, which picks its own cap
-        return dccl_amd.local_reduce(ps, pr, 7, n, 0, st) if lds is None else tune(ps, pr, n, v, cap, lds, st)
+        ps += soff
+        if lds is None:
+            return dccl_amd.local_reduce(ps, pr, 7, n, 0, st)
+        if a.kind.startswith("shift"):
+            return tune_lib.lib.dccl_tune_shift_caps_f32_sum(ps, pr, n, lds, st)
+        return tune(ps, pr, n, straddle_variant if a.kind == "straddle" else v, cap, lds, st)
 
     caps = {**CAPS, "product": None}
     times = {(name, w): [] for name, _, _ in pairs for w in caps}
@@ -71,8 +83,8 @@ def main():
                 e1.record()
                 e1.synchronize()
                 times[(name, w)].append(e0.elapsed_time(e1) / a.iters)
-    frac = {k: 3 * nb / (statistics.median(v) * 1e-3) / 1e9 / 8000.0 for k, v in times.items()}
-    out = {"mib": a.mib, "pairs": {}, "by_cap": {}}
+    frac = {k: 3 * n * 4 / (statistics.median(v) * 1e-3) / 1e9 / 8000.0 for k, v in times.items()}
+    out = {"mib": a.mib, "kind": a.kind, "pairs": {}, "by_cap": {}}
     for name, _, _ in pairs:
         out["pairs"][name] = {str(w): round(frac[(name, w)], 4) for w in caps}
     seps = [name for name, _, _ in pairs if name != "pooled"]
