@@ -616,7 +616,8 @@ def test_graph_capture_replay(dccl):
 
 
 def test_separate_allocations_capped_launch_eager_and_graph(dccl):
-    """Operands of >= 1 GiB in two allocations take the aligned launch under the 22-wave cap, chosen from a
+    """Operands of >= 512 MiB in two allocations take the aligned launch under a 22-wave cap (the shifted one under
+    a 26-wave cap), chosen from a
     hipMemGetAddressRange lookup of both operands on every call (local_reduce.hip, pair_occupancy_lds).  The
     lookup must neither disturb a HIP-graph capture nor leave an error behind: eager, captured and replayed
     results are checked exactly (integer Sum), and torch's error state stays clean."""
