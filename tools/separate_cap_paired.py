@@ -34,13 +34,14 @@ def main():
     p.add_argument("--iters", type=int, default=10)
     p.add_argument("--out", default="")
     p.add_argument("--mib", type=int, default=1024, help="bytes per operand, MiB")
-    p.add_argument("--kind", default="aligned", choices=["aligned", "straddle", "shift", "shift_straddle"],
+    p.add_argument("--kind", default="aligned", choices=["aligned", "straddle", "shift", "shift_straddle", "group"],
                    help="aligned: send and recv on equal 128-B phases (DefaultCfg); straddle: send 16 B further "
                         "(StraddleCfg, send loads cached); shift: send 4 B further (the shifted kernel); shift_straddle: "
-                        "send 20 B further (the shifted kernel with cached send loads)")
+                        "send 20 B further (the shifted kernel with cached send loads); group: aligned, the shipped shape in "
+                        "the group-interleaved XCD tile order (dccl_tune_group_f32_sum)")
     a = p.parse_args()
     nb = a.mib << 20
-    soff = {"aligned": 0, "straddle": 16, "shift": 4, "shift_straddle": 20}[a.kind]
+    soff = {"aligned": 0, "straddle": 16, "shift": 4, "shift_straddle": 20, "group": 0}[a.kind]
     n = nb // 4 - (16 if soff else 0)
     st = torch.cuda.current_stream().cuda_stream
     pairs, keep = [], []
@@ -63,6 +64,8 @@ def main():
         ps += soff
         if lds is None:
             return dccl_amd.local_reduce(ps, pr, 7, n, 0, st)
+        if a.kind == "group":
+            return tune_lib.lib.dccl_tune_group_f32_sum(ps, pr, n, lds, st)
         if a.kind.startswith("shift"):
             return tune_lib.lib.dccl_tune_shift_caps_f32_sum(ps, pr, n, lds, st)
         return tune(ps, pr, n, straddle_variant if a.kind == "straddle" else v, cap, lds, st)

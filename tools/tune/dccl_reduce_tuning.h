@@ -32,6 +32,7 @@ int dccl_tune_skew_f32_sum(const void* send, void* recv, size_t count, int waves
 int dccl_tune_chain_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
                             size_t lds_bytes, void* stream);
 /* the misaligned-recv combine in shape `variant` 0-9 (see tune_kernels.hip) */
+int dccl_tune_group_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes, void* stream);
 int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t count, int variant, void* stream);
 int dccl_tune_multi_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, int variant,
                             size_t lds_bytes, void* stream);

@@ -61,6 +61,31 @@ extern "C" int dccl_tune_reduce_f32_sum_lds(const void* send, void* recv, size_t
                              lds_bytes);
 }
 
+// The shipped aligned shape (one-wave blocks, one 16-B vector per lane, every access non-temporal) in the
+// group-interleaved XCD tile order (xcd_group_tile: each XCD walks 8 consecutive tiles of every group of 64
+// blocks, one front for the chip).  recv and send must be 16-B aligned with count % 4 == 0 (no head / tail).
+namespace {
+__global__ __launch_bounds__(64) void tune_vec_group_kernel(const u32x4* __restrict__ vs, u32x4* __restrict__ vr,
+                                                            size_t nvec) {
+    const size_t ntiles = (nvec + 63) / 64;
+    for (size_t t = xcd_group_tile(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+        const size_t i = t * 64 + threadIdx.x;
+        if (i < nvec)
+            __builtin_nontemporal_store(combine16<float, kSum>(__builtin_nontemporal_load(vr + i),
+                                                               __builtin_nontemporal_load(vs + i)), vr + i);
+    }
+}
+}  // namespace
+extern "C" int dccl_tune_group_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes, void* stream) {
+    if (((reinterpret_cast<uintptr_t>(send) | reinterpret_cast<uintptr_t>(recv)) & 15) || (count & 3) ||
+        lds_bytes > (64u << 10))
+        return DCCL_INVALID_ARGUMENT;
+    size_t nvec = count / 4;
+    void* args[] = {&send, &recv, &nvec};
+    return launch(reinterpret_cast<const void*>(&tune_vec_group_kernel), ceil_div(nvec, size_t(64)), args,
+                  static_cast<hipStream_t>(stream), 64, lds_bytes);
+}
+
 extern "C" int dccl_tune_reduce_f32_sum(const void* send, void* recv, size_t count, int variant, size_t grid_cap,
                                         void* stream) {
     return dccl_tune_reduce_f32_sum_lds(send, recv, count, variant, grid_cap, 0, stream);
