@@ -25,6 +25,8 @@ import dccl_amd  # noqa: E402
 from tools import tune_lib  # noqa: E402
 
 CAPS = {32: 0, 27: 5888, 26: 6144, 25: 6400, 24: 6656, 22: 7168, 21: 7680, 20: 8192}  # waves per CU -> LDS bytes per block
+if os.environ.get("DCCL_PAIRED_CAPS") == "fine":  # 28-30 waves
+    CAPS = {32: 0, 30: 5376, 29: 5632, 28: 5760}  # nominal: LDS allocation granularity may merge some
 
 
 def main():
