@@ -654,6 +654,40 @@ def test_separate_allocations_capped_launch_eager_and_graph(dccl):
     assert bool(torch.all(pool[:n] == 8)) and bool(torch.all(pool[n:n + 1024] == 5))
 
 
+_FORCED_CAP_CHILD = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+import dccl_amd
+n = (512 << 20) // 4 + 5
+st = torch.cuda.current_stream().cuda_stream
+s = torch.full((n + 4,), 3, dtype=torch.int32, device="cuda")
+r = torch.full((n,), 5, dtype=torch.int32, device="cuda")
+assert dccl_amd.local_reduce(s.data_ptr(), r.data_ptr(), 2, n, 0, st) == 0        # aligned
+assert dccl_amd.local_reduce(s.data_ptr() + 4, r.data_ptr(), 2, n, 0, st) == 0    # shifted
+assert dccl_amd.local_reduce(s.data_ptr() + 16, r.data_ptr(), 2, n - 4, 0, st) == 0  # line-straddling send
+torch.cuda.synchronize()
+assert bool(torch.all(r[:n - 4] == 14)) and bool(torch.all(r[n - 4:] == 11))
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("cap", ["", "0", "7168", "20480"])
+def test_forced_occupancy_cap(dccl, cap):
+    """DCCL_REDUCE_LDS_CAP (read once per process, hence a child process per value) forces the occupancy cap of
+    the aligned, shifted and line-straddling pairwise launches: unset (the allocation rule), 0 (uncapped), 22 and
+    8 waves per CU.  512 MiB operands in two allocations, so the unset case takes the allocation lookup; every
+    result exact."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "DCCL_REDUCE_LDS_CAP"}
+    if cap:
+        env["DCCL_REDUCE_LDS_CAP"] = cap
+    p = subprocess.run([sys.executable, "-c", _FORCED_CAP_CHILD, root], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stderr[-2000:]
+
+
 def test_graph_capture_every_kernel_family(dccl):
     """Every launch path enqueues kernels only (no allocation, no host synchronisation), so each can be
     captured in one HIP graph and replayed: the pairwise combine with send off phase (shifted kernel) and
