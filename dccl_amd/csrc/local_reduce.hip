@@ -157,7 +157,7 @@ int launch_multi_vec(SendList sl, unsigned char* r, Split sp, hipStream_t stream
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, C>), grid, args, stream, C::BLOCK,
-                  multi_lds(K));
+                  multi_lds_for(K, sp.nvec * 16));
 }
 
 template <typename T, int OP>
@@ -233,7 +233,7 @@ int launch_chain_vec(SendList sl, const unsigned char* own, unsigned char* d, Sp
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_chain_vec_kernel<T, OP, K, C>), grid, args, stream, C::BLOCK,
-                  chain_lds(K));
+                  chain_lds_for(K, sp.nvec * 16));
 }
 
 template <typename T, int OP>

@@ -638,6 +638,40 @@ inline constexpr int kChainWaves[9] = {32, 32, 24, 20, 16, 13, 11, 10, 9};
 constexpr size_t chain_lds(int k) {
     return kChainWaves[k] >= 32 ? 0 : (kLdsPerCu / kChainWaves[k] + 255) / 256 * 256;
 }
+// The same launches on smaller operands: below 96 MiB per operand a launch has few tiles per resident wave,
+// the grid's tail dominates and more resident waves win.  Swept for k = 2..8 at 16, 32, 64 and 128 MiB per
+// operand (tools/kway_size_caps.py, operand sets rotated past the Infinity Cache, two runs agreeing within
+// 0.2 points, profiles/r2_s70_kway_size_caps_*.json): a class takes the best of {the 1 GiB cap, 16, 20, 24, 32}
+// where that gains at least a point, else the 1 GiB cap.  Gains over the 1 GiB caps: k-way +1 to +8 points
+// at 16-32 MiB and +2 to +3 at 64 MiB for k <= 3; chain +2 to +7 at 16 MiB, +1.3 to +5 at 32 MiB, +1.5 to
+// +3.7 at 64 MiB for k <= 3.  From 96 MiB (the 128 MiB class) the 1 GiB caps are best to within a point.
+// k-way k = 8 below 24 MiB takes 32 waves on a smaller lead (+0.6-0.8 at 16 MiB, +3.5 at 8 MiB).  The product
+// against the 1 GiB caps on the same operands (profiles/r2_s70_kway_size_caps_product.json): +1 to +8 points
+// wherever a class differs, within 0.3 points everywhere else.
+// Rows: operands below 24, 48 and 96 MiB.
+inline constexpr int kMultiWavesSmall[3][9] = {
+    {32, 32, 32, 24, 16, 16, 16, 16, 32},
+    {32, 32, 32, 20, 16, 16, 11, 10, 9},
+    {32, 32, 24, 16, 13, 11, 11, 10, 9},
+};
+inline constexpr int kChainWavesSmall[3][9] = {
+    {32, 32, 32, 32, 32, 24, 16, 16, 16},
+    {32, 32, 32, 32, 16, 16, 16, 16, 16},
+    {32, 32, 32, 24, 16, 13, 11, 10, 9},
+};
+inline int size_class(size_t bytes) {  // 0, 1, 2 for operands below 24, 48, 96 MiB; 3 from 96 MiB
+    return bytes < (size_t(24) << 20) ? 0 : bytes < (size_t(48) << 20) ? 1 : bytes < (size_t(96) << 20) ? 2 : 3;
+}
+inline size_t multi_lds_for(int k, size_t bytes) {
+    const int c = size_class(bytes);
+    const int w = c < 3 ? kMultiWavesSmall[c][k] : kMultiWaves[k];
+    return w >= 32 ? 0 : (kLdsPerCu / w + 255) / 256 * 256;
+}
+inline size_t chain_lds_for(int k, size_t bytes) {
+    const int c = size_class(bytes);
+    const int w = c < 3 ? kChainWavesSmall[c][k] : kChainWaves[k];
+    return w >= 32 ? 0 : (kLdsPerCu / w + 255) / 256 * 256;
+}
 // Caps of the line-straddling launches (in-phase sources off recv's 128-B lines, loaded through the
 // caches): swept on their own in round 2 (tools/phased_probe.py --straddle-caps, 1 GiB fp32 Sum, sources
 // at 16 (2j+1) B, profiles/r2_kway_straddle_caps.json).  The straddling loads want fewer waves than
