@@ -31,9 +31,9 @@ int launch_straddle(SendList sl, const unsigned char* own, unsigned char* d, Spl
     size_t grid = ceil_div(sp.nvec, size_t(64));
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
-    // the chain kernel's line-straddle caps (chain_straddle_lds, reduce_kernels.hpp)
+    // the chain kernel's line-straddle caps by operand size (chain_straddle_lds_for, reduce_kernels.hpp)
     return launch(reinterpret_cast<const void*>(&reduce_chain_vec_kernel<T, OP, K, StraddleKwayCfg>), grid, args, stream, 64,
-                  chain_straddle_lds(K));
+                  chain_straddle_lds_for(K, sp.nvec * 16));
 }
 
 }  // namespace

@@ -32,7 +32,7 @@ int launch_straddle(SendList sl, unsigned char* r, Split sp, hipStream_t stream)
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, StraddleKwayCfg>), grid, args, stream, 64,
-                  straddle_lds(K));
+                  straddle_lds_for(K, sp.nvec * 16));
 }
 
 }  // namespace

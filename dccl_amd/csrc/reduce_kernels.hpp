@@ -689,6 +689,30 @@ inline constexpr int kChainStraddleWaves[9] = {32, 32, 24, 18, 13, 13, 11, 10, 9
 constexpr size_t chain_straddle_lds(int k) {
     return kChainStraddleWaves[k] >= 32 ? 0 : (kLdsPerCu / kChainStraddleWaves[k] + 255) / 256 * 256;
 }
+// The line-straddling launches below 96 MiB per operand, by the same rule as kMultiWavesSmall /
+// kChainWavesSmall (tools/kway_size_caps.py --straddle, profiles/r2_s70_kway_size_caps_straddle.json): gains
+// over the 1 GiB caps of +2 to +6 points at 16 MiB, up to +5.6 at 32 MiB and +1.5 to +4.7 at 64 MiB.
+// Rows: operands below 24, 48 and 96 MiB.
+inline constexpr int kStraddleWavesSmall[3][9] = {
+    {32, 32, 32, 24, 16, 16, 16, 16, 32},
+    {32, 32, 24, 16, 13, 11, 16, 9, 32},
+    {32, 32, 24, 16, 13, 11, 9, 9, 7},
+};
+inline constexpr int kChainStraddleWavesSmall[3][9] = {
+    {32, 32, 32, 32, 24, 24, 16, 16, 16},
+    {32, 32, 32, 32, 24, 16, 11, 10, 9},
+    {32, 32, 32, 24, 16, 13, 11, 10, 9},
+};
+inline size_t straddle_lds_for(int k, size_t bytes) {
+    const int c = size_class(bytes);
+    const int w = c < 3 ? kStraddleWavesSmall[c][k] : kStraddleWaves[k];
+    return w >= 32 ? 0 : (kLdsPerCu / w + 255) / 256 * 256;
+}
+inline size_t chain_straddle_lds_for(int k, size_t bytes) {
+    const int c = size_class(bytes);
+    const int w = c < 3 ? kChainStraddleWavesSmall[c][k] : kChainStraddleWaves[k];
+    return w >= 32 ? 0 : (kLdsPerCu / w + 255) / 256 * 256;
+}
 
 constexpr size_t kMaxGrid = size_t(1) << 24;  // grid-stride beyond this (2^24 x 64 threads)
 

@@ -23,6 +23,8 @@ from tools import tune_lib  # noqa: E402
 
 MULTI_WAVES = [32, 32, 18, 13, 13, 11, 11, 10, 9]  # kMultiWaves, dccl_amd/csrc/reduce_kernels.hpp
 CHAIN_WAVES = [32, 32, 24, 20, 16, 13, 11, 10, 9]  # kChainWaves
+STRADDLE_WAVES = [32, 32, 18, 13, 13, 11, 9, 9, 7]  # kStraddleWaves
+CHAIN_STRADDLE_WAVES = [32, 32, 24, 18, 13, 13, 11, 10, 9]  # kChainStraddleWaves
 
 
 def lds_of(w: int) -> int:
@@ -36,8 +38,16 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--caps", default="16,32", help="wave caps timed beside the shipped one")
     p.add_argument("--product", action="store_true", help="also time the product entry points (their own caps)")
+    p.add_argument("--straddle", action="store_true",
+                   help="sources 16 (2j+1) B off recv's 128-B lines (the line-straddling launches: tune_multi variant 8, "
+                        "chain policy 6, caps kStraddleWaves / kChainStraddleWaves)")
     p.add_argument("--out", default="")
     a = p.parse_args()
+    global MULTI_WAVES, CHAIN_WAVES
+    soff = (lambda j: 16 * (2 * j + 1)) if a.straddle else (lambda j: 0)
+    variant, policy = (8, 6) if a.straddle else (0, 7)
+    if a.straddle:
+        MULTI_WAVES, CHAIN_WAVES = STRADDLE_WAVES, CHAIN_STRADDLE_WAVES
     st = torch.cuda.current_stream().cuda_stream
     gib = 1 << 30
     kmax = max(int(x) for x in a.ks.split(","))
@@ -52,11 +62,11 @@ def main():
         n = nb // 4
         sets = max(1, min(8, gib // nb))
         for k in (int(x) for x in a.ks.split(",")):
-            arrs = [(ctypes.c_void_p * k)(*[base[1 + j] + s * nb for j in range(k)]) for s in range(sets)]
-            lists = [[base[1 + j] + s * nb for j in range(k)] for s in range(sets)]
+            arrs = [(ctypes.c_void_p * k)(*[base[1 + j] + s * nb + soff(j) for j in range(k)]) for s in range(sets)]
+            lists = [[base[1 + j] + s * nb + soff(j) for j in range(k)] for s in range(sets)]
             dsts = [base[0] + s * nb for s in range(sets)]
             configs = []
-            for what, shipped in (("multi", MULTI_WAVES[k]), ("chain", CHAIN_WAVES[k])):
+            for what, shipped in (("multi", MULTI_WAVES[k]), ("chain", CHAIN_WAVES[k])):  # noqa: F821
                 for w in sorted({shipped, *(int(x) for x in a.caps.split(","))}):
                     configs.append((what, w))
                 if a.product:
@@ -74,9 +84,9 @@ def main():
                             rc = (dccl_amd.local_reduce_multi(lists[s], dsts[s], 7, n, 0, st) if what == "multi" else
                                   dccl_amd.local_reduce_chain(lists[s], dsts[s], dsts[s], 7, n, 0, st))
                         elif what == "multi":
-                            rc = multi(arrs[s], k, dsts[s], n, 0, lds, st)
+                            rc = multi(arrs[s], k, dsts[s], n, variant, lds, st)
                         else:
-                            rc = chain(arrs[s], k, dsts[s], dsts[s], n, lds, 7, st)
+                            rc = chain(arrs[s], k, dsts[s], dsts[s], n, lds, policy, st)
                         assert rc == 0, (what, k, w, rc)
                     e1.record()
                     e1.synchronize()
