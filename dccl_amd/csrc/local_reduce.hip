@@ -112,7 +112,7 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
         void* args[] = {const_cast<unsigned char**>(&s), &p, const_cast<unsigned char**>(&r),
                         const_cast<size_t*>(&nvec), &count};
         return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<T, OP>), grid, args, stream, 64,
-                      waves_lds(kUnalignedWaves));
+                      unaligned_lds_for(count * sizeof(T)));
     }
     const size_t bytes = count * sizeof(T);
     if (as % sizeof(T)) {  // an element-aligned recv and a send at any byte address: the shifted kernel

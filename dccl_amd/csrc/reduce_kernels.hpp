@@ -429,6 +429,11 @@ constexpr size_t waves_lds(int waves) { return waves >= 32 ? 0 : ((160u << 10) /
 // reduce_unaligned_kernel's wave cap: 1 GiB fp32 Sum, recv + 1 B, 76.7 % uncapped, 78.0 % at 26 waves,
 // 78.8 % at 24 and 22, 76.1 % at 20 (a cliff), both operand layouts (profiles/r2_misaligned_caps.json).
 inline constexpr int kUnalignedWaves = 24;
+// ... and by operand size, as the k-way caps (size_class below): uncapped below 48 MiB, 26 waves below 96 MiB.
+// recv +1 B, operand sets rotated past the Infinity Cache (tools/misaligned_size_caps.py,
+// profiles/r2_s70_misaligned_size_caps.json): 16 MiB 62.7 -> 66.4 %, 32 MiB 68.6 -> 71.6 %, 64 MiB 72.4 -> 74.0 %;
+// from 128 MiB the 24-wave cap is best.
+inline constexpr int kUnalignedWavesSmall[3] = {32, 32, 26};
 
 // The 16 body bytes of vector v (zero for v >= nvec) of an operand whose body starts at `body`,
 // phase p.  All 64 lanes must call it (p is uniform).
@@ -661,6 +666,10 @@ inline constexpr int kChainWavesSmall[3][9] = {
 };
 inline int size_class(size_t bytes) {  // 0, 1, 2 for operands below 24, 48, 96 MiB; 3 from 96 MiB
     return bytes < (size_t(24) << 20) ? 0 : bytes < (size_t(48) << 20) ? 1 : bytes < (size_t(96) << 20) ? 2 : 3;
+}
+inline size_t unaligned_lds_for(size_t bytes) {
+    const int c = size_class(bytes);
+    return waves_lds(c < 3 ? kUnalignedWavesSmall[c] : kUnalignedWaves);
 }
 inline size_t multi_lds_for(int k, size_t bytes) {
     const int c = size_class(bytes);
