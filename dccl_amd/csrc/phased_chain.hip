@@ -20,7 +20,7 @@ int launch_phased(SendList sl, PhaseList ph, const unsigned char* own, unsigned 
     // its own cap (kChainPhasedFirstWaves, reduce_kernels.hpp)
     if constexpr (kChainPhasedFirstWaves[K] != 0)
         return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K, false, true>), grid, args,
-                      stream, 64, waves_lds(kChainPhasedFirstWaves[K]));
+                      stream, 64, chain_phased_first_lds_for(K, sp.nvec * 16));
     return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K, (K <= kPhasedXcdMaxK)>), grid, args, stream, 64);
 }
 

@@ -20,7 +20,7 @@ int launch_phased(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStre
     // its own cap (kPhasedFirstWaves, reduce_kernels.hpp)
     if constexpr (kPhasedFirstWaves[K] != 0)
         return launch(reinterpret_cast<const void*>(&reduce_multi_phased_kernel<T, OP, K, false, true>), grid, args,
-                      stream, 64, waves_lds(kPhasedFirstWaves[K]));
+                      stream, 64, phased_first_lds_for(K, sp.nvec * 16));
     return launch(reinterpret_cast<const void*>(&reduce_multi_phased_kernel<T, OP, K, (K <= kPhasedXcdMaxK)>), grid, args, stream, 64);
 }
 

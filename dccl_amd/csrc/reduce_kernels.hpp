@@ -667,6 +667,27 @@ inline constexpr int kChainWavesSmall[3][9] = {
 inline int size_class(size_t bytes) {  // 0, 1, 2 for operands below 24, 48, 96 MiB; 3 from 96 MiB
     return bytes < (size_t(24) << 20) ? 0 : bytes < (size_t(48) << 20) ? 1 : bytes < (size_t(96) << 20) ? 2 : 3;
 }
+// The loads-first phased launches' caps by operand size (the k's of kPhasedFirstWaves / kChainPhasedFirstWaves;
+// tools/kway_size_caps.py --phased, sources 4 B off phase, profiles/r2_s70_kway_size_caps_phased.json): +1.3 to
+// +7.7 points at 16-32 MiB, chain k = 4 +2.1 at 64 MiB.  Rows: operands below 24, 48 and 96 MiB.
+inline constexpr int kPhasedFirstWavesSmall[3][9] = {
+    {0, 0, 0, 0, 0, 16, 0, 24, 16},
+    {0, 0, 0, 0, 0, 16, 0, 16, 24},
+    {0, 0, 0, 0, 0, 13, 0, 12, 11},
+};
+inline constexpr int kChainPhasedFirstWavesSmall[3][9] = {
+    {0, 0, 0, 0, 24, 24, 0, 24, 16},
+    {0, 0, 0, 0, 16, 16, 0, 16, 24},
+    {0, 0, 0, 0, 16, 13, 0, 11, 11},
+};
+inline size_t phased_first_lds_for(int k, size_t bytes) {
+    const int c = size_class(bytes);
+    return waves_lds(c < 3 ? kPhasedFirstWavesSmall[c][k] : kPhasedFirstWaves[k]);
+}
+inline size_t chain_phased_first_lds_for(int k, size_t bytes) {
+    const int c = size_class(bytes);
+    return waves_lds(c < 3 ? kChainPhasedFirstWavesSmall[c][k] : kChainPhasedFirstWaves[k]);
+}
 inline size_t unaligned_lds_for(size_t bytes) {
     const int c = size_class(bytes);
     return waves_lds(c < 3 ? kUnalignedWavesSmall[c] : kUnalignedWaves);

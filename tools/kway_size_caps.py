@@ -24,6 +24,8 @@ from tools import tune_lib  # noqa: E402
 MULTI_WAVES = [32, 32, 18, 13, 13, 11, 11, 10, 9]  # kMultiWaves, dccl_amd/csrc/reduce_kernels.hpp
 CHAIN_WAVES = [32, 32, 24, 20, 16, 13, 11, 10, 9]  # kChainWaves
 STRADDLE_WAVES = [32, 32, 18, 13, 13, 11, 9, 9, 7]  # kStraddleWaves
+PHASED_FIRST = [0, 0, 0, 0, 0, 13, 0, 12, 11]  # kPhasedFirstWaves (0: per-operand form, uncapped)
+CHAIN_PHASED_FIRST = [0, 0, 0, 0, 13, 13, 0, 11, 11]  # kChainPhasedFirstWaves
 CHAIN_STRADDLE_WAVES = [32, 32, 24, 18, 13, 13, 11, 10, 9]  # kChainStraddleWaves
 
 
@@ -38,16 +40,23 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--caps", default="16,32", help="wave caps timed beside the shipped one")
     p.add_argument("--product", action="store_true", help="also time the product entry points (their own caps)")
+    p.add_argument("--phased", action="store_true",
+                   help="sources 4 B off the destination's 16-B phase (the phased launches: the loads-first form under "
+                        "caps for k in kPhasedFirstWaves / kChainPhasedFirstWaves, else the per-operand form)")
     p.add_argument("--straddle", action="store_true",
                    help="sources 16 (2j+1) B off recv's 128-B lines (the line-straddling launches: tune_multi variant 8, "
                         "chain policy 6, caps kStraddleWaves / kChainStraddleWaves)")
     p.add_argument("--out", default="")
     a = p.parse_args()
     global MULTI_WAVES, CHAIN_WAVES
-    soff = (lambda j: 16 * (2 * j + 1)) if a.straddle else (lambda j: 0)
+    soff = (lambda j: 16 * (2 * j + 1)) if a.straddle else (lambda j: 4) if a.phased else (lambda j: 0)
     variant, policy = (8, 6) if a.straddle else (0, 7)
     if a.straddle:
         MULTI_WAVES, CHAIN_WAVES = STRADDLE_WAVES, CHAIN_STRADDLE_WAVES
+    if a.phased:
+        MULTI_WAVES = [w or 32 for w in PHASED_FIRST]
+        CHAIN_WAVES = [w or 32 for w in CHAIN_PHASED_FIRST]
+    prod = tune_lib.lib.dccl_tune_phased_prod_f32_sum
     st = torch.cuda.current_stream().cuda_stream
     gib = 1 << 30
     kmax = max(int(x) for x in a.ks.split(","))
@@ -83,6 +92,10 @@ def main():
                         if lds is None:
                             rc = (dccl_amd.local_reduce_multi(lists[s], dsts[s], 7, n, 0, st) if what == "multi" else
                                   dccl_amd.local_reduce_chain(lists[s], dsts[s], dsts[s], 7, n, 0, st))
+                        elif a.phased:
+                            first = int((PHASED_FIRST if what == "multi" else CHAIN_PHASED_FIRST)[k] != 0)
+                            rc = prod(arrs[s], k, None if what == "multi" else dsts[s], dsts[s], n, first,
+                                      int(not first and k <= 4), lds, st)
                         elif what == "multi":
                             rc = multi(arrs[s], k, dsts[s], n, variant, lds, st)
                         else:
