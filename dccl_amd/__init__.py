@@ -114,6 +114,7 @@ def _load():
         "dccl_all_gather": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, c_void_p]),
         "dccl_rccl_available": (c_int, []),
         "dccl_bootstrap_unique_id": (c_int, [ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
+        "dccl_bootstrap_done": (c_int, [ctypes.c_uint32, ctypes.c_uint32]),
         "dccl_synth_fill": (c_int, [c_void_p, c_int, c_size_t, c_int, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),
         "dccl_synth_fill_range": (c_int, [c_void_p, c_int, c_size_t, c_int, ctypes.c_uint64, ctypes.c_uint64,
                                           c_size_t, c_void_p]),
@@ -136,6 +137,7 @@ EXPORTED_SYMBOLS = [
     "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available", "dccl_bootstrap_unique_id",
     "dccl_synth_fill", "dccl_synth_fill_range", "dccl_local_reduce_chain", "dccl_copy_multi",
     "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_local_reduce_chain_host", "dccl_comm_init_p2p",
+    "dccl_bootstrap_done",
 ]
 
 

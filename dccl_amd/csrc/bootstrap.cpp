@@ -7,13 +7,27 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <map>
+#include <mutex>
 #include <sstream>
 #include <thread>
 
 namespace dccl_amd {
 namespace {
 
-constexpr const char* kMagic = "DCCLRDV1";
+constexpr const char* kMagic = "DCCLRDV2";
+
+// A publisher's stamp: pid, that process's start time, and the generation (how many times this process
+// has published to the path).  A reader remembers the last stamp it consumed per (path, reader), so a
+// second group formed under the same tag by the same live rank 0 is never joined with the previous id.
+struct Stamp {
+    long pid = 0;
+    unsigned long long start = 0, gen = 0;
+    bool operator==(const Stamp& o) const { return pid == o.pid && start == o.start && gen == o.gen; }
+};
+std::mutex g_mu;
+std::map<std::string, unsigned long long> g_published;  // path -> generations published by this process
+std::map<std::string, Stamp> g_consumed;                 // path#reader -> last stamp consumed
 
 // Start time of process `pid` in clock ticks since boot (/proc/<pid>/stat field 22), 0 if it is gone.
 unsigned long long proc_start_time(long pid) {
@@ -55,15 +69,13 @@ bool from_hex(const std::string& h, std::string* out) {
     return true;
 }
 
-// The payload of a file published by a live process for `world` ranks, or false.
-bool try_read(const std::string& path, uint32_t world, std::string* payload) {
+// The payload and stamp of a file published by a live process for `world` ranks, or false.
+bool try_read(const std::string& path, uint32_t world, std::string* payload, Stamp* st) {
     std::ifstream f(path);
     std::string magic, hex;
-    long pid = 0;
-    unsigned long long start = 0;
     uint32_t w = 0;
-    if (!(f >> magic >> pid >> start >> w >> hex) || magic != kMagic) return false;
-    if (w != world || pid <= 0 || start == 0 || proc_start_time(pid) != start) return false;  // stale
+    if (!(f >> magic >> st->pid >> st->start >> st->gen >> w >> hex) || magic != kMagic) return false;
+    if (w != world || st->pid <= 0 || st->start == 0 || proc_start_time(st->pid) != st->start) return false;  // stale
     return from_hex(hex, payload);
 }
 
@@ -86,10 +98,15 @@ dccl::ncclResult_t rdv_publish(const std::string& path, uint32_t world, const st
     const long pid = static_cast<long>(::getpid());
     const unsigned long long start = proc_start_time(pid);
     if (start == 0) return dccl::ncclSystemError;
+    unsigned long long gen = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        gen = ++g_published[path];
+    }
     const std::string tmp = path + ".tmp." + std::to_string(pid);
     {
         std::ofstream f(tmp, std::ios::trunc);
-        f << kMagic << ' ' << pid << ' ' << start << ' ' << world << ' ' << to_hex(payload) << '\n';
+        f << kMagic << ' ' << pid << ' ' << start << ' ' << gen << ' ' << world << ' ' << to_hex(payload) << '\n';
         if (!f) return dccl::ncclSystemError;
     }
     if (std::rename(tmp.c_str(), path.c_str()) != 0) {
@@ -99,10 +116,20 @@ dccl::ncclResult_t rdv_publish(const std::string& path, uint32_t world, const st
     return dccl::ncclSuccess;
 }
 
-dccl::ncclResult_t rdv_read(const std::string& path, uint32_t world, double timeout_s, std::string* payload) {
+dccl::ncclResult_t rdv_read(const std::string& path, uint32_t world, uint32_t reader, double timeout_s,
+                            std::string* payload) {
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+    const std::string key = path + "#" + std::to_string(reader);
     for (;;) {
-        if (try_read(path, world, payload)) return dccl::ncclSuccess;
+        Stamp st;
+        if (try_read(path, world, payload, &st)) {
+            std::lock_guard<std::mutex> lk(g_mu);
+            auto it = g_consumed.find(key);
+            if (it == g_consumed.end() || !(it->second == st)) {  // not the publication this reader already took
+                g_consumed[key] = st;
+                return dccl::ncclSuccess;
+            }
+        }
         if (std::chrono::steady_clock::now() >= deadline) return dccl::ncclSystemError;
         std::this_thread::sleep_for(std::chrono::milliseconds(10));
     }

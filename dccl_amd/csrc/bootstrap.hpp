@@ -11,6 +11,10 @@
 // gives up.  The publisher therefore stamps the file with its pid, that process's start time (field
 // 22 of /proc/<pid>/stat) and the world size; a reader accepts a file only while that very process is
 // alive and the world size matches.  Writes are atomic (temporary file + rename).
+// The same live rank 0 may form a second group under the same tag: the stamp also carries a generation
+// (the publisher's count of publications to that path), and a reader never takes the publication it
+// already consumed (per path and reader rank), so it waits for the republished id instead of joining a
+// finished bootstrap.
 #pragma once
 
 #include <cstdint>
@@ -25,8 +29,10 @@ std::string rdv_path(const char* prefix);
 // Poll limit of rdv_read: DCCL_BOOTSTRAP_TIMEOUT_S, default 120 s.
 double rdv_timeout_s();
 dccl::ncclResult_t rdv_publish(const std::string& path, uint32_t world, const std::string& payload);
-// Waits up to timeout_s for a file published by a live process for `world` ranks; ncclSystemError on timeout.
-dccl::ncclResult_t rdv_read(const std::string& path, uint32_t world, double timeout_s, std::string* payload);
+// Waits up to timeout_s for a file published by a live process for `world` ranks that `reader` (a rank) has
+// not consumed before; ncclSystemError on timeout.
+dccl::ncclResult_t rdv_read(const std::string& path, uint32_t world, uint32_t reader, double timeout_s,
+                            std::string* payload);
 void rdv_remove(const std::string& path);
 
 }  // namespace dccl_amd

@@ -1,0 +1,151 @@
+// dccl_amd/csrc/caps.hpp — resident-wave caps of every capped combine launch, in one table, and the one
+// function that selects them.  Pure host C++ (no HIP): tests/test_caps.py compiles it with g++ and checks
+// every entry; the static_asserts below check the table at every build.
+//
+// Why caps.  Every combine kernel is a one-wave (64-thread) block streaming 16-B vectors.  A CU holds up
+// to 32 such blocks; with k + 1 loads per lane in flight each, too many bytes are outstanding and the DRAM
+// serves the streams worse.  A launch asks for `bytes` of (unused) dynamic LDS per block, so a CU holds
+// floor(160 KiB / bytes) of them (lds_for_waves).  The values are NOMINAL wave counts: the 256-B rounding
+// of the LDS request makes some neighbours the same occupancy (8 and 9, 16 and 18).
+//
+// How they were chosen (profiles/): each entry is the best cap of a sweep of the launch at
+// that k, 1 GiB fp32 Sum per operand for the 1 GiB row, operand sets rotated past the Infinity Cache for
+// the size rows; a size-row entry differs from the 1 GiB row only where that gained at least one point.
+// Frozen from round 3: an entry changes only for a candidate that leads by >= 2 points on two boxes.
+#pragma once
+
+#include <cstddef>
+
+namespace dccl_amd {
+namespace caps {
+
+// Kernel classes that take a cap.  Values index kWaves.
+enum Kernel : int {
+    kMulti = 0,         // reduce_multi_vec_kernel, sources in phase and on recv's 128-B lines (k = 2..8)
+    kChain,             // reduce_chain_vec_kernel, the same (k = 1..8)
+    kMultiStraddle,     // reduce_multi_vec_kernel, in-phase sources off recv's lines (loaded through the caches)
+    kChainStraddle,     // reduce_chain_vec_kernel, the same
+    kMultiPhasedFirst,  // reduce_multi_phased_kernel, loads-first form; 0 = the per-operand form, uncapped
+    kChainPhasedFirst,  // reduce_chain_phased_kernel, the same
+    kUnaligned,         // reduce_unaligned_kernel (recv not element-aligned; pairwise, column k = 1)
+    kNumKernels
+};
+
+inline constexpr int kUncapped = 32;          // 32 one-wave blocks per CU: the hardware limit
+inline constexpr size_t kLdsPerCu = size_t(160) << 10;
+inline constexpr size_t kMaxLdsPerBlock = size_t(64) << 10;
+inline constexpr int kSizeClasses = 4;
+
+// Size class of a launch by bytes per operand: 0, 1, 2 below 24, 48 and 96 MiB, 3 (the 1 GiB-tuned row)
+// from 96 MiB.  Below 96 MiB a launch has few tiles per resident wave and its tail dominates, so more
+// resident waves win.
+constexpr int size_class(size_t bytes) {
+    return bytes < (size_t(24) << 20) ? 0 : bytes < (size_t(48) << 20) ? 1 : bytes < (size_t(96) << 20) ? 2 : 3;
+}
+
+// kWaves[kernel][size class][k]: nominal resident waves per CU (32 = uncapped; 0 = the kernel class is
+// not used at that k).  Evidence per row:
+//  kMulti      1 GiB: r1 sweep (+3-5 points over uncapped, r1_tune_multi_waves.json), r2 re-sweep at 1 GiB on
+//              both layouts found nothing 0.7 points better (r2_kway_waves.json); size rows: kway_size_caps.py,
+//              +1 to +8 points at 16-64 MiB (r2_s70_kway_size_caps_*.json, two sweeps within 0.2 points).
+//  kChain      as kMulti (r1_s5_chain_waves_sweep.json, r2_kway_waves.json, r2_s70_kway_size_caps_*.json).
+//  kMultiStraddle / kChainStraddle  phased_probe.py --straddle-caps (r2_kway_straddle_caps.json; A/B on a
+//              second box r2_kway_straddle_caps_ab.json: k-way k = 6 74.1 -> 79.0 %, chain k = 4 77.3 ->
+//              80.2 %); size rows r2_s70_kway_size_caps_straddle*.json.
+//  kMultiPhasedFirst / kChainPhasedFirst  the loads-first form wins from k = 5 (k-way) / k = 4 (chain)
+//              under these caps on two boxes (r2_phased_first_caps.json, r2_phased_first_ab.json); k = 6
+//              keeps the per-operand form (the two disagree in sign); size rows r2_s70_..._phased.json.
+//  kUnaligned  recv + 1 B: 76.7 % uncapped, 78.8 % at 24 waves, 76.1 % at 20 (r2_misaligned_caps.json);
+//              size rows r2_s70_misaligned_size_caps.json (16 MiB 62.7 -> 66.4 %).
+inline constexpr unsigned char kWaves[kNumKernels][kSizeClasses][9] = {
+    // k:  0   1   2   3   4   5   6   7   8
+    {{0, 0, 32, 24, 16, 16, 16, 16, 32},  // kMulti            < 24 MiB
+     {0, 0, 32, 20, 16, 16, 11, 10, 9},   //                   < 48 MiB
+     {0, 0, 24, 16, 13, 11, 11, 10, 9},   //                   < 96 MiB
+     {0, 0, 18, 13, 13, 11, 11, 10, 9}},  //                   from 96 MiB
+    {{0, 32, 32, 32, 32, 24, 16, 16, 16},  // kChain
+     {0, 32, 32, 32, 16, 16, 16, 16, 16},
+     {0, 32, 32, 24, 16, 13, 11, 10, 9},
+     {0, 32, 24, 20, 16, 13, 11, 10, 9}},
+    {{0, 0, 32, 24, 16, 16, 16, 16, 32},  // kMultiStraddle
+     {0, 0, 24, 16, 13, 11, 16, 9, 32},
+     {0, 0, 24, 16, 13, 11, 9, 9, 7},
+     {0, 0, 18, 13, 13, 11, 9, 9, 7}},
+    {{0, 32, 32, 32, 24, 24, 16, 16, 16},  // kChainStraddle
+     {0, 32, 32, 32, 24, 16, 11, 10, 9},
+     {0, 32, 32, 24, 16, 13, 11, 10, 9},
+     {0, 32, 24, 18, 13, 13, 11, 10, 9}},
+    {{0, 0, 0, 0, 0, 16, 0, 24, 16},  // kMultiPhasedFirst
+     {0, 0, 0, 0, 0, 16, 0, 16, 24},
+     {0, 0, 0, 0, 0, 13, 0, 12, 11},
+     {0, 0, 0, 0, 0, 13, 0, 12, 11}},
+    {{0, 0, 0, 0, 24, 24, 0, 24, 16},  // kChainPhasedFirst
+     {0, 0, 0, 0, 16, 16, 0, 16, 24},
+     {0, 0, 0, 0, 16, 13, 0, 11, 11},
+     {0, 0, 0, 0, 13, 13, 0, 11, 11}},
+    {{0, 32, 0, 0, 0, 0, 0, 0, 0},  // kUnaligned
+     {0, 32, 0, 0, 0, 0, 0, 0, 0},
+     {0, 26, 0, 0, 0, 0, 0, 0, 0},
+     {0, 24, 0, 0, 0, 0, 0, 0, 0}},
+};
+
+// The valid k range of each class (the launchers' with_k bounds).
+constexpr int min_k(Kernel c) { return c == kMulti || c == kMultiStraddle || c == kMultiPhasedFirst ? 2 : 1; }
+constexpr int max_k(Kernel c) { return c == kUnaligned ? 1 : 8; }
+
+// Nominal waves of a launch of class c with k sources and `bytes` per operand; -1 for a k outside the
+// class's range.  0 for the phased classes means "the per-operand form, uncapped".
+constexpr int waves(Kernel c, int k, size_t bytes) {
+    return (c < 0 || c >= kNumKernels || k < min_k(c) || k > max_k(c)) ? -1 : kWaves[c][size_class(bytes)][k];
+}
+
+// Dynamic LDS bytes per one-wave block for a nominal wave count (0 = no request: uncapped).
+constexpr size_t lds_for_waves(int w) { return (w <= 0 || w >= kUncapped) ? 0 : (kLdsPerCu / size_t(w) + 255) / 256 * 256; }
+
+// The LDS request of a launch (0 = uncapped, also for a k outside the class's range).
+constexpr size_t lds(Kernel c, int k, size_t bytes) { return lds_for_waves(waves(c, k, bytes)); }
+
+// Does the phased k-way (chain) launch with k sources take the loads-first form?  A compile-time choice
+// per K: the 1 GiB row decides (every size row agrees on which k are non-zero, checked below).
+constexpr bool phased_loads_first(bool chain, int k) {
+    return waves(chain ? kChainPhasedFirst : kMultiPhasedFirst, k, size_t(1) << 30) > 0;
+}
+
+// Pairwise launches: capped only when send and recv lie in two allocations of at least kSeparateCapBytes
+// each on the current device (DCCL's scratchpad + user chunk).  Paired A/B of the same pairs under every
+// cap (tools/separate_cap_paired.py, 6-8 separate pairs per run, profiles/r2_s61_separate_cap_*.json,
+// r2_s66_separate_cap_shift*.json), median pair against uncapped: aligned at 22 resident waves +0.6 to
+// +1.0 points at 1 GiB (six runs, three boxes), -0.8 at 256 MiB; shifted at 26 +1.0 to +1.25 (four runs);
+// one-allocation pairs lose 0.4-1.1 under any cap and stay uncapped.  The LDS bytes are the values measured.
+inline constexpr size_t kSeparateCapBytes = size_t(512) << 20;
+inline constexpr size_t kSeparateLds = 7168;       // aligned vector kernel: floor(160 KiB / 7168) = 22 waves
+inline constexpr size_t kSeparateShiftLds = 6144;  // shifted kernel: 26 waves
+
+constexpr size_t pair_lds(bool shifted, bool separate_allocations, size_t bytes) {
+    return (!separate_allocations || bytes < kSeparateCapBytes) ? 0 : shifted ? kSeparateShiftLds : kSeparateLds;
+}
+
+// ---- checks of the table, at every build ----
+constexpr bool table_ok() {
+    for (int c = 0; c < kNumKernels; ++c)
+        for (int s = 0; s < kSizeClasses; ++s)
+            for (int k = 0; k <= 8; ++k) {
+                const int w = kWaves[c][s][k];
+                const bool in_range = k >= min_k(Kernel(c)) && k <= max_k(Kernel(c));
+                const bool phased = c == kMultiPhasedFirst || c == kChainPhasedFirst;
+                if (!in_range && w != 0) return false;                                  // unused cells empty
+                if (in_range && !phased && (w < 7 || w > kUncapped)) return false;     // a legal cap
+                if (phased && w != 0 && (w < 7 || w > kUncapped)) return false;
+                if (phased && (w == 0) != (kWaves[c][3][k] == 0)) return false;         // one form per k
+                if (lds_for_waves(w) > kMaxLdsPerBlock) return false;
+            }
+    return true;
+}
+static_assert(table_ok(), "every cap is a legal LDS request and the phased form is fixed per k");
+static_assert(size_class((size_t(24) << 20) - 1) == 0 && size_class(size_t(24) << 20) == 1 &&
+                  size_class(size_t(48) << 20) == 2 && size_class(size_t(96) << 20) == 3,
+              "size-class boundaries at 24 / 48 / 96 MiB");
+static_assert(kLdsPerCu / kSeparateLds == 22 && kLdsPerCu / kSeparateShiftLds == 26, "pair caps");
+
+}  // namespace caps
+}  // namespace dccl_amd

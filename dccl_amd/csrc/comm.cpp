@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <thread>
 
 #include "dccl/dccl_reduce.h"
@@ -205,8 +206,13 @@ ncclResult_t ensure_work(dccl::dcclComm* c, size_t bytes, bool device) {
 }
 
 bool fault_injected(const char* site, uint32_t rank) {
-    const char* f = std::getenv("DCCL_FAULT_INJECT");
-    if (f == nullptr) return false;
+    // read once per process (the tests set it per child process): no getenv on the collectives' steps
+    static const std::string spec = [] {
+        const char* e = std::getenv("DCCL_FAULT_INJECT");
+        return std::string(e ? e : "");
+    }();
+    if (spec.empty()) return false;
+    const char* f = spec.c_str();
     const size_t n = std::strlen(site);
     return std::strncmp(f, site, n) == 0 && f[n] == ':' && std::strtoul(f + n + 1, nullptr, 10) == rank;
 }

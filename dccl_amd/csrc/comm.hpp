@@ -159,7 +159,7 @@ ncclResult_t ensure_work(dccl::dcclComm* c, size_t bytes, bool device);
 // Test-only fault injection: DCCL_FAULT_INJECT=<site>:<rank> makes `site` fail on that rank, so the
 // tests can check that one rank's failure reaches every member of the group (as an error) instead of
 // leaving peers blocked in a barrier.  Sites: join_events (group formation, dccl_api.cpp),
-// direct_combine (the combine step of the direct collectives, direct.cpp).
+// direct_combine (the combine step of the direct collectives, direct.cpp).  Read once per process.
 bool fault_injected(const char* site, uint32_t rank);
 
 // Local combine on either side of the host/device boundary.

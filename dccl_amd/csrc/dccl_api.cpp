@@ -233,7 +233,7 @@ ncclResult_t bootstrap_unique_id(uint32_t rank, uint32_t world, unsigned char* i
         return rdv_publish(path, world, std::string(reinterpret_cast<const char*>(id), kRcclUniqueIdBytes));
     }
     std::string payload;
-    const ncclResult_t rc = rdv_read(path, world, rdv_timeout_s(), &payload);
+    const ncclResult_t rc = rdv_read(path, world, rank, rdv_timeout_s(), &payload);
     if (rc != dccl::ncclSuccess) return rc;
     if (payload.size() != kRcclUniqueIdBytes) return dccl::ncclSystemError;
     std::memcpy(id, payload.data(), kRcclUniqueIdBytes);
@@ -686,4 +686,10 @@ extern "C" int dccl_rccl_available(void) { return rccl_available(); }
 extern "C" int dccl_bootstrap_unique_id(uint32_t rank, uint32_t world, void* id128) {
     if (id128 == nullptr || world == 0 || rank >= world) return DCCL_INVALID_ARGUMENT;
     return guarded([&] { return bootstrap_unique_id(rank, world, static_cast<unsigned char*>(id128)); });
+}
+
+extern "C" int dccl_bootstrap_done(uint32_t rank, uint32_t world) {
+    if (world == 0 || rank >= world) return DCCL_INVALID_ARGUMENT;
+    if (rank == 0) rdv_remove(rdv_path("dccl_rccl_uid_"));  // as ncclCommInit does once the group formed
+    return DCCL_SUCCESS;
 }

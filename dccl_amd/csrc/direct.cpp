@@ -263,7 +263,7 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(rdv_timeout_s());
         while (fd < 0) {
             const double left = std::chrono::duration<double>(deadline - std::chrono::steady_clock::now()).count();
-            if (left <= 0 || rdv_read(path, world, left, &name) != dccl::ncclSuccess) return dccl::ncclSystemError;
+            if (left <= 0 || rdv_read(path, world, rank, left, &name) != dccl::ncclSuccess) return dccl::ncclSystemError;
             fd = shm_open(name.c_str(), O_RDWR, 0600);
             if (fd < 0) std::this_thread::sleep_for(std::chrono::milliseconds(10));
         }

@@ -54,26 +54,13 @@ size_t recv_align() {
     }();
     return v;
 }
-// Occupancy caps of the pairwise launches, as bytes of (unused) dynamic LDS per one-wave block (160 KiB /
-// bytes resident waves per CU).  DCCL_REDUCE_LDS_CAP, read once per process, forces a value for the vector
-// and shifted kernels (0 = uncapped).  Unset, the cap follows the operands' allocations:
-//   * both in ONE allocation (the bench's pooled pair): uncapped;
-//   * in two allocations (DCCL's scratchpad + user chunk) of at least kSeparateCapBytes each: the aligned
-//     vector kernel at 22 waves per CU, the shifted kernel at 26.  Paired A/B of the same pairs under every cap
-//     (tools/separate_cap_paired.py, 6-8 separate pairs per run, profiles/r2_s61_separate_cap_*.json,
-//     r2_s66_separate_cap_shift*.json), median over pairs against uncapped:
-//       aligned, 22 waves: +0.6 to +1.0 points at 1 GiB (six runs, three boxes), +0.7 at 2 and 4 GiB, +0.5 at
-//         512 MiB, -0.8 at 256 MiB; 21-24 waves are equivalent, 20 and 26 lose; the pooled pair loses
-//         0.4-1.1 points under any cap, so it stays uncapped;
-//       shifted (send at another 16-B phase), 26 waves: +1.0 to +1.25 points at 1 and 2 GiB (four runs, send
-//         nt or cached), +0.9 at 512 MiB, -0.9 at 256 MiB and -1.3 at 128 MiB; 25-27 waves are equivalent,
-//         24 and below lose; the pooled pair moves by -0.3 to +1.0.
-//   The line-straddling vector launch (StraddleCfg) gains nothing from any cap (+0.0 median) and stays
-//   uncapped.
+// Occupancy caps of the pairwise launches, as bytes of (unused) dynamic LDS per one-wave block (caps.hpp:
+// caps::pair_lds, with the measurements behind it).  DCCL_REDUCE_LDS_CAP, read once per process, forces a
+// value for the vector and shifted kernels (0 = uncapped).  Unset, the cap follows the operands' allocations:
+// uncapped for one allocation (the bench's pooled pair), capped for two allocations of at least 512 MiB on
+// the current device.  The line-straddling vector launch (StraddleCfg) gains nothing from any cap (+0.0
+// median) and stays uncapped.
 constexpr size_t kUnsetCap = ~size_t(0);
-constexpr size_t kSeparateCapBytes = size_t(512) << 20;
-constexpr size_t kSeparateLds = 7168;       // aligned vector kernel: 22 waves per CU
-constexpr size_t kSeparateShiftLds = 6144;  // shifted kernel: 26 waves per CU
 size_t forced_occupancy_lds() {
     static const size_t v = [] {
         const char* e = std::getenv("DCCL_REDUCE_LDS_CAP");
@@ -83,12 +70,25 @@ size_t forced_occupancy_lds() {
     }();
     return v;
 }
-// `lds` when send and recv lie in two allocations of at least kSeparateCapBytes each, else 0 (or the forced
-// value): one hipMemGetAddressRange per operand, only for launches that large.
-size_t pair_occupancy_lds(const void* send, const void* recv, size_t bytes, size_t lds) {
+// True when p is device memory of the current device (not a peer GPU's buffer, an IPC import or host memory).
+bool on_current_device(const void* p) {
+    int dev = -1;
+    hipPointerAttribute_t at{};
+    if (hipGetDevice(&dev) != hipSuccess || hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice && at.device == dev;
+}
+// The pairwise launch's LDS request (the forced value, or caps::pair_lds): whether send and recv lie in two
+// allocations on the current device costs one hipPointerGetAttributes and one hipMemGetAddressRange per
+// operand, only for launches of at least caps::kSeparateCapBytes.  The caps were measured on two local HBM
+// allocations; reads of a peer's buffer over xGMI (the direct collectives' W = 2 step) stay uncapped.
+size_t pair_occupancy_lds(const void* send, const void* recv, size_t bytes, bool shifted) {
     const size_t forced = forced_occupancy_lds();
     if (forced != kUnsetCap) return forced;
-    if (bytes < kSeparateCapBytes) return 0;
+    if (bytes < caps::kSeparateCapBytes) return 0;
+    if (!on_current_device(send) || !on_current_device(recv)) return 0;
     hipDeviceptr_t bs = nullptr, br = nullptr;
     size_t ls = 0, lr = 0;
     if (hipMemGetAddressRange(&bs, &ls, const_cast<void*>(send)) != hipSuccess ||
@@ -96,7 +96,7 @@ size_t pair_occupancy_lds(const void* send, const void* recv, size_t bytes, size
         (void)hipGetLastError();  // not runtime-allocated device memory: no cap, and no stale error left behind
         return 0;
     }
-    return bs == br ? 0 : lds;
+    return caps::pair_lds(shifted, bs != br, bytes);
 }
 template <typename T, int OP>
 int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream) {
@@ -112,20 +112,20 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
         void* args[] = {const_cast<unsigned char**>(&s), &p, const_cast<unsigned char**>(&r),
                         const_cast<size_t*>(&nvec), &count};
         return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<T, OP>), grid, args, stream, 64,
-                      unaligned_lds_for(count * sizeof(T)));
+                      caps::lds(caps::kUnaligned, 1, count * sizeof(T)));
     }
     const size_t bytes = count * sizeof(T);
     if (as % sizeof(T)) {  // an element-aligned recv and a send at any byte address: the shifted kernel
         const Split sp = split_for_vectors<T>(ar, count, align);
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);
-        const size_t lds = pair_occupancy_lds(send, recv, bytes, kSeparateShiftLds);
+        const size_t lds = pair_occupancy_lds(send, recv, bytes, true);
         return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, false>(s, r, count, stream, align, lds)
                          : launch_shift<T, OP, ShiftPolicy, false, 0, false>(s, r, count, stream, align, lds);
     }
     const Split sp = split_for_vectors<T>(ar, count, align);
     if ((as ^ ar) & 15) {
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);  // the shifted kernel's send vectors
-        const size_t lds = pair_occupancy_lds(send, recv, bytes, kSeparateShiftLds);
+        const size_t lds = pair_occupancy_lds(send, recv, bytes, true);
         return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false>(s, r, count, stream, align, lds)
                          : launch_shift<T, OP, ShiftPolicy, false>(s, r, count, stream, align, lds);
     }
@@ -133,7 +133,7 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
         const size_t forced = forced_occupancy_lds();
         return launch_vec<T, OP, StraddleCfg>(s, r, sp, stream, 0, forced == kUnsetCap ? 0 : forced);
     }
-    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream, 0, pair_occupancy_lds(send, recv, bytes, kSeparateLds));
+    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream, 0, pair_occupancy_lds(send, recv, bytes, false));
 }
 
 // k-way combine: every resident wave keeps k+1 16-B loads per lane in flight, so the resident waves
@@ -157,7 +157,7 @@ int launch_multi_vec(SendList sl, unsigned char* r, Split sp, hipStream_t stream
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, C>), grid, args, stream, C::BLOCK,
-                  multi_lds_for(K, sp.nvec * 16));
+                  caps::lds(caps::kMulti, K, sp.nvec * 16));
 }
 
 template <typename T, int OP>
@@ -233,7 +233,7 @@ int launch_chain_vec(SendList sl, const unsigned char* own, unsigned char* d, Sp
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_chain_vec_kernel<T, OP, K, C>), grid, args, stream, C::BLOCK,
-                  chain_lds_for(K, sp.nvec * 16));
+                  caps::lds(caps::kChain, K, sp.nvec * 16));
 }
 
 template <typename T, int OP>

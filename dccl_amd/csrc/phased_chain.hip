@@ -17,10 +17,10 @@ int launch_phased(SendList sl, PhaseList ph, const unsigned char* own, unsigned 
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &ph, &own, &d, &sp.head, &sp.nvec, &sp.tail};
     // the per-operand form uncapped (with the XCD order up to kPhasedXcdMaxK), or the loads-first form under
-    // its own cap (kChainPhasedFirstWaves, reduce_kernels.hpp)
-    if constexpr (kChainPhasedFirstWaves[K] != 0)
+    // its own cap (caps::kChainPhasedFirst, caps.hpp)
+    if constexpr (caps::phased_loads_first(true, K))
         return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K, false, true>), grid, args,
-                      stream, 64, chain_phased_first_lds_for(K, sp.nvec * 16));
+                      stream, 64, caps::lds(caps::kChainPhasedFirst, K, sp.nvec * 16));
     return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K, (K <= kPhasedXcdMaxK)>), grid, args, stream, 64);
 }
 
@@ -31,9 +31,9 @@ int launch_straddle(SendList sl, const unsigned char* own, unsigned char* d, Spl
     size_t grid = ceil_div(sp.nvec, size_t(64));
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
-    // the chain kernel's line-straddle caps by operand size (chain_straddle_lds_for, reduce_kernels.hpp)
+    // the chain kernel's line-straddle caps by operand size (caps::kChainStraddle, caps.hpp)
     return launch(reinterpret_cast<const void*>(&reduce_chain_vec_kernel<T, OP, K, StraddleKwayCfg>), grid, args, stream, 64,
-                  chain_straddle_lds_for(K, sp.nvec * 16));
+                  caps::lds(caps::kChainStraddle, K, sp.nvec * 16));
 }
 
 }  // namespace

@@ -17,10 +17,10 @@ int launch_phased(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStre
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &ph, &r, &sp.head, &sp.nvec, &sp.tail};
     // the per-operand form uncapped (with the XCD order up to kPhasedXcdMaxK), or the loads-first form under
-    // its own cap (kPhasedFirstWaves, reduce_kernels.hpp)
-    if constexpr (kPhasedFirstWaves[K] != 0)
+    // its own cap (caps::kMultiPhasedFirst, caps.hpp)
+    if constexpr (caps::phased_loads_first(false, K))
         return launch(reinterpret_cast<const void*>(&reduce_multi_phased_kernel<T, OP, K, false, true>), grid, args,
-                      stream, 64, phased_first_lds_for(K, sp.nvec * 16));
+                      stream, 64, caps::lds(caps::kMultiPhasedFirst, K, sp.nvec * 16));
     return launch(reinterpret_cast<const void*>(&reduce_multi_phased_kernel<T, OP, K, (K <= kPhasedXcdMaxK)>), grid, args, stream, 64);
 }
 
@@ -32,7 +32,7 @@ int launch_straddle(SendList sl, unsigned char* r, Split sp, hipStream_t stream)
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, StraddleKwayCfg>), grid, args, stream, 64,
-                  straddle_lds_for(K, sp.nvec * 16));
+                  caps::lds(caps::kMultiStraddle, K, sp.nvec * 16));
 }
 
 }  // namespace

@@ -10,6 +10,7 @@
 #include <cstddef>
 #include <cstdint>
 
+#include "caps.hpp"
 #include "combine.hpp"
 #include "dccl/dccl_reduce.h"
 
@@ -165,7 +166,6 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, unsigned b) {
 // verified on gfx950 by tools/dpp_probe.hip: wave_rol:1 (0x134) gives lane l lane (l+1) % 64's value,
 // wave_shl:1 (0x130) the same except that lane 63 keeps `old`; wave_ror:1 (0x13C) gives lane l lane
 // (l+63) % 64's value, wave_shr:1 (0x138) the same except that lane 0 keeps `old`.
-// DCCL_LANE_SHIFT_BPERMUTE selects the round-1 ds_bpermute form (tuning A/B only).
 template <int CTRL>
 __device__ __forceinline__ u32x4 dpp16(u32x4 x, u32x4 old) {
     u32x4 o;
@@ -175,49 +175,14 @@ __device__ __forceinline__ u32x4 dpp16(u32x4 x, u32x4 old) {
     o.w = unsigned(__builtin_amdgcn_update_dpp(int(old.w), int(x.w), CTRL, 0xF, 0xF, false));
     return o;
 }
-__device__ __forceinline__ u32x4 bpermute16(u32x4 x, int src_lane) {
-    const int a = src_lane << 2;
-    u32x4 o;
-    o.x = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.x)));
-    o.y = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.y)));
-    o.z = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.z)));
-    o.w = unsigned(__builtin_amdgcn_ds_bpermute(a, int(x.w)));
-    return o;
-}
 // lane l receives lane (l+1) % 64's vector
-__device__ __forceinline__ u32x4 from_next_lane(u32x4 x) {
-#ifdef DCCL_LANE_SHIFT_BPERMUTE
-    return bpermute16(x, int((threadIdx.x + 1) & 63));
-#else
-    return dpp16<0x134>(x, x);
-#endif
-}
+__device__ __forceinline__ u32x4 from_next_lane(u32x4 x) { return dpp16<0x134>(x, x); }
 // lane l < 63 receives lane l+1's x, lane 63 keeps its own `last`
-__device__ __forceinline__ u32x4 from_next_lane_or(u32x4 x, u32x4 last) {
-#ifdef DCCL_LANE_SHIFT_BPERMUTE
-    const u32x4 o = bpermute16(x, int((threadIdx.x + 1) & 63));
-    return (threadIdx.x & 63) == 63 ? last : o;
-#else
-    return dpp16<0x130>(x, last);
-#endif
-}
+__device__ __forceinline__ u32x4 from_next_lane_or(u32x4 x, u32x4 last) { return dpp16<0x130>(x, last); }
 // lane l receives lane (l+63) % 64's vector
-__device__ __forceinline__ u32x4 from_prev_lane(u32x4 x) {
-#ifdef DCCL_LANE_SHIFT_BPERMUTE
-    return bpermute16(x, int((threadIdx.x + 63) & 63));
-#else
-    return dpp16<0x13C>(x, x);
-#endif
-}
+__device__ __forceinline__ u32x4 from_prev_lane(u32x4 x) { return dpp16<0x13C>(x, x); }
 // lane l > 0 receives lane l-1's x, lane 0 keeps its own `first`
-__device__ __forceinline__ u32x4 from_prev_lane_or(u32x4 x, u32x4 first) {
-#ifdef DCCL_LANE_SHIFT_BPERMUTE
-    const u32x4 o = bpermute16(x, int((threadIdx.x + 63) & 63));
-    return (threadIdx.x & 63) == 0 ? first : o;
-#else
-    return dpp16<0x138>(x, first);
-#endif
-}
+__device__ __forceinline__ u32x4 from_prev_lane_or(u32x4 x, u32x4 first) { return dpp16<0x138>(x, first); }
 
 template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true>
 __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* __restrict__ send,
@@ -263,7 +228,7 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
 // reads it (aligned loads, lane exchange, funnel shift by its own phase): unaligned send loads as well
 // cost a further 7-10 points.  A 1 KiB tile spans 9 lines of recv, one shared with the next tile;
 // consecutive tiles go to one XCD (blocks are dealt round-robin over the 8 XCDs), so the shared lines meet
-// in one L2.  1 GiB fp32 Sum on MI355X, recv + 1 B: 78.4-78.8 % of HBM peak under the kUnalignedWaves cap
+// in one L2.  1 GiB fp32 Sum on MI355X, recv + 1 B: 78.4-78.8 % of HBM peak under the caps::kUnaligned cap
 // (76.4-76.7 % uncapped), against 74.6-74.8 % with consecutive tiles on different XCDs and 72-73 % for a
 // byte-gather kernel; a two-pass form writing every recv vector whole from one wave reached 74-75.5 %
 // (tools/tune/, profiles/r2_misaligned_ab.json, r2_misaligned_caps.json).  The tail (< V elements) is
@@ -374,7 +339,7 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sen
 // operand's loads before the first shift (branch-free selects) and the k-way kernel's wave caps:
 // 74-79 % of HBM peak for k = 1..7 against 45-61 %.  Round 2: the loads-first form with the same
 // uniform-branch shifts, under caps of its own, wins from k = 5 (k-way) / k = 4 (chain); see
-// kPhasedFirstWaves below and DESIGN.md §12.
+// caps::kMultiPhasedFirst (caps.hpp) and DESIGN.md §12.
 // One-wave blocks and a per-tile loop uniform per wave: every lane reaches the lane exchange.
 // ---------------------------------------------------------------------------------
 struct PhaseList { unsigned p[9]; };
@@ -414,26 +379,9 @@ __device__ __forceinline__ u32x4 ld_phased_finish(const PhasedLoad& x, unsigned 
 inline constexpr int kPhasedXcdMaxK = 4;
 // From k = 5 (k-way) / k = 4 (chain) the phased kernels take the loads-first form (every operand's loads
 // issued before the first shift, ld_phased_issue / ld_phased_finish) under a wave cap of their own
-// (0 = the per-operand form above, uncapped).  Without a cap the loads-first form loses (too many streams
-// in flight), with a cap of 11-13 waves it wins: 1 GiB fp32 Sum, sources 4 B off phase
-// (tools/phased_probe.py --prod-caps, profiles/r2_phased_first_caps.json): k-way k = 5 76.4 -> 78.8 %,
-// k = 7 77.4 -> 78.8 %, k = 8 72.7 -> 78.4 %; chain k = 4 77.7 -> 79.5 %, k = 5 77.1 -> 80.1 %, k = 7
-// 73.6 -> 78.5 %, k = 8 72.0 -> 78.1 %; A/B of the two builds on another box
-// (profiles/r2_phased_first_ab.json): k-way k = 5 76.8 -> 78.7 %, k = 8 74.1 -> 78.8 %; chain k = 4
-// 78.2 -> 79.1 %, k = 7 74.8 -> 79.0 %, k = 8 73.6 -> 79.3 %.  k = 6 stays on the per-operand form (the
-// two measurements disagree in sign, within a point), and so do k <= 4 (k-way) / k <= 3 (chain), where
-// the per-operand form with the XCD order is ahead.
-inline constexpr int kPhasedFirstWaves[9] = {0, 0, 0, 0, 0, 13, 0, 12, 11};
-inline constexpr int kChainPhasedFirstWaves[9] = {0, 0, 0, 0, 13, 13, 0, 11, 11};
-constexpr size_t waves_lds(int waves) { return waves >= 32 ? 0 : ((160u << 10) / waves + 255) / 256 * 256; }
-// reduce_unaligned_kernel's wave cap: 1 GiB fp32 Sum, recv + 1 B, 76.7 % uncapped, 78.0 % at 26 waves,
-// 78.8 % at 24 and 22, 76.1 % at 20 (a cliff), both operand layouts (profiles/r2_misaligned_caps.json).
-inline constexpr int kUnalignedWaves = 24;
-// ... and by operand size, as the k-way caps (size_class below): uncapped below 48 MiB, 26 waves below 96 MiB.
-// recv +1 B, operand sets rotated past the Infinity Cache (tools/misaligned_size_caps.py,
-// profiles/r2_s70_misaligned_size_caps.json): 16 MiB 62.7 -> 66.4 %, 32 MiB 68.6 -> 71.6 %, 64 MiB 72.4 -> 74.0 %;
-// from 128 MiB the 24-wave cap is best.
-inline constexpr int kUnalignedWavesSmall[3] = {32, 32, 26};
+// (caps::kMultiPhasedFirst / kChainPhasedFirst in caps.hpp); below, and at k = 6, the per-operand form
+// above, uncapped.  Without a cap the loads-first form loses (too many streams in flight); with 11-13 waves it
+// wins by 1.5-6 points at k = 5, 7, 8.
 
 // The 16 body bytes of vector v (zero for v >= nvec) of an operand whose body starts at `body`,
 // phase p.  All 64 lanes must call it (p is uniform).
@@ -629,121 +577,6 @@ __global__ __launch_bounds__(64) void reduce_chain_unaligned_kernel(SendList sen
 // ---------------------------------------------------------------------------------
 // Host-side launch helpers
 // ---------------------------------------------------------------------------------
-inline constexpr int kMultiWaves[9] = {32, 32, 18, 13, 13, 11, 11, 10, 9};
-inline constexpr size_t kLdsPerCu = 160u << 10;
-constexpr size_t multi_lds(int k) {
-    return kMultiWaves[k] >= 32 ? 0 : (kLdsPerCu / kMultiWaves[k] + 255) / 256 * 256;
-}
-// The chain kernel's own caps (K sources + own, one store), used by its in-phase launch and by its
-// line-straddling launch alike: first swept at 256 MiB per operand (profiles/r1_s5_chain_waves_sweep.json,
-// k = 2 79.5 -> 82.2 % with 24 waves instead of 18); re-swept for every k at 1 GiB in round 2, both
-// kernels and both operand layouts (tools/kway_waves.py, profiles/r2_kway_waves.json): no cap beat the
-// shipped ones by more than 0.7 points at any k, and every k runs at >= 80.1 % of (k+2)N.
-inline constexpr int kChainWaves[9] = {32, 32, 24, 20, 16, 13, 11, 10, 9};
-constexpr size_t chain_lds(int k) {
-    return kChainWaves[k] >= 32 ? 0 : (kLdsPerCu / kChainWaves[k] + 255) / 256 * 256;
-}
-// The same launches on smaller operands: below 96 MiB per operand a launch has few tiles per resident wave,
-// the grid's tail dominates and more resident waves win.  Swept for k = 2..8 at 16, 32, 64 and 128 MiB per
-// operand (tools/kway_size_caps.py, operand sets rotated past the Infinity Cache, two runs agreeing within
-// 0.2 points, profiles/r2_s70_kway_size_caps_*.json): a class takes the best of {the 1 GiB cap, 16, 20, 24, 32}
-// where that gains at least a point, else the 1 GiB cap.  Gains over the 1 GiB caps: k-way +1 to +8 points
-// at 16-32 MiB and +2 to +3 at 64 MiB for k <= 3; chain +2 to +7 at 16 MiB, +1.3 to +5 at 32 MiB, +1.5 to
-// +3.7 at 64 MiB for k <= 3.  From 96 MiB (the 128 MiB class) the 1 GiB caps are best to within a point.
-// k-way k = 8 below 24 MiB takes 32 waves on a smaller lead (+0.6-0.8 at 16 MiB, +3.5 at 8 MiB).  The product
-// against the 1 GiB caps on the same operands (profiles/r2_s70_kway_size_caps_product.json): +1 to +8 points
-// wherever a class differs, within 0.3 points everywhere else.
-// Rows: operands below 24, 48 and 96 MiB.
-inline constexpr int kMultiWavesSmall[3][9] = {
-    {32, 32, 32, 24, 16, 16, 16, 16, 32},
-    {32, 32, 32, 20, 16, 16, 11, 10, 9},
-    {32, 32, 24, 16, 13, 11, 11, 10, 9},
-};
-inline constexpr int kChainWavesSmall[3][9] = {
-    {32, 32, 32, 32, 32, 24, 16, 16, 16},
-    {32, 32, 32, 32, 16, 16, 16, 16, 16},
-    {32, 32, 32, 24, 16, 13, 11, 10, 9},
-};
-inline int size_class(size_t bytes) {  // 0, 1, 2 for operands below 24, 48, 96 MiB; 3 from 96 MiB
-    return bytes < (size_t(24) << 20) ? 0 : bytes < (size_t(48) << 20) ? 1 : bytes < (size_t(96) << 20) ? 2 : 3;
-}
-// The loads-first phased launches' caps by operand size (the k's of kPhasedFirstWaves / kChainPhasedFirstWaves;
-// tools/kway_size_caps.py --phased, sources 4 B off phase, profiles/r2_s70_kway_size_caps_phased.json): +1.3 to
-// +7.7 points at 16-32 MiB, chain k = 4 +2.1 at 64 MiB.  Rows: operands below 24, 48 and 96 MiB.
-inline constexpr int kPhasedFirstWavesSmall[3][9] = {
-    {0, 0, 0, 0, 0, 16, 0, 24, 16},
-    {0, 0, 0, 0, 0, 16, 0, 16, 24},
-    {0, 0, 0, 0, 0, 13, 0, 12, 11},
-};
-inline constexpr int kChainPhasedFirstWavesSmall[3][9] = {
-    {0, 0, 0, 0, 24, 24, 0, 24, 16},
-    {0, 0, 0, 0, 16, 16, 0, 16, 24},
-    {0, 0, 0, 0, 16, 13, 0, 11, 11},
-};
-inline size_t phased_first_lds_for(int k, size_t bytes) {
-    const int c = size_class(bytes);
-    return waves_lds(c < 3 ? kPhasedFirstWavesSmall[c][k] : kPhasedFirstWaves[k]);
-}
-inline size_t chain_phased_first_lds_for(int k, size_t bytes) {
-    const int c = size_class(bytes);
-    return waves_lds(c < 3 ? kChainPhasedFirstWavesSmall[c][k] : kChainPhasedFirstWaves[k]);
-}
-inline size_t unaligned_lds_for(size_t bytes) {
-    const int c = size_class(bytes);
-    return waves_lds(c < 3 ? kUnalignedWavesSmall[c] : kUnalignedWaves);
-}
-inline size_t multi_lds_for(int k, size_t bytes) {
-    const int c = size_class(bytes);
-    const int w = c < 3 ? kMultiWavesSmall[c][k] : kMultiWaves[k];
-    return w >= 32 ? 0 : (kLdsPerCu / w + 255) / 256 * 256;
-}
-inline size_t chain_lds_for(int k, size_t bytes) {
-    const int c = size_class(bytes);
-    const int w = c < 3 ? kChainWavesSmall[c][k] : kChainWaves[k];
-    return w >= 32 ? 0 : (kLdsPerCu / w + 255) / 256 * 256;
-}
-// Caps of the line-straddling launches (in-phase sources off recv's 128-B lines, loaded through the
-// caches): swept on their own in round 2 (tools/phased_probe.py --straddle-caps, 1 GiB fp32 Sum, sources
-// at 16 (2j+1) B, profiles/r2_kway_straddle_caps.json).  The straddling loads want fewer waves than
-// line-aligned ones from k = 4 (k-way) / k = 3 (chain); past the best cap the rate falls off a cliff of
-// 5 points (k-way k = 6: 79.3 % at 10 waves, 74.1 % at 11; k = 7: 78.6 % at 9, 74.0 % at 10), so each
-// value sits inside its plateau.  Nominal counts: the LDS rounding makes 8 and 9 (and 16 and 18) the same
-// occupancy.  A/B against the k-way caps on one box (profiles/r2_kway_straddle_caps_ab.json): k-way k = 6
-// 74.1 -> 79.0 %, k = 7 73.6 -> 78.8 %, k = 8 74.8 -> 75.9 %; chain k = 3 79.6 -> 81.3 %, k = 4 77.3 -> 80.2 %
-// (k-way k = 4 keeps 13: 79.4 % against 78.9 % at 11).
-inline constexpr int kStraddleWaves[9] = {32, 32, 18, 13, 13, 11, 9, 9, 7};
-constexpr size_t straddle_lds(int k) {
-    return kStraddleWaves[k] >= 32 ? 0 : (kLdsPerCu / kStraddleWaves[k] + 255) / 256 * 256;
-}
-inline constexpr int kChainStraddleWaves[9] = {32, 32, 24, 18, 13, 13, 11, 10, 9};
-constexpr size_t chain_straddle_lds(int k) {
-    return kChainStraddleWaves[k] >= 32 ? 0 : (kLdsPerCu / kChainStraddleWaves[k] + 255) / 256 * 256;
-}
-// The line-straddling launches below 96 MiB per operand, by the same rule as kMultiWavesSmall /
-// kChainWavesSmall (tools/kway_size_caps.py --straddle, profiles/r2_s70_kway_size_caps_straddle.json): gains
-// over the 1 GiB caps of +2 to +6 points at 16 MiB, up to +5.6 at 32 MiB and +1.5 to +4.7 at 64 MiB.
-// Rows: operands below 24, 48 and 96 MiB.
-inline constexpr int kStraddleWavesSmall[3][9] = {
-    {32, 32, 32, 24, 16, 16, 16, 16, 32},
-    {32, 32, 24, 16, 13, 11, 16, 9, 32},
-    {32, 32, 24, 16, 13, 11, 9, 9, 7},
-};
-inline constexpr int kChainStraddleWavesSmall[3][9] = {
-    {32, 32, 32, 32, 24, 24, 16, 16, 16},
-    {32, 32, 32, 32, 24, 16, 11, 10, 9},
-    {32, 32, 32, 24, 16, 13, 11, 10, 9},
-};
-inline size_t straddle_lds_for(int k, size_t bytes) {
-    const int c = size_class(bytes);
-    const int w = c < 3 ? kStraddleWavesSmall[c][k] : kStraddleWaves[k];
-    return w >= 32 ? 0 : (kLdsPerCu / w + 255) / 256 * 256;
-}
-inline size_t chain_straddle_lds_for(int k, size_t bytes) {
-    const int c = size_class(bytes);
-    const int w = c < 3 ? kChainStraddleWavesSmall[c][k] : kChainStraddleWaves[k];
-    return w >= 32 ? 0 : (kLdsPerCu / w + 255) / 256 * 256;
-}
-
 constexpr size_t kMaxGrid = size_t(1) << 24;  // grid-stride beyond this (2^24 x 64 threads)
 
 inline int launch(const void* fn, size_t grid, void** args, hipStream_t stream, int block = kBlock,

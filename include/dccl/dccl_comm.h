@@ -22,7 +22,10 @@
  *                         creates and publishes it, the others wait (DCCL_BOOTSTRAP_TIMEOUT_S, default
  *                         120 s) for a file published by a LIVE rank 0 of the same world size, so a
  *                         file an earlier job left behind is never taken (what ncclCommInit does
- *                         with DCCL_TRANSPORT=rccl)
+ *                         with DCCL_TRANSPORT=rccl).  A second call under the same tag waits for a new
+ *                         publication: a rank never takes the id it already took
+ *   dccl_bootstrap_done   rank 0 removes the published id once dccl_comm_init_rccl returned (every rank
+ *                         has read it then), as ncclCommInit does; other ranks: no-op
  *   dccl_all_reduce       ncclAllReduce       (/root/reference/include/dccl/dccl.hpp:206-207)
  *   dccl_reduce_scatter   ncclReduceScatter   (/root/reference/include/dccl/dccl.hpp:243-244)
  *   dccl_all_gather       ncclAllGather       (/root/reference/include/dccl/dccl.hpp:392-393)
@@ -47,6 +50,7 @@ int dccl_comm_init_ipc(void** comm, uint32_t world, uint32_t rank);
 int dccl_comm_init_p2p(void** comm, uint32_t world, uint32_t rank, dccl_p2p_exchange_fn exchange, void* ctx,
                        int memory);
 int dccl_bootstrap_unique_id(uint32_t rank, uint32_t world, void* unique_id_128);
+int dccl_bootstrap_done(uint32_t rank, uint32_t world);
 int dccl_comm_finalize(void* comm);
 int dccl_all_reduce(const void* send, void* recv, size_t count, int dtype, int op, void* comm, void* stream);
 int dccl_reduce_scatter(const void* send, void* recv, size_t recvcount, int dtype, int op, void* comm,

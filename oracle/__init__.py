@@ -7,8 +7,10 @@ The product path (``dccl_amd``) never imports it.
 * ``restatement()`` — ``oracle/liboracle_host_reduce.so``, the C restatement of
   ``do_host_reduce<DT>`` (/root/reference/src/core/internal_common.hpp:496-586),
   compiled with the reference's Release flags (CMakeLists.txt:25).
-* ``restatement_native()`` — the same source with the reference's Benchmark flags
-  (-Ofast -march=native, CMakeLists.txt:26), a labelled CPU-baseline variant only.
+* ``restatement_benchflags(path)`` — the same source with the reference's Benchmark
+  flags (-Ofast -march=native, CMakeLists.txt:26), a labelled CPU-baseline variant only.
+  ``bench.py`` compiles it on the host it runs on (``compile_benchflags``); the prebuilt
+  ``liboracle_host_reduce_v4.so`` (-march=x86-64-v4) is the fallback.
 
 Parity unpinned: the reference's own combine is not built here (it needs its
 CMake-generated config.h and spdlog, which the image lacks), and the reference
@@ -24,7 +26,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 _RESTATEMENT = os.path.join(HERE, "liboracle_host_reduce.so")
-_NATIVE = os.path.join(HERE, "liboracle_host_reduce_native.so")
+_V4 = os.path.join(HERE, "liboracle_host_reduce_v4.so")
+SOURCE = os.path.join(HERE, "host_reduce.c")
+BENCH_FLAGS = ["-std=c11", "-Ofast", "-march=native", "-mprefer-vector-width=512", "-fPIC", "-shared"]
 
 # ncclDataType_t -> numpy dtype (fp16 / bf16 travel as raw uint16 bit patterns)
 NP_DTYPES = {
@@ -36,7 +40,7 @@ _cache: dict = {}
 
 
 def build() -> None:
-    """Compile the restatement (Release flags, plus the labelled -Ofast -march=native variant)."""
+    """Compile the restatement (Release flags, plus the labelled -Ofast -march=x86-64-v4 variant)."""
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
 
@@ -69,11 +73,26 @@ def restatement():
     return _cache["rs"]
 
 
-def restatement_native():
-    """The restatement built with the reference's Benchmark flags (-Ofast -march=native), or None."""
-    if "native" not in _cache:
-        _cache["native"] = _bind(_NATIVE, ["oracle_host_reduce"]) if os.path.exists(_NATIVE) else None
-    return _cache["native"]
+def compile_benchflags(outdir: str) -> str | None:
+    """The restatement compiled with the reference's Benchmark flags for THIS host's CPU (-march=native,
+    CMakeLists.txt:26) into `outdir`; None when no compiler is available."""
+    out = os.path.join(outdir, "liboracle_host_reduce_benchflags.so")
+    try:
+        subprocess.run(["gcc", *BENCH_FLAGS, SOURCE, "-o", out], check=True, capture_output=True, timeout=120)
+    except Exception:
+        return None
+    return out
+
+
+def benchflags_fallback() -> str | None:
+    """The prebuilt Benchmark-flags variant (-march=x86-64-v4), or None."""
+    return _V4 if os.path.exists(_V4) else None
+
+
+def restatement_benchflags(path: str):
+    """The restatement built with the reference's Benchmark flags (a library from compile_benchflags or
+    benchflags_fallback); only ever loaded in a child process (an unsupported instruction ends the child)."""
+    return _bind(path, ["oracle_host_reduce"])
 
 
 def _ptr(a: np.ndarray) -> int:

@@ -11,11 +11,14 @@
  * load this file's library, and only as the checker / the timed CPU baseline.
  * The product path (dccl_amd/) never links or calls it.
  *
- * Pinning: tests/test_oracle.py checks this restatement bit-for-bit against
- * the reference's own do_host_reduce compiled from /root/reference by
- * oracle/build_ref.sh (-> oracle/_ref/, when the reference is present) and
- * against the committed golden fixtures in tests/golden/ that were generated
- * from that compiled reference (tests/golden/make_golden.py).
+ * Parity unpinned: the reference holds no test vectors and its
+ * combine does not build here without stand-ins (the CMake-generated
+ * dccl/config.h and spdlog are absent), so nothing is compiled from
+ * /root/reference.  tests/test_oracle.py checks this restatement against
+ * regression fixtures in tests/golden/ that were frozen from a round-1 build
+ * with stand-in headers (tests/golden/make_golden.py says how; they pin
+ * nothing), against the C1 known answers recorded in SURVEY.md §8(c), and
+ * against numpy / torch for fp16 / bf16.
  *
  * Two entry points:
  *   oracle_host_reduce()   — the reference's loop split, faithfully: head up to

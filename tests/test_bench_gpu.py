@@ -72,6 +72,31 @@ def test_bench_direct_allreduce_two_processes_one_gpu():
     assert ar["c5_allgather"]["direct"]["bit_exact"], ar["c5_allgather"]
 
 
+def test_bench_self_launch_two_ranks_one_gpu():
+    """Plain `python3 bench.py --gpus 2` (no launcher): bench.py starts its two rank processes itself, here both on
+    the box's one GPU (gloo for torch.distributed, the direct IPC collectives between the two processes), and
+    prints one line with n_gpus == 2 and its sampled results verified."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update({"DCCL_BENCH_BACKEND": "gloo", "DCCL_BENCH_AR_TRANSPORTS": "direct",
+                "DCCL_BOOTSTRAP_TAG": f"bench_self_launch_{_port()}"})
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--mib", "64",
+           "--c5-gib", "0.25", "--no-cpu", "--other-pairs", "2"]
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, p.stdout[-3000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["verified"] is True, res
+    assert res["c5"]["verified"] and res["other_layout"]["pairs"] == 2, res
+    s = res["dccl_allreduce_summary"]
+    assert s["direct"]["int32_sum_bit_exact_vs_rccl"] and s["dccl_allgather"]["direct"]["bit_exact"], s
+    assert list(res)[-1] == "verified"
+
+
 def test_bench_single_gpu_line():
     """bench.py at N=1 prints exactly one JSON line with the contract's keys, the C5 extra and the C3 / C4
     legs (every C3 entry sample-verified)."""
@@ -99,3 +124,7 @@ def test_bench_single_gpu_line():
     assert sizes == [1 << e for e in range(12, 33)] and all(r["us_per_launch"] > 0 for r in res["c4"])
     assert all(r["graph_us_per_launch"] > 0 for r in res["c4"] if r["bytes_per_operand"] <= 64 << 20)
     assert all(r["native_eager_us_per_launch"] > 0 for r in res["c4"] if r["bytes_per_operand"] <= 64 << 20)
+    assert res["other_layout"]["layout"] == "separate" and res["other_layout"]["pairs"] == 4
+    assert res["verified"] is True and list(res)[-1] == "verified"
+    cb = res["cpu_baseline"]
+    assert cb["all_cores"]["cores"] == cb["affinity_cpus"] and cb["threads_16"]["cores"] == min(16, cb["affinity_cpus"])

@@ -1,0 +1,125 @@
+"""The resident-wave caps of the capped combine launches (dccl_amd/csrc/caps.hpp), on the CPU: caps.hpp is
+host-only C++, compiled here with g++ into a small harness that prints caps::waves / caps::lds for every
+(kernel class, k, size) the launchers can ask for.  This is the guard VERDICT r2 asked for: every cap is a
+legal LDS request (<= 64 KiB per block), the size classes switch at 24 / 48 / 96 MiB, k outside [1, 8] (or a
+class's own range) is rejected, the separate-allocation rule holds, and the table is the frozen one below —
+changing an entry means changing this test, with the measurement that justifies it (>= 2 points, two boxes)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "dccl_amd", "csrc")
+
+HARNESS = r"""
+#include <cstdio>
+#include "caps.hpp"
+using namespace dccl_amd::caps;
+int main() {
+    const size_t MiB = size_t(1) << 20;
+    const size_t sizes[] = {4096, 24 * MiB - 1, 24 * MiB, 48 * MiB - 1, 48 * MiB, 96 * MiB - 1, 96 * MiB, 1024 * MiB};
+    std::printf("{\"rows\": [");
+    bool first = true;
+    for (int c = 0; c < kNumKernels; ++c)
+        for (size_t b : sizes)
+            for (int k = -1; k <= 9; ++k) {
+                std::printf("%s[%d, %zu, %d, %d, %zu]", first ? "" : ", ", c, b, k, waves(Kernel(c), k, b),
+                            lds(Kernel(c), k, b));
+                first = false;
+            }
+    std::printf("], \"pair\": [");
+    first = true;
+    for (int sh = 0; sh < 2; ++sh)
+        for (int sep = 0; sep < 2; ++sep)
+            for (size_t b : sizes) {
+                std::printf("%s[%d, %d, %zu, %zu]", first ? "" : ", ", sh, sep, b, pair_lds(sh, sep, b));
+                first = false;
+            }
+    std::printf("], \"loads_first\": [");
+    for (int ch = 0; ch < 2; ++ch)
+        for (int k = 1; k <= 8; ++k) std::printf("%s%d", (ch || k > 1) ? ", " : "", int(phased_loads_first(ch, k)));
+    std::printf("]}\n");
+}
+"""
+
+NAMES = ["multi", "chain", "multi_straddle", "chain_straddle", "multi_phased_first", "chain_phased_first", "unaligned"]
+# frozen table: class -> size class (<24, <48, <96 MiB, >=96 MiB) -> waves for k = 0..8 (0 = not used at that k)
+FROZEN = {
+    "multi": [[0, 0, 32, 24, 16, 16, 16, 16, 32], [0, 0, 32, 20, 16, 16, 11, 10, 9],
+              [0, 0, 24, 16, 13, 11, 11, 10, 9], [0, 0, 18, 13, 13, 11, 11, 10, 9]],
+    "chain": [[0, 32, 32, 32, 32, 24, 16, 16, 16], [0, 32, 32, 32, 16, 16, 16, 16, 16],
+              [0, 32, 32, 24, 16, 13, 11, 10, 9], [0, 32, 24, 20, 16, 13, 11, 10, 9]],
+    "multi_straddle": [[0, 0, 32, 24, 16, 16, 16, 16, 32], [0, 0, 24, 16, 13, 11, 16, 9, 32],
+                       [0, 0, 24, 16, 13, 11, 9, 9, 7], [0, 0, 18, 13, 13, 11, 9, 9, 7]],
+    "chain_straddle": [[0, 32, 32, 32, 24, 24, 16, 16, 16], [0, 32, 32, 32, 24, 16, 11, 10, 9],
+                       [0, 32, 32, 24, 16, 13, 11, 10, 9], [0, 32, 24, 18, 13, 13, 11, 10, 9]],
+    "multi_phased_first": [[0, 0, 0, 0, 0, 16, 0, 24, 16], [0, 0, 0, 0, 0, 16, 0, 16, 24],
+                           [0, 0, 0, 0, 0, 13, 0, 12, 11], [0, 0, 0, 0, 0, 13, 0, 12, 11]],
+    "chain_phased_first": [[0, 0, 0, 0, 24, 24, 0, 24, 16], [0, 0, 0, 0, 16, 16, 0, 16, 24],
+                           [0, 0, 0, 0, 16, 13, 0, 11, 11], [0, 0, 0, 0, 13, 13, 0, 11, 11]],
+    "unaligned": [[0, 32] + [0] * 7, [0, 32] + [0] * 7, [0, 26] + [0] * 7, [0, 24] + [0] * 7],
+}
+K_RANGE = {"multi": (2, 8), "chain": (1, 8), "multi_straddle": (2, 8), "chain_straddle": (1, 8),
+           "multi_phased_first": (2, 8), "chain_phased_first": (1, 8), "unaligned": (1, 1)}
+
+
+@pytest.fixture(scope="module")
+def table(tmp_path_factory):
+    d = tmp_path_factory.mktemp("caps")
+    src, exe = d / "caps_dump.cpp", d / "caps_dump"
+    src.write_text(HARNESS)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", f"-I{CSRC}", str(src), "-o", str(exe)],
+                   check=True)
+    return json.loads(subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout)
+
+
+def size_class(b):
+    return 0 if b < 24 << 20 else 1 if b < 48 << 20 else 2 if b < 96 << 20 else 3
+
+
+def lds_for(w):
+    return 0 if w <= 0 or w >= 32 else ((160 << 10) // w + 255) // 256 * 256
+
+
+def test_every_entry_is_the_frozen_table_and_a_legal_request(table):
+    seen = 0
+    for c, b, k, w, lds in table["rows"]:
+        name = NAMES[c]
+        lo, hi = K_RANGE[name]
+        if not lo <= k <= hi:
+            assert w == -1 and lds == 0, (name, k)  # k outside the class's range: rejected, no request
+            continue
+        assert w == FROZEN[name][size_class(b)][k], (name, b, k, w)
+        assert lds == lds_for(w) and lds <= 64 << 10, (name, b, k, lds)
+        if w:
+            assert 7 <= w <= 32 and (lds == 0) == (w == 32)
+            assert (160 << 10) // lds >= w - 2 if lds else True  # the request really caps near w waves
+        seen += 1
+    assert seen == sum(8 * (hi - lo + 1) for lo, hi in K_RANGE.values())
+
+
+def test_size_class_boundaries(table):
+    rows = {(NAMES[c], b, k): w for c, b, k, w, _ in table["rows"]}
+    MiB = 1 << 20
+    # kMulti k = 2 switches 32 -> 32 -> 24 -> 18 at 24 / 48 / 96 MiB; k = 3 24 -> 20 -> 16 -> 13
+    assert [rows[("multi", b, 3)] for b in (24 * MiB - 1, 24 * MiB, 48 * MiB - 1, 48 * MiB, 96 * MiB - 1, 96 * MiB)] \
+        == [24, 20, 20, 16, 16, 13]
+    assert rows[("unaligned", 96 * MiB - 1, 1)] == 26 and rows[("unaligned", 96 * MiB, 1)] == 24
+    assert rows[("multi", 1024 * MiB, 8)] == rows[("multi", 96 * MiB, 8)] == 9
+
+
+def test_phased_form_is_fixed_per_k(table):
+    lf = table["loads_first"]
+    assert lf[:8] == [0, 0, 0, 0, 1, 0, 1, 1]   # k-way: loads-first at k = 5, 7, 8
+    assert lf[8:] == [0, 0, 0, 1, 1, 0, 1, 1]   # chain: at k = 4, 5, 7, 8
+
+
+def test_separate_allocation_rule(table):
+    for sh, sep, b, lds in table["pair"]:
+        if not sep or b < 512 << 20:
+            assert lds == 0, (sh, sep, b)
+        else:
+            assert lds == (6144 if sh else 7168), (sh, sep, b)
+            assert (160 << 10) // lds == (26 if sh else 22)

@@ -79,8 +79,8 @@ def _start_time(pid: int) -> int:
     return int(line[line.rindex(")") + 2:].split()[19])
 
 
-def _stamp(pid: int, start: int, world: int, payload: bytes) -> str:
-    return f"DCCLRDV1 {pid} {start} {world} {payload.hex()}\n"
+def _stamp(pid: int, start: int, world: int, payload: bytes, gen: int = 1) -> str:
+    return f"DCCLRDV2 {pid} {start} {gen} {world} {payload.hex()}\n"
 
 
 @pytest.fixture()
@@ -124,6 +124,31 @@ def test_bootstrap_accepts_live_publisher_cpu(rdv):
     # the live pid but another start time: a recycled pid
     rdv.write_text(_stamp(os.getpid(), _start_time(os.getpid()) + 1, 2, uid))
     assert _read_id()[0] == 2
+
+
+def test_bootstrap_two_groups_same_tag_cpu(rdv):
+    """the same live rank 0 forms a second group under the same tag.  A peer that polls before rank 0
+    republishes must not take the first group's id (it would join a finished RCCL bootstrap and hang); it
+    waits for the new publication.  dccl_bootstrap_done then removes the file, as ncclCommInit does."""
+    import dccl_amd
+    first = ctypes.create_string_buffer(128)
+    assert dccl_amd.lib.dccl_bootstrap_unique_id(0, 2, first) == 0  # rank 0 publishes group 1's id
+    rc, got = _read_id()
+    assert rc == 0 and got == first.raw
+    # group 2: rank 1 polls before rank 0 republished -> times out instead of returning the old id
+    assert _read_id()[0] == 2
+    second = ctypes.create_string_buffer(128)
+    assert dccl_amd.lib.dccl_bootstrap_unique_id(0, 2, second) == 0
+    assert second.raw != first.raw
+    rc, got = _read_id()
+    assert rc == 0 and got == second.raw
+    # another reader rank of the same process takes the current publication once, too
+    rc, got = _read_id(rank=1, world=2)
+    assert rc == 2
+    assert dccl_amd.lib.dccl_bootstrap_done(1, 2) == 0 and rdv.exists()  # not rank 0: nothing removed
+    assert dccl_amd.lib.dccl_bootstrap_done(0, 2) == 0 and not rdv.exists()
+    assert _read_id()[0] == 2
+    assert dccl_amd.lib.dccl_bootstrap_done(2, 2) == 4 and dccl_amd.lib.dccl_bootstrap_done(0, 0) == 4
 
 
 def test_bootstrap_argument_checks_cpu():

@@ -775,7 +775,7 @@ int tune_unaligned_edge(const unsigned char* s, unsigned char* r, size_t count, 
     unsigned p = unsigned(reinterpret_cast<uintptr_t>(s) & 15);
     size_t cnt = count, nv = nvec;
     void* args[] = {const_cast<unsigned char**>(&s), &p, &r, &nv, &cnt};
-    return launch(reinterpret_cast<const void*>(&tune_unaligned_edge_kernel<E>), grid, args, st, 64, waves_lds(waves));
+    return launch(reinterpret_cast<const void*>(&tune_unaligned_edge_kernel<E>), grid, args, st, 64, caps::lds_for_waves(waves));
 }
 // Aligned-vector form of the misaligned-recv combine (walks of W tiles per wave).  recv's body is walked in
 // ALIGNED 16-B vectors V_v (from the first 16-B boundary inside recv, Vstart); every element boundary then
@@ -884,7 +884,7 @@ int tune_unaligned_walk_vec(const unsigned char* s, unsigned char* r, size_t cou
     if (grid == 0) grid = 1;
     void* args[] = {const_cast<unsigned char**>(&s), &r, &vb, &ub, &nv, &c, &sigma, &js, &je, &count};
     return launch(reinterpret_cast<const void*>(&tune_unaligned_walk_vec_kernel<T, OP, W>), grid, args, st, 64,
-                  waves_lds(waves));
+                  caps::lds_for_waves(waves));
 }
 }  // namespace
 // recv must not be element-aligned (fp32: an address that is not a multiple of 4).
@@ -1052,7 +1052,7 @@ int tune_phased_k(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStre
     if (grid > kMaxGrid) return DCCL_INVALID_ARGUMENT;  // one tile per block (the XCD map is over the grid)
     void* args[] = {&sl, &ph, &r, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&tune_phased_kernel<K, MODE>), grid, args, st, 64,
-                  lds != 0 ? lds : (MODE & 16) ? multi_lds(K) : 0);
+                  lds != 0 ? lds : (MODE & 16) ? caps::lds(caps::kMulti, K, size_t(1) << 30) : 0);
 }
 template <int MODE>
 int tune_phased_mode(SendList sl, PhaseList ph, int k, unsigned char* r, Split sp, hipStream_t st, size_t lds) {
