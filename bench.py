@@ -598,6 +598,7 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
             torch.cuda.synchronize(dev)
             t = (time.perf_counter() - t0) / iters
             res.update({"ms": round(t * 1e3, 3), "busbw_gb_s": round(2 * (world - 1) / world * count * 4 / t / 1e9, 1)})
+            res.update(root_ops(comm, world, rank, dev, st, xi, ri, iters))
             out[name] = res
             yf_by[name] = yf
         if "ring" in yf_by and "direct" in yf_by:
@@ -630,6 +631,37 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
     finally:
         for comm in comms.values():
             comm.finalize()
+    return out
+
+
+def root_ops(comm, world: int, rank: int, dev, st, xi, ri, iters: int) -> dict:
+    """ncclBroadcast and ncclReduce (root 0, int32) through the namespace-dccl API of this transport: the
+    broadcast must deliver rank 0's input bit for bit (regenerated from its seed), the reduce must leave
+    RCCL's own all_reduce sum at the root; each is timed.  On the RCCL transport the root's W - 1 transfers
+    run in one group (rccl_fan)."""
+    count = xi.numel()
+    want0 = torch.randint(-2**20, 2**20, (count,), device=dev, dtype=torch.int32,
+                          generator=torch.Generator(device=dev).manual_seed(1234))
+    y = torch.empty_like(xi)
+    z = torch.zeros_like(xi)
+    out = {}
+    for what in ("broadcast", "reduce"):
+        def call():
+            if what == "broadcast":
+                return comm.broadcast(xi.data_ptr(), y.data_ptr(), count, 2, 0, st.cuda_stream)
+            return comm.reduce(xi.data_ptr(), z.data_ptr(), count, 2, 0, 0, st.cuda_stream)
+        dccl_amd.check(call(), what)
+        torch.cuda.synchronize(dev)
+        ok = bool(torch.equal(y, want0)) if what == "broadcast" else (rank != 0 or bool(torch.equal(z, ri)))
+        flag = torch.tensor([int(ok)], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dccl_amd.check(call(), what)
+        torch.cuda.synchronize(dev)
+        out[f"{what}_bit_exact"] = bool(flag[0])
+        out[f"{what}_ms"] = round((time.perf_counter() - t0) / iters * 1e3, 3)
     return out
 
 
@@ -904,7 +936,8 @@ def allreduce_summary(ar) -> dict:
     for name in ("ring", "direct"):
         if isinstance(ar.get(name), dict):
             out[name] = {k: ar[name][k] for k in ("int32_sum_bit_exact_vs_rccl", "fp32_within_bound", "ms",
-                                                  "busbw_gb_s") if k in ar[name]}
+                                                  "busbw_gb_s", "broadcast_bit_exact", "broadcast_ms",
+                                                  "reduce_bit_exact", "reduce_ms") if k in ar[name]}
     if isinstance(ar.get("rccl_allreduce"), dict):
         out["rccl"] = {k: ar["rccl_allreduce"][k] for k in ("ms", "busbw_gb_s")}
     for key in ("dccl_allgather", "c5_allgather"):

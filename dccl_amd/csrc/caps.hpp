@@ -27,7 +27,6 @@ enum Kernel : int {
     kChainStraddle,     // reduce_chain_vec_kernel, the same
     kMultiPhasedFirst,  // reduce_multi_phased_kernel, loads-first form; 0 = the per-operand form, uncapped
     kChainPhasedFirst,  // reduce_chain_phased_kernel, the same
-    kUnaligned,         // reduce_unaligned_kernel (recv not element-aligned; pairwise, column k = 1)
     kNumKernels
 };
 
@@ -55,8 +54,9 @@ constexpr int size_class(size_t bytes) {
 //  kMultiPhasedFirst / kChainPhasedFirst  the loads-first form wins from k = 5 (k-way) / k = 4 (chain)
 //              under these caps on two boxes (r2_phased_first_caps.json, r2_phased_first_ab.json); k = 6
 //              keeps the per-operand form (the two disagree in sign); size rows r2_s70_..._phased.json.
-//  kUnaligned  recv + 1 B: 76.7 % uncapped, 78.8 % at 24 waves, 76.1 % at 20 (r2_misaligned_caps.json);
-//              size rows r2_s70_misaligned_size_caps.json (16 MiB 62.7 -> 66.4 %).
+// The misaligned-recv kernel took a cap of its own in round 2 (24 waves); round 3's form (recv read through
+// aligned loads, group-interleaved tile order) runs best uncapped (profiles/r3_s4_unaligned_orders_caps.json),
+// so that row is gone.
 inline constexpr unsigned char kWaves[kNumKernels][kSizeClasses][9] = {
     // k:  0   1   2   3   4   5   6   7   8
     {{0, 0, 32, 24, 16, 16, 16, 16, 32},  // kMulti            < 24 MiB
@@ -83,15 +83,11 @@ inline constexpr unsigned char kWaves[kNumKernels][kSizeClasses][9] = {
      {0, 0, 0, 0, 16, 16, 0, 16, 24},
      {0, 0, 0, 0, 16, 13, 0, 11, 11},
      {0, 0, 0, 0, 13, 13, 0, 11, 11}},
-    {{0, 32, 0, 0, 0, 0, 0, 0, 0},  // kUnaligned
-     {0, 32, 0, 0, 0, 0, 0, 0, 0},
-     {0, 26, 0, 0, 0, 0, 0, 0, 0},
-     {0, 24, 0, 0, 0, 0, 0, 0, 0}},
 };
 
 // The valid k range of each class (the launchers' with_k bounds).
 constexpr int min_k(Kernel c) { return c == kMulti || c == kMultiStraddle || c == kMultiPhasedFirst ? 2 : 1; }
-constexpr int max_k(Kernel c) { return c == kUnaligned ? 1 : 8; }
+constexpr int max_k(Kernel) { return 8; }
 
 // Nominal waves of a launch of class c with k sources and `bytes` per operand; -1 for a k outside the
 // class's range.  0 for the phased classes means "the per-operand form, uncapped".

@@ -23,6 +23,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 
 #include "algorithms.hpp"
@@ -489,6 +490,11 @@ ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, nccl
                              [W](uint32_t o) { return (o + W - 1) % W; }, [W](uint32_t n) { return (n + 1) % W; });
     if (rc != ncclSuccess) return rc;
     auto at = [&](uint32_t i) { return static_cast<unsigned char*>(rbuf) + size_t(i) * slot; };
+    if (comm->rccl != nullptr && iamroot) {  // gather to the root (dccl.cpp:803-840): one RCCL group
+        std::vector<void*> bufs(W);
+        for (uint32_t p = 0; p < W; ++p) bufs[p] = at(p);
+        return static_cast<ncclResult_t>(rccl_fan(comm->rccl, false, bufs.data(), slot, W, r, stream));
+    }
     if (comm->p2p != nullptr) {  // gather to the root (dccl.cpp:803-840), one exchange per peer
         for (uint32_t p = 0; p < W && rc == ncclSuccess; ++p) {
             if (p == uint32_t(root) || (!iamroot && p != r)) continue;
@@ -539,8 +545,13 @@ ncclResult_t ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, n
     if (!transport_accepts(comm, dev)) return ncclInvalidUsage;
     if (W > 1 && dev && direct_selected(comm))
         return direct_broadcast(comm, sendbuff, recvbuff, count, datatype, uint32_t(root), stream);
-    if (comm->p2p != nullptr) {  // root -> every rank, one exchange per peer
+    if (comm->p2p != nullptr) {  // root -> every rank, one exchange per peer (RCCL: one group)
         if (r != uint32_t(root)) return p2p_exchange(comm, nullptr, 0, 0, recvbuff, bytes, uint32_t(root), stream);
+        if (comm->rccl != nullptr) {
+            std::vector<void*> bufs(W, const_cast<void*>(sendbuff));
+            rc = static_cast<ncclResult_t>(rccl_fan(comm->rccl, true, bufs.data(), bytes, W, r, stream));
+            return rc == ncclSuccess ? copy_bytes(recvbuff, sendbuff, bytes, dev, stream) : rc;
+        }
         for (uint32_t p = 0; p < W && rc == ncclSuccess; ++p)
             if (p != r) rc = p2p_exchange(comm, sendbuff, bytes, p, nullptr, 0, 0, stream);
         return rc == ncclSuccess ? copy_bytes(recvbuff, sendbuff, bytes, dev, stream) : rc;

@@ -86,4 +86,20 @@ int rccl_exchange(void* rcomm, const void* sendbuf, size_t send_bytes, uint32_t 
     return r != 0 ? r : re;
 }
 
+int rccl_fan(void* rcomm, bool send, void* const* bufs, size_t bytes, uint32_t world, uint32_t self,
+             hipStream_t stream) {
+    const RcclApi& a = api();
+    if (!a.ok) return kSystem;
+    auto c = static_cast<ncclComm_t>(rcomm);
+    int r = rc(a.group_start());
+    if (r != 0) return r;
+    for (uint32_t p = 0; p < world && r == 0 && bytes; ++p) {
+        if (p == self) continue;
+        r = send ? rc(a.send(bufs[p], bytes, ncclUint8, int(p), c, stream))
+                 : rc(a.recv(bufs[p], bytes, ncclUint8, int(p), c, stream));
+    }
+    const int re = rc(a.group_end());  // always close the group
+    return r != 0 ? r : re;
+}
+
 }  // namespace dccl_amd

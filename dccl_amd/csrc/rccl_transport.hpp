@@ -27,5 +27,10 @@ int rccl_comm_destroy(void* rcomm);
 // `recvbuf` from `from` (either side may be skipped with a null buffer), enqueued on `stream`.
 int rccl_exchange(void* rcomm, const void* sendbuf, size_t send_bytes, uint32_t to, void* recvbuf,
                   size_t recv_bytes, uint32_t from, hipStream_t stream);
+// The root's side of a one-to-all (send) or all-to-one (receive) step in ONE group: `bytes` to / from every
+// rank p != self at bufs[p], enqueued on `stream`, so the root's transfers to its W - 1 peers run together
+// (broadcast; the gather to the root of ncclReduce, dccl.cpp:803-840) instead of one after another.
+int rccl_fan(void* rcomm, bool send, void* const* bufs, size_t bytes, uint32_t world, uint32_t self,
+             hipStream_t stream);
 
 }  // namespace dccl_amd

@@ -114,6 +114,15 @@ __device__ __forceinline__ size_t xcd_group_tile(size_t b, size_t nb) {
     return (q + 1) * 64 > nb ? b : q * 64 + (r % 8) * 8 + r / 8;
 }
 
+// First tile of block b of a g-block grid (g a multiple of 8) for the misaligned-destination kernels, by a
+// uniform runtime `order`: kOrderXcd gives each XCD one contiguous range (consecutive tiles on one XCD: the
+// line two tiles share meets in one L2), kOrderBlock is block order, kOrderGroup the group-interleaved order
+// above (one front for the chip, 7 of 8 tile boundaries inside one XCD).  Computed once per block.
+enum : int { kOrderXcd = 0, kOrderBlock = 1, kOrderGroup = 2 };
+__device__ __forceinline__ size_t tile_order(int order, size_t b, size_t g) {
+    return order == kOrderXcd ? (b % 8) * (g / 8) + b / 8 : order == kOrderBlock ? b : xcd_group_tile(b, g);
+}
+
 template <typename T, int OP, typename C>
 __global__ __launch_bounds__(C::BLOCK) void reduce_vec_kernel(const unsigned char* __restrict__ send,
                                                               unsigned char* __restrict__ recv,
@@ -175,14 +184,9 @@ __device__ __forceinline__ u32x4 dpp16(u32x4 x, u32x4 old) {
     o.w = unsigned(__builtin_amdgcn_update_dpp(int(old.w), int(x.w), CTRL, 0xF, 0xF, false));
     return o;
 }
-// lane l receives lane (l+1) % 64's vector
-__device__ __forceinline__ u32x4 from_next_lane(u32x4 x) { return dpp16<0x134>(x, x); }
-// lane l < 63 receives lane l+1's x, lane 63 keeps its own `last`
+// lane l < 63 receives lane l+1's x, lane 63 keeps its own `last` (the tuning code's other shifts:
+// tools/tune/misaligned_2pass.hpp)
 __device__ __forceinline__ u32x4 from_next_lane_or(u32x4 x, u32x4 last) { return dpp16<0x130>(x, last); }
-// lane l receives lane (l+63) % 64's vector
-__device__ __forceinline__ u32x4 from_prev_lane(u32x4 x) { return dpp16<0x13C>(x, x); }
-// lane l > 0 receives lane l-1's x, lane 0 keeps its own `first`
-__device__ __forceinline__ u32x4 from_prev_lane_or(u32x4 x, u32x4 first) { return dpp16<0x138>(x, first); }
 
 template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true>
 __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* __restrict__ send,
@@ -221,18 +225,15 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
 // ---------------------------------------------------------------------------------
 // A recv that is not element-aligned (e.g. fp32 at an odd byte address; the reference's host loop takes
 // it with a warning, internal_common.hpp:504-512, its CUDA kernel not at all).  gfx950 executes
-// global_load_dwordx4 / global_store_dwordx4 at any byte address (tools/unaligned_probe.hip checks every
-// element), so lane i simply moves the 16 bytes of elements [V i, V i + V) of each operand at their own
-// addresses (V = 16 / sizeof(T)): adjacent lanes' windows are disjoint and hold whole elements, so no byte
-// is written twice and nothing needs a neighbour's original bytes.  send is read as the shifted kernel
-// reads it (aligned loads, lane exchange, funnel shift by its own phase): unaligned send loads as well
-// cost a further 7-10 points.  A 1 KiB tile spans 9 lines of recv, one shared with the next tile;
-// consecutive tiles go to one XCD (blocks are dealt round-robin over the 8 XCDs), so the shared lines meet
-// in one L2.  1 GiB fp32 Sum on MI355X, recv + 1 B: 78.4-78.8 % of HBM peak under the caps::kUnaligned cap
-// (76.4-76.7 % uncapped), against 74.6-74.8 % with consecutive tiles on different XCDs and 72-73 % for a
-// byte-gather kernel; a two-pass form writing every recv vector whole from one wave reached 74-75.5 %
-// (tools/tune/, profiles/r2_misaligned_ab.json, r2_misaligned_caps.json).  The tail (< V elements) is
-// block 0's, element by element.  Kernel: after ld_phased below.
+// global_store_dwordx4 at any byte address (tools/unaligned_probe.hip checks every element), so lane i owns
+// the 16 bytes of elements [V i, V i + V) at their displaced address (V = 16 / sizeof(T)): adjacent lanes'
+// windows are disjoint and hold whole elements, so no byte is written twice.  Both operands' windows are
+// read the shifted kernel's way (aligned loads, lane exchange, funnel shift by the operand's own phase);
+// unaligned 16-B loads of recv ran 2-5 points slower, of send 7-10.  A 1 KiB tile spans 9 lines of recv,
+// one shared with the next tile: the launch takes the group-interleaved tile order (tile_order), so 7 of 8 such
+// lines meet in one L2 while the chip sweeps one front, uncapped: 85.1-85.2 % of peak, the aligned kernel's
+// rate, against 80.7-82.1 % for round 2's XCD ranges under a 24-wave cap (profiles/r3_s4_*).  The tail
+// (< V elements) is block 0's, element by element.  Kernel: after ld_phased below.
 // ---------------------------------------------------------------------------------
 typedef u32x4 u32x4_u __attribute__((aligned(1)));
 
@@ -333,13 +334,9 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sen
 // kernel's way: every lane loads the ALIGNED vector A_j[v] (non-temporal), lane 63 also loads A_j[v+1]
 // (through the caches), the other lanes take it from their right-hand neighbour (DPP wave shift), and
 // the 32 bytes are funnel-shifted by p_j (v_alignbyte_b32, any byte count).  An operand with p_j == 0 is
-// a plain vector load.  The head / tail scalars read operands bytewise (any alignment).
-// Measured on MI355X (tools/bench_suite.py --parts phased, profiles/r1_s5_phased_probe.json): one
-// operand at a time with a uniform branch on its phase, and no occupancy cap, beat issuing every
-// operand's loads before the first shift (branch-free selects) and the k-way kernel's wave caps:
-// 74-79 % of HBM peak for k = 1..7 against 45-61 %.  Round 2: the loads-first form with the same
-// uniform-branch shifts, under caps of its own, wins from k = 5 (k-way) / k = 4 (chain); see
-// caps::kMultiPhasedFirst (caps.hpp) and DESIGN.md §12.
+// a plain vector load.  The head / tail scalars read operands bytewise (any alignment).  One operand at a
+// time, uncapped (74-79 % of peak, profiles/r1_s5_phased_probe.json), or, from k = 5 (k-way) / k = 4 (chain),
+// every operand's loads first under caps of their own (below).
 // One-wave blocks and a per-tile loop uniform per wave: every lane reaches the lane exchange.
 // ---------------------------------------------------------------------------------
 struct PhaseList { unsigned p[9]; };
@@ -377,11 +374,9 @@ __device__ __forceinline__ u32x4 ld_phased_finish(const PhasedLoad& x, unsigned 
 // HBM peak gained: k-way k = 2 +2.1..+4.0, k = 3 +2.1..+2.5, k = 4 +0.6..+1.7, k = 5 -0.2..+0.8,
 // k = 7 -2.2..-5.1; the chain kernel (in place) within 0.5 points of the same at every k.
 inline constexpr int kPhasedXcdMaxK = 4;
-// From k = 5 (k-way) / k = 4 (chain) the phased kernels take the loads-first form (every operand's loads
-// issued before the first shift, ld_phased_issue / ld_phased_finish) under a wave cap of their own
-// (caps::kMultiPhasedFirst / kChainPhasedFirst in caps.hpp); below, and at k = 6, the per-operand form
-// above, uncapped.  Without a cap the loads-first form loses (too many streams in flight); with 11-13 waves it
-// wins by 1.5-6 points at k = 5, 7, 8.
+// From k = 5 (k-way) / k = 4 (chain), k = 6 aside, the phased kernels take the loads-first form
+// (ld_phased_issue / ld_phased_finish) under caps::kMultiPhasedFirst / kChainPhasedFirst (11-13 waves at
+// 1 GiB): +1.5-6 points at k = 5, 7, 8; uncapped it loses (too many streams in flight).
 
 // The 16 body bytes of vector v (zero for v >= nvec) of an operand whose body starts at `body`,
 // phase p.  All 64 lanes must call it (p is uniform).
@@ -406,20 +401,24 @@ __device__ __forceinline__ u32x4 ld_phased(const unsigned char* body, unsigned p
     }
 }
 
-// grid: a multiple of 8.  Block b takes tile (b % 8) * (grid / 8) + b / 8, then strides by grid.  send's
-// 16 bytes per lane come from aligned loads and the lane exchange (ld_phased, phase p = send & 15).
+// grid: a multiple of 8.  Block b takes tile (b % 8) * (grid / 8) + b / 8, then strides by grid.  Lane i's
+// window is recv's elements [V i, V i + V): its 16 bytes at the displaced address are read the shifted
+// kernel's way (aligned loads, lane exchange, funnel shift by recv & 15), like send's (phase p), all loads
+// issued before the first wait, and the result goes back with one 16-B store at the displaced address.
+// Reading recv through aligned loads instead of one unaligned 16-B load per lane: +2.4 points (recv + 1 B)
+// and +4.8 (recv + 2 B, send + 3 B) on one box, bit-exact (profiles/r3_s2_ab_recv_phased.json).  The bytes a
+// lane takes from A[v + 1] are its own window's, so the neighbouring tile's stores never touch them.
 template <typename T, int OP>
 __global__ __launch_bounds__(64) void reduce_unaligned_kernel(const unsigned char* __restrict__ send, unsigned p,
                                                               unsigned char* __restrict__ recv, size_t nvec,
-                                                              size_t count) {
+                                                              size_t count, int order) {
     const size_t g = gridDim.x;
-    for (size_t t = size_t(blockIdx.x % 8) * (g / 8) + blockIdx.x / 8; t * 64 < nvec; t += g) {
+    const unsigned pr = unsigned(reinterpret_cast<uintptr_t>(recv) & 15);
+    for (size_t t = tile_order(order, blockIdx.x, g); t * 64 < nvec; t += g) {
         const size_t i = t * 64 + threadIdx.x;
-        const u32x4 b = ld_phased(send, p, i, nvec);
-        if (i < nvec) {
-            u32x4_u* pr = reinterpret_cast<u32x4_u*>(recv + 16 * i);
-            __builtin_nontemporal_store(combine16<T, OP>(__builtin_nontemporal_load(pr), b), pr);
-        }
+        const PhasedLoad xr = ld_phased_issue(recv, pr, i, nvec), xs = ld_phased_issue(send, p, i, nvec);
+        const u32x4 o = combine16<T, OP>(ld_phased_finish(xr, pr), ld_phased_finish(xs, p));
+        if (i < nvec) __builtin_nontemporal_store(o, reinterpret_cast<u32x4_u*>(recv + 16 * i));
     }
     if (blockIdx.x == 0)
         for (size_t j = nvec * Pack<T>::N + threadIdx.x; j < count; j += 64)
@@ -519,23 +518,32 @@ __global__ __launch_bounds__(64) void reduce_chain_phased_kernel(SendList sends,
 // reads for it through ld_phased belong to lane i alone, so own may alias dst.  The tail (< V elements)
 // is block 0's, element by element.
 // ---------------------------------------------------------------------------------
-template <typename T, int OP, int K>
+template <typename T, int OP, int K, bool FIRST = false>
 __global__ __launch_bounds__(64) void reduce_multi_unaligned_kernel(SendList sends, PhaseList ph,
                                                                     unsigned char* __restrict__ recv, size_t nvec,
-                                                                    size_t count) {
+                                                                    size_t count, int order) {
     const size_t g = gridDim.x;
-    for (size_t t = size_t(blockIdx.x % 8) * (g / 8) + blockIdx.x / 8; t * 64 < nvec; t += g) {
+    const unsigned pr = unsigned(reinterpret_cast<uintptr_t>(recv) & 15);
+    for (size_t t = tile_order(order, blockIdx.x, g); t * 64 < nvec; t += g) {
         const size_t i = t * 64 + threadIdx.x;
-        u32x4 s[K];
+        const PhasedLoad xr = ld_phased_issue(recv, pr, i, nvec);  // recv's window, as reduce_unaligned_kernel
+        u32x4 acc;
+        if constexpr (FIRST) {  // every source's loads, then the shifts
+            PhasedLoad x[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k], ph.p[k], i, nvec);
-        if (i < nvec) {
-            u32x4_u* pr = reinterpret_cast<u32x4_u*>(recv + 16 * i);
-            u32x4 acc = __builtin_nontemporal_load(pr);
+            for (int k = 0; k < K; ++k) x[k] = ld_phased_issue(sends.p[k], ph.p[k], i, nvec);
+            acc = ld_phased_finish(xr, pr);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, ld_phased_finish(x[k], ph.p[k]));
+        } else {  // one source at a time
+            u32x4 s[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k], ph.p[k], i, nvec);
+            acc = ld_phased_finish(xr, pr);
 #pragma unroll
             for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, s[k]);
-            __builtin_nontemporal_store(acc, pr);
         }
+        if (i < nvec) __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_u*>(recv + 16 * i));
     }
     if (blockIdx.x == 0)
         for (size_t j = nvec * Pack<T>::N + threadIdx.x; j < count; j += 64) {
@@ -547,23 +555,33 @@ __global__ __launch_bounds__(64) void reduce_multi_unaligned_kernel(SendList sen
 }
 
 // Chain order as reduce_chain_vec_kernel; ph.p[K] is own's phase.
-template <typename T, int OP, int K>
+template <typename T, int OP, int K, bool FIRST = false>
 __global__ __launch_bounds__(64) void reduce_chain_unaligned_kernel(SendList sends, PhaseList ph,
                                                                     const unsigned char* own, unsigned char* dst,
-                                                                    size_t nvec, size_t count) {
+                                                                    size_t nvec, size_t count, int order) {
     const size_t g = gridDim.x;
-    for (size_t t = size_t(blockIdx.x % 8) * (g / 8) + blockIdx.x / 8; t * 64 < nvec; t += g) {
+    for (size_t t = tile_order(order, blockIdx.x, g); t * 64 < nvec; t += g) {
         const size_t i = t * 64 + threadIdx.x;
-        u32x4 s[K];
+        u32x4 acc, o;
+        if constexpr (FIRST) {  // every operand's loads, then the shifts
+            PhasedLoad x[K + 1];
 #pragma unroll
-        for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k], ph.p[k], i, nvec);
-        const u32x4 o = ld_phased(own, ph.p[K], i, nvec);
-        if (i < nvec) {
-            u32x4 acc = s[0];
+            for (int k = 0; k < K; ++k) x[k] = ld_phased_issue(sends.p[k], ph.p[k], i, nvec);
+            x[K] = ld_phased_issue(own, ph.p[K], i, nvec);
+            acc = ld_phased_finish(x[0], ph.p[0]);
+#pragma unroll
+            for (int k = 1; k < K; ++k) acc = combine16<T, OP>(ld_phased_finish(x[k], ph.p[k]), acc);
+            o = ld_phased_finish(x[K], ph.p[K]);
+        } else {
+            u32x4 s[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k], ph.p[k], i, nvec);
+            o = ld_phased(own, ph.p[K], i, nvec);
+            acc = s[0];
 #pragma unroll
             for (int k = 1; k < K; ++k) acc = combine16<T, OP>(s[k], acc);
-            __builtin_nontemporal_store(combine16<T, OP>(o, acc), reinterpret_cast<u32x4_u*>(dst + 16 * i));
         }
+        if (i < nvec) __builtin_nontemporal_store(combine16<T, OP>(o, acc), reinterpret_cast<u32x4_u*>(dst + 16 * i));
     }
     if (blockIdx.x == 0)
         for (size_t j = nvec * Pack<T>::N + threadIdx.x; j < count; j += 64) {

@@ -16,10 +16,22 @@ size_t unaligned_grid(size_t nvec) {
     return g == 0 ? 8 : g;
 }
 
+// Tile order: with every source at 16-B phase 0 (plain vector loads) one front for the chip wins, the
+// group-interleaved order up to k = 2 and block order above; sources at other phases keep consecutive tiles
+// on one XCD, where the vector lane 63 reads past its tile meets the next tile's first line in one L2.
+// 1 GiB fp32 Sum, destination + 2 B, one box (tools/unaligned_forms_probe.py, profiles/r3_s4_*): aligned sources
+// k = 2 80.0 -> 83.4 % (group), k = 4 74.6 -> 78.0 %, k = 8 71.7 -> 76.4 % (block); the chain the same.
+int unaligned_order(const PhaseList& ph, int nsend) {
+    for (int k = 0; k < nsend; ++k)
+        if (ph.p[k] != 0) return kOrderXcd;
+    return nsend <= 2 ? kOrderGroup : kOrderBlock;
+}
+
 template <typename T, int OP, int K>
 int launch_multi(SendList sl, PhaseList ph, unsigned char* r, size_t count, hipStream_t stream) {
     size_t nvec = count / Pack<T>::N;
-    void* args[] = {&sl, &ph, &r, &nvec, &count};
+    int order = unaligned_order(ph, K);
+    void* args[] = {&sl, &ph, &r, &nvec, &count, &order};
     return launch(reinterpret_cast<const void*>(&reduce_multi_unaligned_kernel<T, OP, K>), unaligned_grid(nvec), args,
                   stream, 64);
 }
@@ -28,7 +40,8 @@ template <typename T, int OP, int K>
 int launch_chain(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, size_t count,
                  hipStream_t stream) {
     size_t nvec = count / Pack<T>::N;
-    void* args[] = {&sl, &ph, &own, &d, &nvec, &count};
+    int order = unaligned_order(ph, K);  // the sources' phases decide; own is the destination's window
+    void* args[] = {&sl, &ph, &own, &d, &nvec, &count, &order};
     return launch(reinterpret_cast<const void*>(&reduce_chain_unaligned_kernel<T, OP, K>), unaligned_grid(nvec), args,
                   stream, 64);
 }

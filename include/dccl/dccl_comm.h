@@ -17,7 +17,11 @@
  *                         (reduce_scatter_ring.cpp:73-101, all_gather_ring.cpp:44-64) then run on it,
  *                         with the gfx950 combine after every receive.
  *   dccl_comm_init_ipc    cross-process group over the IPC peer-read transport (one process per GPU
- *                         on one node; rendezvous through DCCL_BOOTSTRAP_DIR, dcclCommInitIpc)
+ *                         on one node; rendezvous through DCCL_BOOTSTRAP_DIR, dcclCommInitIpc).  A failed
+ *                         collective aborts the group, like an aborted NCCL communicator: every later
+ *                         collective returns ncclRemoteError (6) until dccl_comm_finalize, which still
+ *                         returns and releases the shared segment and the peers' mappings.  (The
+ *                         in-process transport agrees per collective and stays usable after a failure.)
  *   dccl_bootstrap_unique_id  single-node exchange of the RCCL id through DCCL_BOOTSTRAP_DIR: rank 0
  *                         creates and publishes it, the others wait (DCCL_BOOTSTRAP_TIMEOUT_S, default
  *                         120 s) for a file published by a LIVE rank 0 of the same world size, so a

@@ -33,6 +33,7 @@ def test_dccl_allreduce_world1(monkeypatch):
         assert "error" not in res, res
         for name in ("ring", "direct"):
             assert res[name]["int32_sum_bit_exact_vs_rccl"] and res[name]["fp32_within_bound"], res
+            assert res[name]["broadcast_bit_exact"] and res[name]["reduce_bit_exact"], res
         assert res["fp32_direct_bit_exact_vs_ring"], res
     finally:
         dist.destroy_process_group()
@@ -68,6 +69,7 @@ def test_bench_direct_allreduce_two_processes_one_gpu():
     ar = res["dccl_allreduce"]
     assert "error" not in ar, ar
     assert ar["direct"]["int32_sum_bit_exact_vs_rccl"] and ar["direct"]["fp32_within_bound"], ar
+    assert ar["direct"]["broadcast_bit_exact"] and ar["direct"]["reduce_bit_exact"], ar
     assert ar["dccl_allgather"]["direct"]["bit_exact"], ar["dccl_allgather"]
     assert ar["c5_allgather"]["direct"]["bit_exact"], ar["c5_allgather"]
 
@@ -94,6 +96,7 @@ def test_bench_self_launch_two_ranks_one_gpu():
     assert res["c5"]["verified"] and res["other_layout"]["pairs"] == 2, res
     s = res["dccl_allreduce_summary"]
     assert s["direct"]["int32_sum_bit_exact_vs_rccl"] and s["dccl_allgather"]["direct"]["bit_exact"], s
+    assert s["direct"]["broadcast_bit_exact"] and s["direct"]["reduce_bit_exact"], s
     assert list(res)[-1] == "verified"
 
 

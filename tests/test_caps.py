@@ -44,7 +44,7 @@ int main() {
 }
 """
 
-NAMES = ["multi", "chain", "multi_straddle", "chain_straddle", "multi_phased_first", "chain_phased_first", "unaligned"]
+NAMES = ["multi", "chain", "multi_straddle", "chain_straddle", "multi_phased_first", "chain_phased_first"]
 # frozen table: class -> size class (<24, <48, <96 MiB, >=96 MiB) -> waves for k = 0..8 (0 = not used at that k)
 FROZEN = {
     "multi": [[0, 0, 32, 24, 16, 16, 16, 16, 32], [0, 0, 32, 20, 16, 16, 11, 10, 9],
@@ -59,10 +59,9 @@ FROZEN = {
                            [0, 0, 0, 0, 0, 13, 0, 12, 11], [0, 0, 0, 0, 0, 13, 0, 12, 11]],
     "chain_phased_first": [[0, 0, 0, 0, 24, 24, 0, 24, 16], [0, 0, 0, 0, 16, 16, 0, 16, 24],
                            [0, 0, 0, 0, 16, 13, 0, 11, 11], [0, 0, 0, 0, 13, 13, 0, 11, 11]],
-    "unaligned": [[0, 32] + [0] * 7, [0, 32] + [0] * 7, [0, 26] + [0] * 7, [0, 24] + [0] * 7],
 }
 K_RANGE = {"multi": (2, 8), "chain": (1, 8), "multi_straddle": (2, 8), "chain_straddle": (1, 8),
-           "multi_phased_first": (2, 8), "chain_phased_first": (1, 8), "unaligned": (1, 1)}
+           "multi_phased_first": (2, 8), "chain_phased_first": (1, 8)}
 
 
 @pytest.fixture(scope="module")
@@ -106,7 +105,6 @@ def test_size_class_boundaries(table):
     # kMulti k = 2 switches 32 -> 32 -> 24 -> 18 at 24 / 48 / 96 MiB; k = 3 24 -> 20 -> 16 -> 13
     assert [rows[("multi", b, 3)] for b in (24 * MiB - 1, 24 * MiB, 48 * MiB - 1, 48 * MiB, 96 * MiB - 1, 96 * MiB)] \
         == [24, 20, 20, 16, 16, 13]
-    assert rows[("unaligned", 96 * MiB - 1, 1)] == 26 and rows[("unaligned", 96 * MiB, 1)] == 24
     assert rows[("multi", 1024 * MiB, 8)] == rows[("multi", 96 * MiB, 8)] == 9
 
 

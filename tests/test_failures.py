@@ -214,3 +214,55 @@ def test_direct_combine_failure_reaches_every_rank(gpu, W, bad, kind):
     for r in range(W):
         want = 1 if r == bad else 6
         assert res["rcs"][r] == [want, want], res
+
+
+# ---------------------------------------------------------------------------------------------
+# the IPC transport after a failure: sticky abort, finalize still releases everything
+# ---------------------------------------------------------------------------------------------
+IPC_FAIL_CHILD = """
+import glob, json, os
+import torch
+import dccl_amd
+W, r = int(os.environ["W"]), int(os.environ["RANK_ID"])
+torch.cuda.set_device(0)
+comm = dccl_amd.Comm.ipc(W, r)
+n = 1024 * W
+x = torch.full((n,), float(r + 1), device="cuda")
+st = torch.cuda.current_stream().cuda_stream
+first = comm.all_reduce(x.data_ptr(), x.data_ptr(), n, 7, 0, st)
+torch.cuda.synchronize()
+second = comm.all_reduce(x.data_ptr(), x.data_ptr(), n, 7, 0, st)   # the abort is sticky on this transport
+torch.cuda.synchronize()
+fin = comm.finalize()
+print(json.dumps({"first": first, "second": second, "finalize": fin, "pid": os.getpid()}))
+"""
+
+
+@pytest.mark.gpu
+def test_ipc_failure_is_sticky_and_finalize_releases(gpu, tmp_path):
+    """On the IPC transport one rank's failed combine aborts the group: every rank gets an error, the next
+    collective returns ncclRemoteError at once (include/dccl/dccl_comm.h), and finalize still returns,
+    unmaps the shared segment and leaves no /dev/shm segment or rendezvous file behind."""
+    import uuid
+    W, tag = 2, "ipcfail_" + uuid.uuid4().hex[:10]
+    env = {**os.environ, "PYTHONPATH": ROOT, "W": str(W), "DCCL_BOOTSTRAP_TAG": tag, "DCCL_BOOTSTRAP_DIR": str(tmp_path),
+           "DCCL_FAULT_INJECT": "direct_combine:1", "DCCL_IPC_TIMEOUT_S": "20"}
+    ps = [subprocess.Popen([sys.executable, "-c", textwrap.dedent(IPC_FAIL_CHILD)], env={**env, "RANK_ID": str(r)},
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(W)]
+    outs = []
+    try:
+        for p in ps:
+            o, e = p.communicate(timeout=120)
+            assert p.returncode == 0, e[-2000:]
+            outs.append(json.loads(o.strip().splitlines()[-1]))
+    finally:
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert outs[1]["first"] == 1 and outs[0]["first"] == 6, outs
+    assert outs[0]["second"] == 6 and outs[1]["second"] != 0, outs
+    assert all(o["finalize"] in (0, 6) for o in outs), outs
+    import glob
+    assert not glob.glob(f"/dev/shm/dccl_ipc_{outs[0]['pid']}_*"), "rank 0's segment left behind"
+    assert not list(tmp_path.iterdir()), list(tmp_path.iterdir())

@@ -138,7 +138,7 @@ def swap_tiling(a, recv, srcs, n, nbytes, st, rows):
                     lds = 0 if w >= 32 else ((160 << 10) // w + 255) // 256 * 256
                     own = None if what == "multi" else r0 + 12
                     fn = lambda lds=lds, own=own: dccl_amd.check(tune_lib.lib.dccl_tune_unaligned_kway_f32_sum(
-                        arr_sw, k, own, r0 + 12, n - 3, lds, st), "swap")
+                        arr_sw, k, own, r0 + 12, n - 3, lds, 0, st), "swap")
                     t[w].append(time_launches([fn], rounds=1, min_ms=20.0)[0])
             for key, v in t.items():
                 ms = statistics.median(v)

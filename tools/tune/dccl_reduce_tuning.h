@@ -78,9 +78,13 @@ int dccl_tune_phased_prod_f32_sum(const void* const* sends, int nsend, const voi
 /* the shipped shifted-kernel dispatch under an explicit wave cap (lds_bytes of unused LDS per block) */
 int dccl_tune_shift_caps_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes, void* stream);
 
-/* the unaligned k-way (own NULL) / chain kernels called directly on any operands, under a wave cap */
+/* the unaligned k-way (own NULL) / chain kernels called directly on any operands, under a wave cap; form bit 0:
+ * the loads-first form, form >> 1: the tile order (0 XCD-contiguous, 1 block order, 2 group-interleaved) */
 int dccl_tune_unaligned_kway_f32_sum(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
-                                     size_t lds_bytes, void* stream);
+                                     size_t lds_bytes, int form, void* stream);
+/* the pairwise misaligned-recv kernel under a wave cap and tile order */
+int dccl_tune_unaligned_pair_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes, int order,
+                                     void* stream);
 
 #ifdef __cplusplus
 }

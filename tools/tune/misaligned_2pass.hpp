@@ -32,6 +32,16 @@
 #include "reduce_kernels.hpp"
 
 namespace dccl_amd {
+// Tuning-only cross-lane moves (the product needs only from_next_lane_or, reduce_kernels.hpp).
+// lane l receives lane (l+1) % 64's vector
+__device__ __forceinline__ u32x4 from_next_lane(u32x4 x) { return dpp16<0x134>(x, x); }
+// lane l receives lane (l+63) % 64's vector
+__device__ __forceinline__ u32x4 from_prev_lane(u32x4 x) { return dpp16<0x13C>(x, x); }
+// lane l > 0 receives lane l-1's x, lane 0 keeps its own `first`
+__device__ __forceinline__ u32x4 from_prev_lane_or(u32x4 x, u32x4 first) { return dpp16<0x138>(x, first); }
+}  // namespace dccl_amd
+
+namespace dccl_amd {
 namespace mis {
 
 struct Geometry {

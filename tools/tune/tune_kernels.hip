@@ -926,7 +926,8 @@ extern "C" int dccl_tune_misaligned_f32_sum(const void* send, void* recv, size_t
         unsigned p = unsigned(reinterpret_cast<uintptr_t>(send) & 15);
         size_t cnt = count;
         size_t nv = nvec;
-        void* args[] = {const_cast<unsigned char**>(&s), &p, const_cast<unsigned char**>(&r), &nv, &cnt};
+        int order = kOrderXcd;  // the round-2 order these caps were measured in
+        void* args[] = {const_cast<unsigned char**>(&s), &p, const_cast<unsigned char**>(&r), &nv, &cnt, &order};
         return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<float, kSum>), grid, args, st, 64, lds);
     }
     // the shipped kernel with write-back stores in the tile's shared edge sectors (tune_unaligned_edge_kernel):
@@ -1362,25 +1363,34 @@ extern "C" int dccl_tune_shift_caps_f32_sum(const void* send, void* recv, size_t
 // explicit wave cap: used to try "sources aligned, destination at another phase" tilings.
 // ---------------------------------------------------------------------------------
 namespace {
-template <int K>
+template <int K, bool FIRST>
 int tune_unaligned_kway_k(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, size_t count,
-                          hipStream_t st, size_t lds) {
+                          hipStream_t st, size_t lds, int order) {
     size_t nvec = count / 4;
     const size_t grid = ceil_div(ceil_div(nvec, size_t(64)), size_t(8)) * 8;
     if (own == nullptr) {
-        void* args[] = {&sl, &ph, &d, &nvec, &count};
-        return launch(reinterpret_cast<const void*>(&reduce_multi_unaligned_kernel<float, kSum, K>), grid, args, st,
-                      64, lds);
+        void* args[] = {&sl, &ph, &d, &nvec, &count, &order};
+        return launch(reinterpret_cast<const void*>(&reduce_multi_unaligned_kernel<float, kSum, K, FIRST>), grid,
+                      args, st, 64, lds);
     }
-    void* args[] = {&sl, &ph, &own, &d, &nvec, &count};
-    return launch(reinterpret_cast<const void*>(&reduce_chain_unaligned_kernel<float, kSum, K>), grid, args, st, 64,
-                  lds);
+    void* args[] = {&sl, &ph, &own, &d, &nvec, &count, &order};
+    return launch(reinterpret_cast<const void*>(&reduce_chain_unaligned_kernel<float, kSum, K, FIRST>), grid,
+                  args, st, 64, lds);
+}
+template <int K>
+int tune_unaligned_kway_form(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, size_t count,
+                             hipStream_t st, size_t lds, int form) {
+    if ((form >> 1) > 2) return DCCL_INVALID_ARGUMENT;
+    return (form & 1) ? tune_unaligned_kway_k<K, true>(sl, ph, own, d, count, st, lds, form >> 1)
+                      : tune_unaligned_kway_k<K, false>(sl, ph, own, d, count, st, lds, form >> 1);
 }
 }  // namespace
 
+// form: bit 0 = the loads-first form (reduce_kernels.hpp FIRST), form >> 1 = the tile ORDER (0 XCD-contiguous,
+// 1 block order, 2 group-interleaved).
 extern "C" int dccl_tune_unaligned_kway_f32_sum(const void* const* sends, int nsend, const void* own, void* dst,
-                                                size_t count, size_t lds_bytes, void* stream) {
-    if (sends == nullptr || dst == nullptr || nsend < 2 || nsend > 8 || lds_bytes > (64u << 10))
+                                                size_t count, size_t lds_bytes, int form, void* stream) {
+    if (sends == nullptr || dst == nullptr || nsend < 1 || nsend > 8 || lds_bytes > (64u << 10))
         return DCCL_INVALID_ARGUMENT;
     SendList sl{};
     PhaseList ph{};
@@ -1390,7 +1400,27 @@ extern "C" int dccl_tune_unaligned_kway_f32_sum(const void* const* sends, int ns
     }
     const auto o = static_cast<const unsigned char*>(own);
     if (o != nullptr) ph.p[nsend] = phase_word(o, 0);
+    if (o == nullptr && nsend < 2) return DCCL_INVALID_ARGUMENT;
     auto d = static_cast<unsigned char*>(dst);
     const auto st = static_cast<hipStream_t>(stream);
-    return with_k<2, 8>(nsend, [&](auto K) { return tune_unaligned_kway_k<K.value>(sl, ph, o, d, count, st, lds_bytes); });
+    return with_k<1, 8>(nsend, [&](auto K) {
+        return tune_unaligned_kway_form<K.value>(sl, ph, o, d, count, st, lds_bytes, form);
+    });
+}
+
+// The pairwise misaligned-recv kernel (reduce_unaligned_kernel) under an explicit cap and tile order (0 XCD-
+// contiguous, 1 block order, 2 group-interleaved); recv not element-aligned.
+extern "C" int dccl_tune_unaligned_pair_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes,
+                                                int order, void* stream) {
+    if ((reinterpret_cast<uintptr_t>(recv) & 3) == 0 || lds_bytes > (64u << 10)) return DCCL_INVALID_ARGUMENT;
+    const unsigned char* s = static_cast<const unsigned char*>(send);
+    unsigned char* r = static_cast<unsigned char*>(recv);
+    size_t nvec = count / 4;
+    unsigned p = unsigned(reinterpret_cast<uintptr_t>(send) & 15);
+    size_t grid = ceil_div(ceil_div(nvec, size_t(64)), size_t(8)) * 8;
+    if (grid == 0) grid = 8;
+    if (order < 0 || order > 2) return DCCL_INVALID_ARGUMENT;
+    void* args[] = {&s, &p, &r, &nvec, &count, &order};
+    return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<float, kSum>), grid, args,
+                  static_cast<hipStream_t>(stream), 64, lds_bytes);
 }
