@@ -334,6 +334,47 @@ def test_multi_byte_offsets(dccl, k):
                 assert not tr[:roff].any() and not tr[roff + nb:].any(), (k, dt, n, offs, roff)
 
 
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 8])
+def test_misaligned_destination_tile_orders(dccl, k):
+    """A destination that is not element-aligned, with sources at 16-B phase 0 (the kernels take the group-
+    interleaved order for k <= 2 and block order above, reduce_kernels.hpp tile_order) and at phase 4 (XCD
+    ranges), k-way and chain (own = dst, in place), at tile counts below one group of 64, exactly two groups,
+    and several groups plus a partial one: every element against the oracle applied in order (k-way) and in
+    the ring's chain order, nothing outside the destination written."""
+    rng = np.random.default_rng(1700 + k)
+    for dt in (7, 9, 4):
+        esz = int(oracle.NP_DTYPES[dt]().itemsize)
+        per_tile = 64 * (16 // esz)
+        for n in (per_tile * 5 + 3, per_tile * 128, per_tile * 200 + 7):
+            for src_phase in (0, 4):
+                op = int(rng.integers(0, 4))
+                sends = [rand_inputs(rng, dt, n)[0] for _ in range(k)]
+                _, r = rand_inputs(rng, dt, n)
+                holders = [dev_bytes(x, 16 * j + src_phase) for j, x in enumerate(sends)]
+                roff = 32 + 1 + int(rng.integers(0, esz - 1))
+                # k-way (k = 1 is the pairwise kernel)
+                tr, pr = dev_bytes(r, roff)
+                rc = dccl.local_reduce(holders[0][1], pr, dt, n, op, 0) if k == 1 else \
+                    dccl.local_reduce_multi([h[1] for h in holders], pr, dt, n, op, 0)
+                assert rc == 0
+                torch.cuda.synchronize()
+                want = r
+                for x in sends:
+                    want = expected(x, want, dt, op)
+                assert fp_equal(host_of(tr, roff, r), want, dt), ("multi", k, dt, n, op, src_phase, roff)
+                assert not tr[:roff].any() and not tr[roff + n * esz:].any()
+                # chain, in place: dst = op(own, op(s[k-1], ... op(s[1], s[0])))
+                to, po = dev_bytes(r, roff)
+                assert dccl.local_reduce_chain([h[1] for h in holders], po, po, dt, n, op, 0) == 0
+                torch.cuda.synchronize()
+                acc = sends[0]
+                for x in sends[1:]:
+                    acc = expected(acc, x, dt, op)
+                want_c = expected(acc, r, dt, op)
+                assert fp_equal(host_of(to, roff, r), want_c, dt), ("chain", k, dt, n, op, src_phase, roff)
+                assert not to[:roff].any() and not to[roff + n * esz:].any()
+
+
 # ----------------------------------------------------------------------------- host path
 @pytest.mark.parametrize("zero_copy", ["default", "0"])
 @pytest.mark.parametrize("pinned", ["none", "both", "send"])

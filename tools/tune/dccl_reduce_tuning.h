@@ -86,6 +86,11 @@ int dccl_tune_unaligned_kway_f32_sum(const void* const* sends, int nsend, const 
 int dccl_tune_unaligned_pair_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes, int order,
                                      void* stream);
 
+/* the persistent work-queue combine (fp32 Sum, aligned): variant = tiles per grab (1-32) or 100 + grab for the
+ * pipelined form; waves_per_cu one-wave blocks per CU; counter = two zeroed 64-bit words (reset by the kernel) */
+int dccl_tune_wq_f32_sum(const void* send, void* recv, size_t count, int variant, int waves_per_cu, void* counter,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1424,3 +1424,95 @@ extern "C" int dccl_tune_unaligned_pair_f32_sum(const void* send, void* recv, si
     return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<float, kSum>), grid, args,
                   static_cast<hipStream_t>(stream), 64, lds_bytes);
 }
+
+// ---------------------------------------------------------------------------------
+// Tuning only (round 3): a persistent work-queue form of the aligned fp32 Sum combine.  `waves` one-wave
+// blocks per CU take GRAB consecutive 1 KiB tiles at a time from a device counter (one returning vector
+// atomic per grab by lane 0, prefetched one grab ahead), so the chip's access front stays as tight as the
+// one-shot grid's without dispatching 1 M workgroups.  PIPE: the next tile's loads are issued before the
+// current tile's store.  Every wave leaves the loop once the counter passes the last tile; the last wave
+// to finish resets ctr[0..1] for the next launch (stream order makes the reset visible to it).
+// ctr: two zero-initialised 64-bit words in device memory, one pair per concurrently running launch.
+// ---------------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ unsigned long long bcast_lane0(unsigned long long x) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(x)), hi = __builtin_amdgcn_readfirstlane(unsigned(x >> 32));
+    return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+
+template <int GRAB, bool PIPE>
+__global__ __launch_bounds__(64) void tune_wq_kernel(const u32x4* __restrict__ vs, u32x4* __restrict__ vr,
+                                                     unsigned long long ntiles, unsigned long long* ctr) {
+    unsigned long long t = 0, nt = 0;
+    if (threadIdx.x == 0) t = atomicAdd(ctr, static_cast<unsigned long long>(GRAB));
+    t = bcast_lane0(t);
+    while (t < ntiles) {
+        if (threadIdx.x == 0) nt = atomicAdd(ctr, static_cast<unsigned long long>(GRAB));  // the next grab, early
+        const unsigned long long end = t + GRAB < ntiles ? t + GRAB : ntiles;
+        if constexpr (PIPE) {
+            size_t i = size_t(t) * 64 + threadIdx.x;
+            u32x4 s = __builtin_nontemporal_load(vs + i), r = __builtin_nontemporal_load(vr + i);
+            for (unsigned long long u = t + 1; u <= end; ++u) {
+                const size_t j = size_t(u) * 64 + threadIdx.x;
+                u32x4 s2{0u, 0u, 0u, 0u}, r2{0u, 0u, 0u, 0u};
+                if (u < end) {
+                    s2 = __builtin_nontemporal_load(vs + j);
+                    r2 = __builtin_nontemporal_load(vr + j);
+                }
+                __builtin_nontemporal_store(combine16<float, kSum>(r, s), vr + i);
+                s = s2;
+                r = r2;
+                i = j;
+            }
+        } else {
+            for (unsigned long long u = t; u < end; ++u) {
+                const size_t i = size_t(u) * 64 + threadIdx.x;
+                const u32x4 s = __builtin_nontemporal_load(vs + i), r = __builtin_nontemporal_load(vr + i);
+                __builtin_nontemporal_store(combine16<float, kSum>(r, s), vr + i);
+            }
+        }
+        t = bcast_lane0(nt);
+    }
+    if (threadIdx.x == 0) {
+        const unsigned long long d = atomicAdd(ctr + 1, 1ull);
+        if (d == gridDim.x - 1) {  // every other wave has left the loop: reset for the next launch
+            ctr[0] = 0;
+            ctr[1] = 0;
+        }
+    }
+}
+
+template <int GRAB, bool PIPE>
+int tune_wq_launch(const u32x4* vs, u32x4* vr, unsigned long long ntiles, unsigned long long* ctr, size_t grid,
+                   hipStream_t st) {
+    void* args[] = {&vs, &vr, &ntiles, &ctr};
+    return launch(reinterpret_cast<const void*>(&tune_wq_kernel<GRAB, PIPE>), grid, args, st, 64);
+}
+}  // namespace
+
+// variant: grab (tiles per atomic) 1, 2, 4, 8, 16 or 32, plus 100 for the pipelined form; waves per CU 1-32.
+// count a multiple of 256 floats, 16-B aligned operands.
+extern "C" int dccl_tune_wq_f32_sum(const void* send, void* recv, size_t count, int variant, int waves_per_cu,
+                                    void* counter, void* stream) {
+    if (count % 256 || waves_per_cu < 1 || waves_per_cu > 32 || counter == nullptr) return DCCL_INVALID_ARGUMENT;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) cus = 256;
+    const auto vs = static_cast<const u32x4*>(send);
+    const auto vr = static_cast<u32x4*>(recv);
+    const unsigned long long ntiles = count / 256;
+    const size_t grid = size_t(cus) * size_t(waves_per_cu);
+    auto* ctr = static_cast<unsigned long long*>(counter);
+    const auto st = static_cast<hipStream_t>(stream);
+    switch (variant) {
+    case 1: return tune_wq_launch<1, false>(vs, vr, ntiles, ctr, grid, st);
+    case 2: return tune_wq_launch<2, false>(vs, vr, ntiles, ctr, grid, st);
+    case 4: return tune_wq_launch<4, false>(vs, vr, ntiles, ctr, grid, st);
+    case 8: return tune_wq_launch<8, false>(vs, vr, ntiles, ctr, grid, st);
+    case 16: return tune_wq_launch<16, false>(vs, vr, ntiles, ctr, grid, st);
+    case 32: return tune_wq_launch<32, false>(vs, vr, ntiles, ctr, grid, st);
+    case 104: return tune_wq_launch<4, true>(vs, vr, ntiles, ctr, grid, st);
+    case 108: return tune_wq_launch<8, true>(vs, vr, ntiles, ctr, grid, st);
+    case 116: return tune_wq_launch<16, true>(vs, vr, ntiles, ctr, grid, st);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
+}
