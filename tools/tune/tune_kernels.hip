@@ -347,6 +347,10 @@ int tune_multi_k(int variant, SendList sl, unsigned char* r, Split sp, hipStream
     case 14: return tune_multi_edge_cached<K>(sl, r, sp, st, lds);
     case 15: return tune_multi_group<K, kNtRecv | kNtStore>(sl, r, sp, st, lds);
     case 16: return tune_multi_group<K, kNtSend | kNtRecv | kNtStore>(sl, r, sp, st, lds);
+    // round 3: the line-straddling rule (sources through the caches) with 2 / 4 consecutive vectors per lane,
+    // so a wave's tile is 2 / 4 KiB and only one line per tile is shared with the neighbouring wave
+    case 17: return tune_multi_launch<K, VecCfg<64, 2, 6, false, 1>>(sl, r, sp, st, lds);
+    case 18: return tune_multi_launch<K, VecCfg<64, 4, 6, false, 1>>(sl, r, sp, st, lds);
     default: return DCCL_INVALID_ARGUMENT;
     }
 }
