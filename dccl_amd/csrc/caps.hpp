@@ -52,8 +52,12 @@ constexpr int size_class(size_t bytes) {
 //              second box r2_kway_straddle_caps_ab.json: k-way k = 6 74.1 -> 79.0 %, chain k = 4 77.3 ->
 //              80.2 %); size rows r2_s70_kway_size_caps_straddle*.json.
 //  kMultiPhasedFirst / kChainPhasedFirst  the loads-first form wins from k = 5 (k-way) / k = 4 (chain)
-//              under these caps on two boxes (r2_phased_first_caps.json, r2_phased_first_ab.json); k = 6
-//              keeps the per-operand form (the two disagree in sign); size rows r2_s70_..._phased.json.
+//              under these caps on two boxes (r2_phased_first_caps.json, r2_phased_first_ab.json); size rows
+//              r2_s70_..._phased.json.  Round 3: in the tile-run order of kRun the loads-first form also wins at
+//              k-way k = 4, 6 and chain k = 3, and the k-way k = 7, 8 / chain k = 7 caps move to 13 (+2.0 to
+//              +3.7 points on two boxes, r3_s11_runs_straddle_phased.json, r3_s12_runs_confirm_*.json,
+//              r3_s10_phased_run_orders.json); their size rows take the 1 GiB value (not swept).
+//  kMultiStraddle k = 8: 9 waves in kRun's order (+2.4 to +3.3 on four boxes, r3_s9..s12).
 // The misaligned-recv kernel took a cap of its own in round 2 (24 waves); round 3's form (recv read through
 // aligned loads, group-interleaved tile order) runs best uncapped (profiles/r3_s4_unaligned_orders_caps.json),
 // so that row is gone.
@@ -69,21 +73,36 @@ inline constexpr unsigned char kWaves[kNumKernels][kSizeClasses][9] = {
      {0, 32, 24, 20, 16, 13, 11, 10, 9}},
     {{0, 0, 32, 24, 16, 16, 16, 16, 32},  // kMultiStraddle
      {0, 0, 24, 16, 13, 11, 16, 9, 32},
-     {0, 0, 24, 16, 13, 11, 9, 9, 7},
-     {0, 0, 18, 13, 13, 11, 9, 9, 7}},
+     {0, 0, 24, 16, 13, 11, 9, 9, 9},
+     {0, 0, 18, 13, 13, 11, 9, 9, 9}},
     {{0, 32, 32, 32, 24, 24, 16, 16, 16},  // kChainStraddle
      {0, 32, 32, 32, 24, 16, 11, 10, 9},
      {0, 32, 32, 24, 16, 13, 11, 10, 9},
      {0, 32, 24, 18, 13, 13, 11, 10, 9}},
-    {{0, 0, 0, 0, 0, 16, 0, 24, 16},  // kMultiPhasedFirst
-     {0, 0, 0, 0, 0, 16, 0, 16, 24},
-     {0, 0, 0, 0, 0, 13, 0, 12, 11},
-     {0, 0, 0, 0, 0, 13, 0, 12, 11}},
-    {{0, 0, 0, 0, 24, 24, 0, 24, 16},  // kChainPhasedFirst
-     {0, 0, 0, 0, 16, 16, 0, 16, 24},
-     {0, 0, 0, 0, 16, 13, 0, 11, 11},
-     {0, 0, 0, 0, 13, 13, 0, 11, 11}},
+    {{0, 0, 0, 0, 16, 16, 13, 24, 16},  // kMultiPhasedFirst
+     {0, 0, 0, 0, 16, 16, 13, 16, 24},
+     {0, 0, 0, 0, 16, 13, 13, 13, 13},
+     {0, 0, 0, 0, 16, 13, 13, 13, 13}},
+    {{0, 0, 0, 16, 24, 24, 0, 24, 16},  // kChainPhasedFirst
+     {0, 0, 0, 16, 16, 16, 0, 16, 24},
+     {0, 0, 0, 16, 16, 13, 0, 13, 11},
+     {0, 0, 0, 16, 13, 13, 0, 13, 11}},
 };
+
+// kRun[kernel][k]: the tile-run order of the launch (reduce_kernels.hpp run_tile<RUN>: each XCD walks RUN
+// consecutive tiles of every group of 8 RUN blocks; 1 = block order).  Runs of 4 keep the chip on one front
+// while the line two neighbouring tiles share (lane 63's extra load of an off-phase operand, a straddling
+// source's partial line) is fetched by one L2 in 3 of 4 cases (round 3, the files above).  The phased
+// per-operand form (kPhasedXcdMaxK) keeps consecutive tiles on one XCD and is not covered by this table.
+inline constexpr unsigned char kRun[kNumKernels][9] = {
+    {1, 1, 1, 1, 1, 1, 1, 1, 1},  // kMulti
+    {1, 1, 1, 1, 1, 1, 1, 1, 1},  // kChain
+    {1, 1, 1, 1, 1, 1, 1, 1, 4},  // kMultiStraddle
+    {1, 1, 1, 1, 1, 1, 1, 1, 1},  // kChainStraddle
+    {1, 1, 1, 1, 4, 1, 4, 4, 4},  // kMultiPhasedFirst
+    {1, 1, 1, 4, 1, 1, 1, 4, 4},  // kChainPhasedFirst
+};
+constexpr int tile_run(Kernel c, int k) { return (c < 0 || c >= kNumKernels || k < 0 || k > 8) ? 1 : kRun[c][k]; }
 
 // The valid k range of each class (the launchers' with_k bounds).
 constexpr int min_k(Kernel c) { return c == kMulti || c == kMultiStraddle || c == kMultiPhasedFirst ? 2 : 1; }
@@ -134,6 +153,9 @@ constexpr bool table_ok() {
                 if (phased && w != 0 && (w < 7 || w > kUncapped)) return false;
                 if (phased && (w == 0) != (kWaves[c][3][k] == 0)) return false;         // one form per k
                 if (lds_for_waves(w) > kMaxLdsPerBlock) return false;
+                const int run = kRun[c][k];
+                if (run != 1 && run != 2 && run != 4 && run != 8) return false;  // run_tile's groups
+                if (run != 1 && phased && w == 0) return false;  // a run only for the loads-first form
             }
     return true;
 }

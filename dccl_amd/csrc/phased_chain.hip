@@ -19,8 +19,9 @@ int launch_phased(SendList sl, PhaseList ph, const unsigned char* own, unsigned 
     // the per-operand form uncapped (with the XCD order up to kPhasedXcdMaxK), or the loads-first form under
     // its own cap (caps::kChainPhasedFirst, caps.hpp)
     if constexpr (caps::phased_loads_first(true, K))
-        return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K, false, true>), grid, args,
-                      stream, 64, caps::lds(caps::kChainPhasedFirst, K, sp.nvec * 16));
+        return launch(reinterpret_cast<const void*>(
+                          &reduce_chain_phased_kernel<T, OP, K, false, true, caps::tile_run(caps::kChainPhasedFirst, K)>),
+                      grid, args, stream, 64, caps::lds(caps::kChainPhasedFirst, K, sp.nvec * 16));
     return launch(reinterpret_cast<const void*>(&reduce_chain_phased_kernel<T, OP, K, (K <= kPhasedXcdMaxK)>), grid, args, stream, 64);
 }
 

@@ -19,19 +19,22 @@ int launch_phased(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStre
     // the per-operand form uncapped (with the XCD order up to kPhasedXcdMaxK), or the loads-first form under
     // its own cap (caps::kMultiPhasedFirst, caps.hpp)
     if constexpr (caps::phased_loads_first(false, K))
-        return launch(reinterpret_cast<const void*>(&reduce_multi_phased_kernel<T, OP, K, false, true>), grid, args,
-                      stream, 64, caps::lds(caps::kMultiPhasedFirst, K, sp.nvec * 16));
+        return launch(reinterpret_cast<const void*>(
+                          &reduce_multi_phased_kernel<T, OP, K, false, true, caps::tile_run(caps::kMultiPhasedFirst, K)>),
+                      grid, args, stream, 64, caps::lds(caps::kMultiPhasedFirst, K, sp.nvec * 16));
     return launch(reinterpret_cast<const void*>(&reduce_multi_phased_kernel<T, OP, K, (K <= kPhasedXcdMaxK)>), grid, args, stream, 64);
 }
 
-using StraddleKwayCfg = VecCfg<64, 1, kNtRecv | kNtStore, false>;
+// sources through the caches, in the tile-run order of caps::kRun
+template <int K>
+using StraddleKwayCfg = VecCfg<64, 1, kNtRecv | kNtStore, false, 0, caps::tile_run(caps::kMultiStraddle, K)>;
 
 template <typename T, int OP, int K>
 int launch_straddle(SendList sl, unsigned char* r, Split sp, hipStream_t stream) {
     size_t grid = ceil_div(sp.nvec, size_t(64));
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
-    return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, StraddleKwayCfg>), grid, args, stream, 64,
+    return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<T, OP, K, StraddleKwayCfg<K>>), grid, args, stream, 64,
                   caps::lds(caps::kMultiStraddle, K, sp.nvec * 16));
 }
 

@@ -54,9 +54,9 @@ __device__ __forceinline__ void st_elem(unsigned char* base, size_t i, T v) {
 // bits, XCD: remap block ids so that each XCD's blocks walk one contiguous range.
 // TAG keeps instantiations of different translation units distinct (production: 0, tuning: 1),
 // so no kernel symbol is registered from two code objects.
-template <int BLOCK_, int UNROLL_, int POLICY_, bool XCD_, int TAG = 0>
+template <int BLOCK_, int UNROLL_, int POLICY_, bool XCD_, int TAG = 0, int RUN_ = 1>
 struct VecCfg {
-    static constexpr int BLOCK = BLOCK_, UNROLL = UNROLL_, POLICY = POLICY_;
+    static constexpr int BLOCK = BLOCK_, UNROLL = UNROLL_, POLICY = POLICY_, RUN = RUN_;  // RUN: run_tile below
     static constexpr bool XCD = XCD_;
     static constexpr size_t TILE = size_t(BLOCK_) * UNROLL_;
 };
@@ -105,14 +105,19 @@ __device__ __forceinline__ size_t xcd_remap(size_t b, size_t nb) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-// Group-interleaved XCD order: in every full group of 64 blocks, block 64q + r (XCD r % 8 under the
-// round-robin dispatch) takes tile 64q + 8 (r % 8) + r / 8, so each XCD walks 8 consecutive tiles of the
-// group while the groups still sweep the range in order.  A line two neighbouring tiles share is then
-// fetched by one L2 in 7 of 8 cases.  A partial last group keeps the identity.  Bijective on [0, nb).
-__device__ __forceinline__ size_t xcd_group_tile(size_t b, size_t nb) {
-    const size_t q = b / 64, r = b % 64;
-    return (q + 1) * 64 > nb ? b : q * 64 + (r % 8) * 8 + r / 8;
+// Tile-run order: in every full group of 8 RUN blocks, block 8 RUN q + r (XCD r % 8 under the round-robin
+// dispatch) takes tile 8 RUN q + RUN (r % 8) + r / 8, so each XCD walks RUN consecutive tiles of the group
+// while the groups sweep the range in order: a line two neighbouring tiles share is fetched by one L2 in
+// RUN - 1 of RUN cases.  RUN 1 is block order, RUN 8 the group-interleaved order (xcd_group_tile).  A partial
+// last group keeps the identity.  Bijective on [0, nb).
+template <int RUN>
+__device__ __forceinline__ size_t run_tile(size_t b, size_t nb) {
+    if constexpr (RUN == 1) return b;
+    constexpr size_t span = size_t(8) * RUN;
+    const size_t q = b / span, r = b % span;
+    return (q + 1) * span > nb ? b : q * span + (r % 8) * RUN + r / 8;
 }
+__device__ __forceinline__ size_t xcd_group_tile(size_t b, size_t nb) { return run_tile<8>(b, nb); }
 
 // First tile of block b of a g-block grid (g a multiple of 8) for the misaligned-destination kernels, by a
 // uniform runtime `order`: kOrderXcd gives each XCD one contiguous range (consecutive tiles on one XCD: the
@@ -247,7 +252,8 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_multi_vec_kernel(SendList sen
                                                                     size_t head, size_t nvec, size_t tail) {
     u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
     const size_t ntiles = (nvec + C::TILE - 1) / C::TILE;
-    for (size_t t = C::XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (size_t t = C::XCD ? xcd_remap(blockIdx.x, gridDim.x) : run_tile<C::RUN>(blockIdx.x, gridDim.x); t < ntiles;
+         t += gridDim.x) {
         const size_t base = t * C::TILE + threadIdx.x;
         u32x4 r[C::UNROLL], s[K][C::UNROLL];
 #pragma unroll
@@ -301,7 +307,8 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sen
     const u32x4* vo = reinterpret_cast<const u32x4*>(own + off);
     u32x4* vd = reinterpret_cast<u32x4*>(dst + off);
     const size_t ntiles = (nvec + C::TILE - 1) / C::TILE;
-    for (size_t t = C::XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (size_t t = C::XCD ? xcd_remap(blockIdx.x, gridDim.x) : run_tile<C::RUN>(blockIdx.x, gridDim.x); t < ntiles;
+         t += gridDim.x) {
         const size_t i = t * C::TILE + threadIdx.x;
         if (i < nvec) {
             u32x4 s[K];
@@ -374,9 +381,9 @@ __device__ __forceinline__ u32x4 ld_phased_finish(const PhasedLoad& x, unsigned 
 // HBM peak gained: k-way k = 2 +2.1..+4.0, k = 3 +2.1..+2.5, k = 4 +0.6..+1.7, k = 5 -0.2..+0.8,
 // k = 7 -2.2..-5.1; the chain kernel (in place) within 0.5 points of the same at every k.
 inline constexpr int kPhasedXcdMaxK = 4;
-// From k = 5 (k-way) / k = 4 (chain), k = 6 aside, the phased kernels take the loads-first form
-// (ld_phased_issue / ld_phased_finish) under caps::kMultiPhasedFirst / kChainPhasedFirst (11-13 waves at
-// 1 GiB): +1.5-6 points at k = 5, 7, 8; uncapped it loses (too many streams in flight).
+// Where caps::kMultiPhasedFirst / kChainPhasedFirst (caps.hpp) have an entry, the phased kernels take the
+// loads-first form (ld_phased_issue / ld_phased_finish) under that cap and in the tile-run order caps::kRun
+// (DESIGN.md §12, §13); uncapped it loses (too many streams in flight).
 
 // The 16 body bytes of vector v (zero for v >= nvec) of an operand whose body starts at `body`,
 // phase p.  All 64 lanes must call it (p is uniform).
@@ -425,14 +432,15 @@ __global__ __launch_bounds__(64) void reduce_unaligned_kernel(const unsigned cha
             st_elem<T, false>(recv, j, Combine<T, OP>::apply(ld_elem<T, false>(recv, j), ld_elem<T, false>(send, j)));
 }
 
-template <typename T, int OP, int K, bool XCD, bool FIRST = false>
+template <typename T, int OP, int K, bool XCD, bool FIRST = false, int RUN = 1>
 __global__ __launch_bounds__(64) void reduce_multi_phased_kernel(SendList sends, PhaseList ph,
                                                                  unsigned char* __restrict__ recv, size_t head,
                                                                  size_t nvec, size_t tail) {
     const size_t off = head * sizeof(T);
     u32x4* vr = reinterpret_cast<u32x4*>(recv + off);
     const size_t ntiles = (nvec + 63) / 64;
-    for (size_t t = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (size_t t = XCD ? xcd_remap(blockIdx.x, gridDim.x) : run_tile<RUN>(blockIdx.x, gridDim.x); t < ntiles;
+         t += gridDim.x) {
         const size_t v = t * 64 + threadIdx.x;
         if constexpr (FIRST) {  // recv, then every source's loads, then the shifts and combines
             u32x4 acc = {0u, 0u, 0u, 0u};
@@ -467,14 +475,15 @@ __global__ __launch_bounds__(64) void reduce_multi_phased_kernel(SendList sends,
 }
 
 // Chain order as reduce_chain_vec_kernel; ph.p[K] is own's phase.
-template <typename T, int OP, int K, bool XCD, bool FIRST = false>
+template <typename T, int OP, int K, bool XCD, bool FIRST = false, int RUN = 1>
 __global__ __launch_bounds__(64) void reduce_chain_phased_kernel(SendList sends, PhaseList ph,
                                                                  const unsigned char* own, unsigned char* dst,
                                                                  size_t head, size_t nvec, size_t tail) {
     const size_t off = head * sizeof(T);
     u32x4* vd = reinterpret_cast<u32x4*>(dst + off);
     const size_t ntiles = (nvec + 63) / 64;
-    for (size_t t = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (size_t t = XCD ? xcd_remap(blockIdx.x, gridDim.x) : run_tile<RUN>(blockIdx.x, gridDim.x); t < ntiles;
+         t += gridDim.x) {
         const size_t v = t * 64 + threadIdx.x;
         if constexpr (FIRST) {  // every operand's loads, then the shifts and combines in chain order
             PhasedLoad x[K + 1];

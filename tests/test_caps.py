@@ -37,6 +37,9 @@ int main() {
                 std::printf("%s[%d, %d, %zu, %zu]", first ? "" : ", ", sh, sep, b, pair_lds(sh, sep, b));
                 first = false;
             }
+    std::printf("], \"runs\": [");
+    for (int c = 0; c < kNumKernels; ++c)
+        for (int k = 0; k <= 8; ++k) std::printf("%s%d", (c || k) ? ", " : "", tile_run(Kernel(c), k));
     std::printf("], \"loads_first\": [");
     for (int ch = 0; ch < 2; ++ch)
         for (int k = 1; k <= 8; ++k) std::printf("%s%d", (ch || k > 1) ? ", " : "", int(phased_loads_first(ch, k)));
@@ -52,13 +55,13 @@ FROZEN = {
     "chain": [[0, 32, 32, 32, 32, 24, 16, 16, 16], [0, 32, 32, 32, 16, 16, 16, 16, 16],
               [0, 32, 32, 24, 16, 13, 11, 10, 9], [0, 32, 24, 20, 16, 13, 11, 10, 9]],
     "multi_straddle": [[0, 0, 32, 24, 16, 16, 16, 16, 32], [0, 0, 24, 16, 13, 11, 16, 9, 32],
-                       [0, 0, 24, 16, 13, 11, 9, 9, 7], [0, 0, 18, 13, 13, 11, 9, 9, 7]],
+                       [0, 0, 24, 16, 13, 11, 9, 9, 9], [0, 0, 18, 13, 13, 11, 9, 9, 9]],
     "chain_straddle": [[0, 32, 32, 32, 24, 24, 16, 16, 16], [0, 32, 32, 32, 24, 16, 11, 10, 9],
                        [0, 32, 32, 24, 16, 13, 11, 10, 9], [0, 32, 24, 18, 13, 13, 11, 10, 9]],
-    "multi_phased_first": [[0, 0, 0, 0, 0, 16, 0, 24, 16], [0, 0, 0, 0, 0, 16, 0, 16, 24],
-                           [0, 0, 0, 0, 0, 13, 0, 12, 11], [0, 0, 0, 0, 0, 13, 0, 12, 11]],
-    "chain_phased_first": [[0, 0, 0, 0, 24, 24, 0, 24, 16], [0, 0, 0, 0, 16, 16, 0, 16, 24],
-                           [0, 0, 0, 0, 16, 13, 0, 11, 11], [0, 0, 0, 0, 13, 13, 0, 11, 11]],
+    "multi_phased_first": [[0, 0, 0, 0, 16, 16, 13, 24, 16], [0, 0, 0, 0, 16, 16, 13, 16, 24],
+                           [0, 0, 0, 0, 16, 13, 13, 13, 13], [0, 0, 0, 0, 16, 13, 13, 13, 13]],
+    "chain_phased_first": [[0, 0, 0, 16, 24, 24, 0, 24, 16], [0, 0, 0, 16, 16, 16, 0, 16, 24],
+                           [0, 0, 0, 16, 16, 13, 0, 13, 11], [0, 0, 0, 16, 13, 13, 0, 13, 11]],
 }
 K_RANGE = {"multi": (2, 8), "chain": (1, 8), "multi_straddle": (2, 8), "chain_straddle": (1, 8),
            "multi_phased_first": (2, 8), "chain_phased_first": (1, 8)}
@@ -110,8 +113,17 @@ def test_size_class_boundaries(table):
 
 def test_phased_form_is_fixed_per_k(table):
     lf = table["loads_first"]
-    assert lf[:8] == [0, 0, 0, 0, 1, 0, 1, 1]   # k-way: loads-first at k = 5, 7, 8
-    assert lf[8:] == [0, 0, 0, 1, 1, 0, 1, 1]   # chain: at k = 4, 5, 7, 8
+    assert lf[:8] == [0, 0, 0, 1, 1, 1, 1, 1]   # k-way: loads-first from k = 4
+    assert lf[8:] == [0, 0, 1, 1, 1, 0, 1, 1]   # chain: at k = 3, 4, 5, 7, 8
+
+
+def test_tile_runs(table):
+    runs = table["runs"]
+    want = {"multi_straddle": {8: 4}, "multi_phased_first": {4: 4, 6: 4, 7: 4, 8: 4},
+            "chain_phased_first": {3: 4, 7: 4, 8: 4}}
+    for c, name in enumerate(NAMES):
+        for k in range(9):
+            assert runs[9 * c + k] == want.get(name, {}).get(k, 1), (name, k)
 
 
 def test_separate_allocation_rule(table):

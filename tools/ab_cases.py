@@ -59,7 +59,7 @@ def case_table(ptrs):
         "pair_dst+2_src+3": (1, lambda lib, n, st: lib.dccl_local_reduce(ptrs[0] + 3, recv + 2, 7, n, 0, st)),
         "pair_src+4": (1, lambda lib, n, st: lib.dccl_local_reduce(ptrs[0] + 4, recv, 7, n, 0, st)),
     }
-    for k in (2, 4, 6, 8):
+    for k in (2, 3, 4, 5, 6, 7, 8):
         t[f"multi{k}"] = (k, multi(ptrs[:k], recv))
         t[f"multi{k}_dst+2"] = (k, multi(ptrs[:k], recv + 2))
         t[f"multi{k}_dst+2_src+4"] = (k, multi([p + 4 for p in ptrs[:k]], recv + 2))
@@ -67,6 +67,7 @@ def case_table(ptrs):
         t[f"multi{k}_strad"] = (k, multi([p + 16 * (2 * j + 1) for j, p in enumerate(ptrs[:k])], recv))
         t[f"chain{k}_dst+2"] = (k, chain(ptrs[:k], recv + 2, recv + 2))
         t[f"chain{k}_dst+2_src+4"] = (k, chain([p + 4 for p in ptrs[:k]], recv + 2, recv + 2))
+        t[f"chain{k}_src+4"] = (k, chain([p + 4 for p in ptrs[:k]], recv, recv))
         t[f"chain{k}_strad"] = (k, chain([p + 16 * (2 * j + 1) for j, p in enumerate(ptrs[:k])], recv, recv))
     return t
 

@@ -1,11 +1,10 @@
 #!/usr/bin/env python3
-"""Tuning only (round 3): line-straddling in-phase k-way sources with 1, 2 or 4 consecutive 16-B vectors per lane
-(tools/tune variants 8 / 17 / 18 of dccl_tune_multi_f32_sum: sources through the caches, a wave's tile 1, 2 or
-4 KiB), so the line two neighbouring tiles share (fetched twice when they run on different XCDs) is one per 2 or
-4 KiB instead of one per KiB.  1 GiB fp32 Sum per operand, ten operands in one allocation (4 KiB x (j+1)
-stagger), destination first, source j at + 16 (2j + 1) B; caps swept; the product's own launch beside them.
+"""Tuning only (round 3): the phased k-way combine (every source + 4 B, recv aligned) in tile-run orders (each XCD
+walks `run` consecutive tiles in every group of 8 * run blocks; run 1 = block order), per-operand and loads-first
+forms, caps swept, the product's own launch beside them.  1 GiB fp32 Sum per operand, ten operands in one
+allocation (4 KiB x (j+1) stagger), destination first.
 
-    python tools/straddle_unroll_probe.py [--ks 4,6,8] [--rounds 3] [--out f.json]
+    python tools/phased_run_probe.py [--ks 3,4,5,6,8] [--rounds 3] [--out f.json]
 """
 import argparse
 import ctypes
@@ -22,11 +21,6 @@ import dccl_amd  # noqa: E402
 from tools import tune_lib  # noqa: E402
 
 PEAK = 8e12
-# (tuning variant, label): shipped shape (1 vector per lane, block order), 2 / 4 vectors per lane, and the
-# shipped shape in runs of 2 / 4 / 8 / 16 consecutive tiles per XCD (variants 19 / 20 / 15 / 21)
-VARIANTS = [(8, "unroll1"), (17, "unroll2"), (18, "unroll4")]
-RUN_VARIANTS = [(8, "run1"), (19, "run2"), (20, "run4"), (15, "run8"), (21, "run16")]
-WAVES = (32, 24, 16, 13, 11, 9, 7, 5)
 
 
 def lds_for(w):
@@ -35,19 +29,11 @@ def lds_for(w):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--ks", default="4,6,8")
+    p.add_argument("--ks", default="3,4,5,6,8")
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--launches", type=int, default=6)
-    p.add_argument("--runs", action="store_true", help="sweep the tile-run orders instead of the unrolls")
-    p.add_argument("--confirm", action="store_true",
-                   help="second-box check of the round's leads: runs of 2 / 4 tiles at 9 / 11 waves, block order at 11")
     p.add_argument("--out", default="")
     a = p.parse_args()
-    global VARIANTS, WAVES
-    if a.runs:
-        VARIANTS, WAVES = RUN_VARIANTS, (32, 16, 13, 11, 9, 7)
-    if a.confirm:
-        VARIANTS, WAVES = [(8, "run1"), (19, "run2"), (20, "run4")], (13, 11, 9)
     st = torch.cuda.current_stream().cuda_stream
     nbytes = 1 << 30
     n = nbytes // 4 - 64
@@ -61,14 +47,15 @@ def main():
     T = tune_lib.lib
     configs = []
     for k in [int(x) for x in a.ks.split(",")]:
-        ss = [q + 16 * (2 * j + 1) for j, q in enumerate(srcs[:k])]
-        arr = (ctypes.c_void_p * k)(*ss)
+        arr = (ctypes.c_void_p * k)(*[q + 4 for q in srcs[:k]])
         configs.append(({"k": k, "form": "shipped"}, k,
                         lambda arr=arr, k=k: dccl_amd.lib.dccl_local_reduce_multi(arr, k, dst, 7, n, 0, st)))
-        for var, form in VARIANTS:
-            for w in WAVES:
-                configs.append(({"k": k, "form": form, "waves": w}, k,
-                                lambda arr=arr, k=k, v=var, l=lds_for(w): T.dccl_tune_multi_f32_sum(arr, k, dst, n, v, l, st)))
+        for first in (0, 1):
+            for run in (1, 2, 4, 8):
+                for w in ((32, 16, 13, 11) if first else (32, 24, 16)):
+                    configs.append(({"k": k, "form": "first" if first else "per_operand", "run": run, "waves": w}, k,
+                                    lambda arr=arr, k=k, f=first, r=run, l=lds_for(w):
+                                    T.dccl_tune_phased_run_f32_sum(arr, k, dst, n, l, f, r, st)))
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     times = [[] for _ in configs]
     for rnd in range(a.rounds):

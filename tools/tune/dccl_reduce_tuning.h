@@ -86,6 +86,12 @@ int dccl_tune_unaligned_kway_f32_sum(const void* const* sends, int nsend, const 
 int dccl_tune_unaligned_pair_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes, int order,
                                      void* stream);
 
+/* the phased k-way combine (sources at other 16-B phases) in the tile-run orders (run 1 = block order) */
+int dccl_tune_phased_run_f32_sum(const void* const* sends, int nsend, void* recv, size_t count, size_t lds_bytes,
+                                 int first, unsigned run, void* stream);
+/* the product's straddling / phased k-way (kind 0 / 2) and chain (1 / 3) kernels in tile-run orders 1, 2, 4 */
+int dccl_tune_runs_f32_sum(int kind, const void* const* sends, int nsend, const void* own, void* dst, size_t count,
+                           size_t lds_bytes, int run, int first, void* stream);
 /* the persistent work-queue combine (fp32 Sum, aligned): variant = tiles per grab (1-32) or 100 + grab for the
  * pipelined form; waves_per_cu one-wave blocks per CU; counter = two zeroed 64-bit words (reset by the kernel) */
 int dccl_tune_wq_f32_sum(const void* send, void* recv, size_t count, int variant, int waves_per_cu, void* counter,

@@ -295,12 +295,18 @@ int tune_multi_edge_cached(SendList sl, unsigned char* r, Split sp, hipStream_t 
 // front).  Tiles t and t+1 then share an L2 in 7 of 8 cases, so a line-straddling source's line that two
 // neighbouring tiles share is fetched from HBM once instead of twice (PMC: each straddling source reads
 // 1.125 x in block order).  P: cache policy bits (6: sources cached, 7: all non-temporal).
+// Round 3: `run` generalises the order: in every group of 8 * run blocks each XCD walks `run` consecutive tiles
+// (run 8 = xcd_group_tile, run 1 = block order); a partial last group keeps the identity.
+__device__ __forceinline__ size_t run_tile_rt(size_t b, size_t g, unsigned run) {
+    const size_t span = size_t(8) * run, q = b / span, r = b % span;
+    return (q + 1) * span > g ? b : q * span + (r % 8) * run + r / 8;
+}
 template <int K, int P>
 __global__ __launch_bounds__(64) void tune_multi_group_kernel(SendList sends, unsigned char* __restrict__ recv,
-                                                              size_t head, size_t nvec, size_t tail) {
+                                                              size_t head, size_t nvec, size_t tail, unsigned run) {
     u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(float));
     const size_t ntiles = (nvec + 63) / 64;
-    for (size_t t = xcd_group_tile(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    for (size_t t = run_tile_rt(blockIdx.x, gridDim.x, run); t < ntiles; t += gridDim.x) {
         const size_t i = t * 64 + threadIdx.x;
         if (i < nvec) {
             u32x4 s[K];
@@ -323,10 +329,10 @@ __global__ __launch_bounds__(64) void tune_multi_group_kernel(SendList sends, un
         }
 }
 template <int K, int P>
-int tune_multi_group(SendList sl, unsigned char* r, Split sp, hipStream_t st, size_t lds) {
+int tune_multi_group(SendList sl, unsigned char* r, Split sp, hipStream_t st, size_t lds, unsigned run = 8) {
     size_t grid = ceil_div(sp.nvec, size_t(64));
     if (grid == 0) grid = 1;
-    void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail};
+    void* args[] = {&sl, &r, &sp.head, &sp.nvec, &sp.tail, &run};
     return launch(reinterpret_cast<const void*>(&tune_multi_group_kernel<K, P>), grid, args, st, 64, lds);
 }
 
@@ -349,6 +355,9 @@ int tune_multi_k(int variant, SendList sl, unsigned char* r, Split sp, hipStream
     case 16: return tune_multi_group<K, kNtSend | kNtRecv | kNtStore>(sl, r, sp, st, lds);
     // round 3: the line-straddling rule (sources through the caches) with 2 / 4 consecutive vectors per lane,
     // so a wave's tile is 2 / 4 KiB and only one line per tile is shared with the neighbouring wave
+    case 19: return tune_multi_group<K, kNtRecv | kNtStore>(sl, r, sp, st, lds, 2);
+    case 20: return tune_multi_group<K, kNtRecv | kNtStore>(sl, r, sp, st, lds, 4);
+    case 21: return tune_multi_group<K, kNtRecv | kNtStore>(sl, r, sp, st, lds, 16);
     case 17: return tune_multi_launch<K, VecCfg<64, 2, 6, false, 1>>(sl, r, sp, st, lds);
     case 18: return tune_multi_launch<K, VecCfg<64, 4, 6, false, 1>>(sl, r, sp, st, lds);
     default: return DCCL_INVALID_ARGUMENT;
@@ -1519,4 +1528,136 @@ extern "C" int dccl_tune_wq_f32_sum(const void* send, void* recv, size_t count, 
     case 116: return tune_wq_launch<16, true>(vs, vr, ntiles, ctr, grid, st);
     default: return DCCL_INVALID_ARGUMENT;
     }
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning only (round 3): the phased k-way kernel (sources at other 16-B phases, element-aligned recv) in the
+// tile-run orders of run_tile (each XCD walks `run` consecutive tiles in every group of 8 * run blocks;
+// run 1 = block order, the shipped order from k = 5), per-operand (FIRST false) or loads-first form.
+// ---------------------------------------------------------------------------------
+namespace {
+template <int K, bool FIRST>
+__global__ __launch_bounds__(64) void tune_phased_run_kernel(SendList sends, PhaseList ph, unsigned char* __restrict__ recv,
+                                                             size_t head, size_t nvec, size_t tail, unsigned run) {
+    const size_t off = head * sizeof(float);
+    u32x4* vr = reinterpret_cast<u32x4*>(recv + off);
+    const size_t ntiles = (nvec + 63) / 64;
+    for (size_t t = run_tile_rt(blockIdx.x, gridDim.x, run); t < ntiles; t += gridDim.x) {
+        const size_t v = t * 64 + threadIdx.x;
+        u32x4 acc = {0u, 0u, 0u, 0u};
+        if constexpr (FIRST) {
+            if (v < nvec) acc = ld16<true>(vr + v);
+            PhasedLoad x[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[k] = ld_phased_issue(sends.p[k] + off, ph.p[k], v, nvec);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = combine16<float, kSum>(acc, ld_phased_finish(x[k], ph.p[k]));
+        } else {
+            u32x4 s[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k] + off, ph.p[k], v, nvec);
+            if (v < nvec) acc = ld16<true>(vr + v);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = combine16<float, kSum>(acc, s[k]);
+        }
+        if (v < nvec) __builtin_nontemporal_store(acc, vr + v);
+    }
+    if (blockIdx.x == 0)
+        for (size_t j = threadIdx.x; j < head + tail; j += 64) {
+            const size_t i = j < head ? j : head + nvec * 4 + (j - head);
+            float acc = ld_elem<float, true>(recv, i);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = Combine<float, kSum>::apply(acc, ld_elem<float, false>(sends.p[k], i));
+            st_elem<float, true>(recv, i, acc);
+        }
+}
+template <int K>
+int tune_phased_run_k(SendList sl, PhaseList ph, unsigned char* r, Split sp, hipStream_t st, size_t lds, bool first,
+                      unsigned run) {
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0) grid = 1;
+    void* args[] = {&sl, &ph, &r, &sp.head, &sp.nvec, &sp.tail, &run};
+    const void* fn = first ? reinterpret_cast<const void*>(&tune_phased_run_kernel<K, true>)
+                           : reinterpret_cast<const void*>(&tune_phased_run_kernel<K, false>);
+    return launch(fn, grid, args, st, 64, lds);
+}
+}  // namespace
+
+extern "C" int dccl_tune_phased_run_f32_sum(const void* const* sends, int nsend, void* recv, size_t count,
+                                            size_t lds_bytes, int first, unsigned run, void* stream) {
+    if (sends == nullptr || recv == nullptr || nsend < 2 || nsend > 8 || lds_bytes > (64u << 10) || run < 1 ||
+        (reinterpret_cast<uintptr_t>(recv) & 3))
+        return DCCL_INVALID_ARGUMENT;
+    const Split sp = split_for_vectors<float>(reinterpret_cast<uintptr_t>(recv), count, 128);
+    SendList sl{};
+    PhaseList ph{};
+    for (int k = 0; k < nsend; ++k) {
+        sl.p[k] = static_cast<const unsigned char*>(sends[k]);
+        ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(float));
+    }
+    auto r = static_cast<unsigned char*>(recv);
+    const auto st = static_cast<hipStream_t>(stream);
+    return with_k<2, 8>(nsend, [&](auto K) {
+        return tune_phased_run_k<K.value>(sl, ph, r, sp, st, lds_bytes, first != 0, run);
+    });
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning only (round 3): the product's straddling and phased k-way / chain kernels in the tile-run orders
+// (reduce_kernels.hpp run_tile<RUN>, VecCfg::RUN): kind 0 k-way straddling (sources cached), 1 chain
+// straddling, 2 k-way phased, 3 chain phased (own = nullptr for the k-way kinds); run 1, 2 or 4; first: the
+// phased kernels' loads-first form.  recv / dst element-aligned, sources in its 16-B phase (kinds 0, 1) or
+// at any phase (2, 3).
+// ---------------------------------------------------------------------------------
+namespace {
+template <int K, int RUN>
+int tune_runs_k(int kind, bool first, SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, Split sp,
+                hipStream_t st, size_t lds) {
+    size_t grid = ceil_div(sp.nvec, size_t(64));
+    if (grid == 0) grid = 1;
+    using C = VecCfg<64, 1, kNtRecv | kNtStore, false, 1, RUN>;
+    void* a_multi[] = {&sl, &d, &sp.head, &sp.nvec, &sp.tail};
+    void* a_chain[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
+    void* a_pm[] = {&sl, &ph, &d, &sp.head, &sp.nvec, &sp.tail};
+    void* a_pc[] = {&sl, &ph, &own, &d, &sp.head, &sp.nvec, &sp.tail};
+    switch (kind) {
+    case 0: return launch(reinterpret_cast<const void*>(&reduce_multi_vec_kernel<float, kSum, K, C>), grid, a_multi, st, 64, lds);
+    case 1: return launch(reinterpret_cast<const void*>(&reduce_chain_vec_kernel<float, kSum, K, C>), grid, a_chain, st, 64, lds);
+    case 2:
+        return launch(first ? reinterpret_cast<const void*>(&reduce_multi_phased_kernel<float, kSum, K, false, true, RUN>)
+                            : reinterpret_cast<const void*>(&reduce_multi_phased_kernel<float, kSum, K, false, false, RUN>),
+                      grid, a_pm, st, 64, lds);
+    default:
+        return launch(first ? reinterpret_cast<const void*>(&reduce_chain_phased_kernel<float, kSum, K, false, true, RUN>)
+                            : reinterpret_cast<const void*>(&reduce_chain_phased_kernel<float, kSum, K, false, false, RUN>),
+                      grid, a_pc, st, 64, lds);
+    }
+}
+}  // namespace
+
+extern "C" int dccl_tune_runs_f32_sum(int kind, const void* const* sends, int nsend, const void* own, void* dst,
+                                      size_t count, size_t lds_bytes, int run, int first, void* stream) {
+    if (kind < 0 || kind > 3 || sends == nullptr || dst == nullptr || nsend < 1 || nsend > 8 ||
+        lds_bytes > (64u << 10) || (reinterpret_cast<uintptr_t>(dst) & 3) || ((kind & 1) != 0) != (own != nullptr))
+        return DCCL_INVALID_ARGUMENT;
+    if ((kind & 1) == 0 && nsend < 2) return DCCL_INVALID_ARGUMENT;
+    const Split sp = split_for_vectors<float>(reinterpret_cast<uintptr_t>(dst), count, 128);
+    SendList sl{};
+    PhaseList ph{};
+    for (int k = 0; k < nsend; ++k) {
+        sl.p[k] = static_cast<const unsigned char*>(sends[k]);
+        ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(float));
+    }
+    const auto o = static_cast<const unsigned char*>(own);
+    if (o != nullptr) ph.p[nsend] = phase_word(o, sp.head * sizeof(float));
+    auto d = static_cast<unsigned char*>(dst);
+    const auto st = static_cast<hipStream_t>(stream);
+    return with_k<1, 8>(nsend, [&](auto K) {
+        switch (run) {
+        case 1: return tune_runs_k<K.value, 1>(kind, first != 0, sl, ph, o, d, sp, st, lds_bytes);
+        case 2: return tune_runs_k<K.value, 2>(kind, first != 0, sl, ph, o, d, sp, st, lds_bytes);
+        case 4: return tune_runs_k<K.value, 4>(kind, first != 0, sl, ph, o, d, sp, st, lds_bytes);
+        default: return int(DCCL_INVALID_ARGUMENT);
+        }
+    });
 }

@@ -41,6 +41,10 @@ def _load():
         "dccl_tune_group_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]),
         "dccl_tune_unaligned_kway_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_void_p, c_size_t,
                                                      c_size_t, c_int, c_void_p]),
+        "dccl_tune_phased_run_f32_sum": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p, c_size_t, c_size_t, c_int,
+                                                 ctypes.c_uint, c_void_p]),
+        "dccl_tune_runs_f32_sum": (c_int, [c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_void_p, c_size_t,
+                                           c_size_t, c_int, c_int, c_void_p]),
         "dccl_tune_wq_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
         "dccl_tune_unaligned_pair_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_int, c_void_p]),
         "dccl_tune_misaligned_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
