@@ -44,6 +44,11 @@ using StraddleCfg = VecCfg<64, 1, kNtRecv | kNtStore, false>;
 // vector is always loaded through the caches.
 constexpr int ShiftPolicy = kNtSend | kNtRecv | kNtStore;
 constexpr int ShiftStraddlePolicy = kNtRecv | kNtStore;
+// ... in the group-interleaved tile order (run_tile<8>): the vector lane 63 reads past its tile and the next
+// tile's first line then meet in one L2 in 7 of 8 cases while the chip sweeps one front.  1 GiB fp32 Sum,
+// pooled layout, two boxes (tools/pair_runs_probe.py, profiles/r3_s16_*, r3_s17_*): send + 4 B 83.8 -> 85.2-85.4 %,
+// send + 1 B 83.7-83.9 -> 85.3-85.4 %, send + 20 B (cached send loads) 84.1 -> 84.7 %: the aligned kernel's rate.
+constexpr int kShiftRun = 8;
 // recv is aligned to this many bytes by the head scalars (DCCL_REDUCE_ALIGN, a power of two from 16 to
 // 4096; default 128, one line): a recv that straddles lines costs 10-15 % (profiles/r1_s3_phase_probe.json).
 size_t recv_align() {
@@ -119,15 +124,17 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
         const Split sp = split_for_vectors<T>(ar, count, align);
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);
         const size_t lds = pair_occupancy_lds(send, recv, bytes, true);
-        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, false>(s, r, count, stream, align, lds)
-                         : launch_shift<T, OP, ShiftPolicy, false, 0, false>(s, r, count, stream, align, lds);
+        return (a & 127)
+                   ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, false, kShiftRun>(s, r, count, stream, align, lds)
+                   : launch_shift<T, OP, ShiftPolicy, false, 0, false, kShiftRun>(s, r, count, stream, align, lds);
     }
     const Split sp = split_for_vectors<T>(ar, count, align);
     if ((as ^ ar) & 15) {
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);  // the shifted kernel's send vectors
         const size_t lds = pair_occupancy_lds(send, recv, bytes, true);
-        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false>(s, r, count, stream, align, lds)
-                         : launch_shift<T, OP, ShiftPolicy, false>(s, r, count, stream, align, lds);
+        return (a & 127)
+                   ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, true, kShiftRun>(s, r, count, stream, align, lds)
+                   : launch_shift<T, OP, ShiftPolicy, false, 0, true, kShiftRun>(s, r, count, stream, align, lds);
     }
     if ((as ^ ar) & 127) {
         const size_t forced = forced_occupancy_lds();

@@ -45,15 +45,10 @@ __device__ __forceinline__ void st_elem(unsigned char* base, size_t i, T v) {
     __builtin_memcpy(base + i * sizeof(T), &v, sizeof(T));
 }
 
-// ---------------------------------------------------------------------------------
-// Vector kernel.  Operands are split as [head scalars | nvec 16-B vectors | tail
-// scalars]; head aligns recv to its 128-B lines (split_for_vectors) and send, which has recv's
-// 16-B phase, to 16 B.
-// ---------------------------------------------------------------------------------
-// Kernel shape: BLOCK threads, UNROLL 16-B vectors per thread per operand, cache POLICY
-// bits, XCD: remap block ids so that each XCD's blocks walk one contiguous range.
-// TAG keeps instantiations of different translation units distinct (production: 0, tuning: 1),
-// so no kernel symbol is registered from two code objects.
+// Vector kernel: [head scalars | nvec 16-B vectors | tail scalars], the head aligning recv to its 128-B lines.
+// Shape: BLOCK threads, UNROLL 16-B vectors per thread per operand, cache POLICY bits, XCD (each XCD's blocks walk
+// one contiguous range) or the tile-run order RUN; TAG keeps the production (0) and tuning (1) translation units'
+// instantiations distinct.
 template <int BLOCK_, int UNROLL_, int POLICY_, bool XCD_, int TAG = 0, int RUN_ = 1>
 struct VecCfg {
     static constexpr int BLOCK = BLOCK_, UNROLL = UNROLL_, POLICY = POLICY_, RUN = RUN_;  // RUN: run_tile below
@@ -123,9 +118,13 @@ __device__ __forceinline__ size_t xcd_group_tile(size_t b, size_t nb) { return r
 // uniform runtime `order`: kOrderXcd gives each XCD one contiguous range (consecutive tiles on one XCD: the
 // line two tiles share meets in one L2), kOrderBlock is block order, kOrderGroup the group-interleaved order
 // above (one front for the chip, 7 of 8 tile boundaries inside one XCD).  Computed once per block.
-enum : int { kOrderXcd = 0, kOrderBlock = 1, kOrderGroup = 2 };
+enum : int { kOrderXcd = 0, kOrderBlock = 1, kOrderGroup = 2, kOrderRun4 = 3, kOrderRun2 = 4 };
 __device__ __forceinline__ size_t tile_order(int order, size_t b, size_t g) {
-    return order == kOrderXcd ? (b % 8) * (g / 8) + b / 8 : order == kOrderBlock ? b : xcd_group_tile(b, g);
+    return order == kOrderXcd     ? (b % 8) * (g / 8) + b / 8
+           : order == kOrderBlock ? b
+           : order == kOrderRun4  ? run_tile<4>(b, g)
+           : order == kOrderRun2  ? run_tile<2>(b, g)
+                                  : xcd_group_tile(b, g);
 }
 
 template <typename T, int OP, typename C>
@@ -135,7 +134,7 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_vec_kernel(const unsigned cha
     const u32x4* __restrict__ vs = reinterpret_cast<const u32x4*>(send + head * sizeof(T));
     u32x4* __restrict__ vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
     const size_t nfull = nvec / C::TILE;
-    const size_t bid = C::XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const size_t bid = C::XCD ? xcd_remap(blockIdx.x, gridDim.x) : run_tile<C::RUN>(blockIdx.x, gridDim.x);
 
     // Full tiles: no bounds checks, all 2*UNROLL loads in flight before the first use.
     for (size_t t = bid; t < nfull; t += gridDim.x)
@@ -149,20 +148,13 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_vec_kernel(const unsigned cha
     if (blockIdx.x == 0) edge_scalars<T, OP>(send, recv, head, nvec, tail);
 }
 
-// ---------------------------------------------------------------------------------
-// Shifted vector kernel: element-aligned operands whose 16-B phases differ.  DCCL combines chunk
-// k of a user buffer (offset k*count/W*sizeof(T)) with an aligned scratchpad, so any chunk size
-// that is not a multiple of 16 B lands here.  recv is walked in aligned 16-B vectors from
-// recv + head; the matching send bytes start p bytes (0 < p < 16, a multiple of sizeof(T)) past
-// the 16-B boundary A.  Every lane loads the ALIGNED send vector A[v], takes A[v+1] from its
-// right-hand neighbour (DPP wave shift; lane 63 loads it itself, issued with the other loads), and
-// funnel-shifts the 32 bytes by p (v_alignbyte_b32), so every access stays a 16-B vector.
-// A[nvec] is loaded although only its first p bytes belong to send: an aligned 16-B load never
-// leaves the page of its first byte, which is send's.
-// v_alignbyte shifts by any byte count, so p need not be a multiple of sizeof(T): a send that is not
-// even element-aligned, against an element-aligned recv, takes this kernel too (SEND_ALIGNED false: its
-// head / tail elements are read bytewise).
-// ---------------------------------------------------------------------------------
+// Shifted vector kernel: element-aligned operands whose 16-B phases differ (any DCCL chunk size that is not
+// a multiple of 16 B).  recv is walked in aligned 16-B vectors; send's bytes start p bytes (0 < p < 16) past a
+// 16-B boundary A.  Every lane loads the ALIGNED vector A[v], takes A[v+1] from its right-hand neighbour (DPP
+// wave shift; lane 63 loads it itself) and funnel-shifts the 32 bytes by p (v_alignbyte_b32), so every access
+// stays a 16-B vector.  A[nvec] is read although only its first p bytes are send's: an aligned 16-B load never
+// leaves the page of its first byte.  p may be any byte count: a send that is not element-aligned takes this
+// kernel too (SEND_ALIGNED false: its head / tail elements are read bytewise).
 constexpr int kNtExtra = 8;  // policy bit: non-temporal load of lane 63's extra vector
 
 template <int Q>
@@ -193,7 +185,7 @@ __device__ __forceinline__ u32x4 dpp16(u32x4 x, u32x4 old) {
 // tools/tune/misaligned_2pass.hpp)
 __device__ __forceinline__ u32x4 from_next_lane_or(u32x4 x, u32x4 last) { return dpp16<0x130>(x, last); }
 
-template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true>
+template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true, int RUN = 1>
 __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* __restrict__ send,
                                                           unsigned char* __restrict__ recv, size_t head,
                                                           size_t nvec, size_t tail, unsigned p) {
@@ -201,7 +193,7 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
     const u32x4* va = reinterpret_cast<const u32x4*>(sa - p);  // A: 16-B aligned
     u32x4* vr = reinterpret_cast<u32x4*>(recv + head * sizeof(T));
     const size_t ntiles = (nvec + 63) / 64;
-    const size_t bid = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    const size_t bid = XCD ? xcd_remap(blockIdx.x, gridDim.x) : run_tile<RUN>(blockIdx.x, gridDim.x);
     const unsigned q = p >> 2, b = p & 3;
     const bool last_lane = threadIdx.x == 63;
     for (size_t t = bid; t < ntiles; t += gridDim.x) {  // uniform per wave: every lane reaches the lane exchange
@@ -661,7 +653,7 @@ int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t s
 
 // Element-aligned operands with different 16-B phases (or an element-aligned recv and a send at any byte
 // address, SEND_ALIGNED false): the shifted vector kernel.
-template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true>
+template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true, int RUN = 1>
 int launch_shift(const unsigned char* s, unsigned char* r, size_t count, hipStream_t stream, size_t align = 16,
                  size_t lds_bytes = 0) {
     Split sp = split_for_vectors<T>(reinterpret_cast<uintptr_t>(r), count, align);
@@ -669,7 +661,7 @@ int launch_shift(const unsigned char* s, unsigned char* r, size_t count, hipStre
     size_t grid = ceil_div(sp.nvec, size_t(64));
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
     void* args[] = {&s, &r, &sp.head, &sp.nvec, &sp.tail, &p};
-    return launch(reinterpret_cast<const void*>(&reduce_shift_kernel<T, OP, POLICY, XCD, TAG, SEND_ALIGNED>), grid,
+    return launch(reinterpret_cast<const void*>(&reduce_shift_kernel<T, OP, POLICY, XCD, TAG, SEND_ALIGNED, RUN>), grid,
                   args, stream, 64, lds_bytes);
 }
 

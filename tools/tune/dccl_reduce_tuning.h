@@ -92,6 +92,8 @@ int dccl_tune_phased_run_f32_sum(const void* const* sends, int nsend, void* recv
 /* the product's straddling / phased k-way (kind 0 / 2) and chain (1 / 3) kernels in tile-run orders 1, 2, 4 */
 int dccl_tune_runs_f32_sum(int kind, const void* const* sends, int nsend, const void* own, void* dst, size_t count,
                            size_t lds_bytes, int run, int first, void* stream);
+/* the pairwise launches (aligned, send off its lines, send at another 16-B phase or byte offset) in tile runs */
+int dccl_tune_pair_run_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes, int run, void* stream);
 /* the persistent work-queue combine (fp32 Sum, aligned): variant = tiles per grab (1-32) or 100 + grab for the
  * pipelined form; waves_per_cu one-wave blocks per CU; counter = two zeroed 64-bit words (reset by the kernel) */
 int dccl_tune_wq_f32_sum(const void* send, void* recv, size_t count, int variant, int waves_per_cu, void* counter,

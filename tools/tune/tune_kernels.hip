@@ -1432,7 +1432,7 @@ extern "C" int dccl_tune_unaligned_pair_f32_sum(const void* send, void* recv, si
     unsigned p = unsigned(reinterpret_cast<uintptr_t>(send) & 15);
     size_t grid = ceil_div(ceil_div(nvec, size_t(64)), size_t(8)) * 8;
     if (grid == 0) grid = 8;
-    if (order < 0 || order > 2) return DCCL_INVALID_ARGUMENT;
+    if (order < 0 || order > 4) return DCCL_INVALID_ARGUMENT;
     void* args[] = {&s, &p, &r, &nvec, &count, &order};
     return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<float, kSum>), grid, args,
                   static_cast<hipStream_t>(stream), 64, lds_bytes);
@@ -1660,4 +1660,42 @@ extern "C" int dccl_tune_runs_f32_sum(int kind, const void* const* sends, int ns
         default: return int(DCCL_INVALID_ARGUMENT);
         }
     });
+}
+
+// ---------------------------------------------------------------------------------
+// Tuning only (round 3): the pairwise launches in tile-run orders: the shipped dispatch for an element-aligned
+// recv and a send at another 16-B phase or byte offset (reduce_shift_kernel, nt or cached send by its line) or
+// in phase but off recv's lines (reduce_vec_kernel, StraddleCfg), or aligned (DefaultCfg), with RUN 1, 2, 4, 8.
+// ---------------------------------------------------------------------------------
+namespace {
+template <int RUN>
+int tune_pair_run(const unsigned char* s, unsigned char* r, size_t count, hipStream_t st, size_t lds) {
+    const uintptr_t as = reinterpret_cast<uintptr_t>(s), ar = reinterpret_cast<uintptr_t>(r);
+    const Split sp = split_for_vectors<float>(ar, count, 128);
+    const uintptr_t a = (as + sp.head * sizeof(float)) & ~uintptr_t(15);
+    constexpr int kP = kNtSend | kNtRecv | kNtStore, kPs = kNtRecv | kNtStore;
+    if (as & 3)
+        return (a & 127) ? launch_shift<float, kSum, kPs, false, 1, false, RUN>(s, r, count, st, 128, lds)
+                         : launch_shift<float, kSum, kP, false, 1, false, RUN>(s, r, count, st, 128, lds);
+    if ((as ^ ar) & 15)
+        return (a & 127) ? launch_shift<float, kSum, kPs, false, 1, true, RUN>(s, r, count, st, 128, lds)
+                         : launch_shift<float, kSum, kP, false, 1, true, RUN>(s, r, count, st, 128, lds);
+    if ((as ^ ar) & 127) return launch_vec<float, kSum, VecCfg<64, 1, kPs, false, 1, RUN>>(s, r, sp, st, 0, lds);
+    return launch_vec<float, kSum, VecCfg<64, 1, kP, false, 1, RUN>>(s, r, sp, st, 0, lds);
+}
+}  // namespace
+
+extern "C" int dccl_tune_pair_run_f32_sum(const void* send, void* recv, size_t count, size_t lds_bytes, int run,
+                                          void* stream) {
+    if ((reinterpret_cast<uintptr_t>(recv) & 3) || lds_bytes > (64u << 10)) return DCCL_INVALID_ARGUMENT;
+    const auto s = static_cast<const unsigned char*>(send);
+    const auto r = static_cast<unsigned char*>(recv);
+    const auto st = static_cast<hipStream_t>(stream);
+    switch (run) {
+    case 1: return tune_pair_run<1>(s, r, count, st, lds_bytes);
+    case 2: return tune_pair_run<2>(s, r, count, st, lds_bytes);
+    case 4: return tune_pair_run<4>(s, r, count, st, lds_bytes);
+    case 8: return tune_pair_run<8>(s, r, count, st, lds_bytes);
+    default: return DCCL_INVALID_ARGUMENT;
+    }
 }

@@ -45,6 +45,7 @@ def _load():
                                                  ctypes.c_uint, c_void_p]),
         "dccl_tune_runs_f32_sum": (c_int, [c_int, ctypes.POINTER(c_void_p), c_int, c_void_p, c_void_p, c_size_t,
                                            c_size_t, c_int, c_int, c_void_p]),
+        "dccl_tune_pair_run_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_int, c_void_p]),
         "dccl_tune_wq_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, c_void_p]),
         "dccl_tune_unaligned_pair_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_int, c_void_p]),
         "dccl_tune_misaligned_f32_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
