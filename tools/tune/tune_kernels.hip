@@ -1393,14 +1393,14 @@ int tune_unaligned_kway_k(SendList sl, PhaseList ph, const unsigned char* own, u
 template <int K>
 int tune_unaligned_kway_form(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, size_t count,
                              hipStream_t st, size_t lds, int form) {
-    if ((form >> 1) > 2) return DCCL_INVALID_ARGUMENT;
+    if ((form >> 1) > 4) return DCCL_INVALID_ARGUMENT;
     return (form & 1) ? tune_unaligned_kway_k<K, true>(sl, ph, own, d, count, st, lds, form >> 1)
                       : tune_unaligned_kway_k<K, false>(sl, ph, own, d, count, st, lds, form >> 1);
 }
 }  // namespace
 
 // form: bit 0 = the loads-first form (reduce_kernels.hpp FIRST), form >> 1 = the tile ORDER (0 XCD-contiguous,
-// 1 block order, 2 group-interleaved).
+// 1 block order, 2 group-interleaved, 3 runs of 4, 4 runs of 2).
 extern "C" int dccl_tune_unaligned_kway_f32_sum(const void* const* sends, int nsend, const void* own, void* dst,
                                                 size_t count, size_t lds_bytes, int form, void* stream) {
     if (sends == nullptr || dst == nullptr || nsend < 1 || nsend > 8 || lds_bytes > (64u << 10))

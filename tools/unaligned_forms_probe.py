@@ -41,6 +41,9 @@ def main():
     p.add_argument("--launches", type=int, default=8)
     p.add_argument("--ks", default="2,4,8")
     p.add_argument("--kinds", default="pair,multi,chain")
+    p.add_argument("--orders", default="0,1,2", help="tile orders: 0 XCD ranges, 1 block, 2 group (run 8), 3 run 4, 4 run 2")
+    p.add_argument("--waves", default="32,24,16")
+    p.add_argument("--src-offs", default="0,4")
     p.add_argument("--out", default="")
     a = p.parse_args()
     st = torch.cuda.current_stream().cuda_stream
@@ -62,7 +65,7 @@ def main():
             base = {"kind": "pair", "k": 1, "dst_off": doff, "src_off": soff}
             configs.append(({**base, "form": "shipped"}, 1,
                             lambda s_=s_, d_=d_: dccl_amd.local_reduce(s_, d_, 7, n, 0, st)))
-            for order in (0, 1, 2):
+            for order in [int(x) for x in a.orders.split(",")]:
                 for w in (32, 26, 24, 20):
                     configs.append(({**base, "form": "phased", "order": order, "waves": w}, 1,
                                     lambda s_=s_, d_=d_, l=lds_for(w), o=order:
@@ -71,7 +74,7 @@ def main():
         if kind not in kinds:
             continue
         for k in [int(x) for x in a.ks.split(",")]:
-            for soff in (0, 4):
+            for soff in [int(x) for x in a.src_offs.split(",")]:
                 ss = [q + soff for q in srcs[:k]]
                 arr = (ctypes.c_void_p * k)(*ss)
                 d_ = dst + 2
@@ -83,8 +86,8 @@ def main():
                 configs.append(({**base, "form": "shipped"}, k, ship))
                 own = None if kind == "multi" else d_
                 for first in (0, 1):
-                    for order in (0, 1, 2):
-                        for w in (32, 24, 16):
+                    for order in [int(x) for x in a.orders.split(",")]:
+                        for w in [int(x) for x in a.waves.split(",")]:
                             configs.append(({**base, "form": "first" if first else "per_operand", "order": order,
                                              "waves": w}, k,
                                             lambda arr=arr, k=k, d_=d_, own=own, l=lds_for(w), f=first + 2 * order:
