@@ -860,9 +860,14 @@ def launch_ranks(a, argv) -> int:
     n = a.gpus
     backend = os.environ.get("DCCL_BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
-    if backend == "nccl" and ndev < n:
-        print(f"bench.py: --gpus {n} needs {n} GPUs, {ndev} visible (DCCL_BENCH_BACKEND=gloo rehearses N ranks "
-              f"on fewer GPUs)", file=sys.stderr)
+    # DCCL_BENCH_RCCL_REHEARSAL=1: N RCCL ranks on fewer GPUs.  RCCL refuses two ranks on one device of one
+    # host, so each rank gets its own NCCL_HOSTID: RCCL then sees N hosts and joins them over its socket
+    # transport on loopback (every RCCL call of the bench, the namespace-dccl ring over RCCL included, runs
+    # for real; the rates are not xGMI rates)
+    rehearse_rccl = backend == "nccl" and os.environ.get("DCCL_BENCH_RCCL_REHEARSAL") == "1"
+    if backend == "nccl" and ndev < n and not rehearse_rccl:
+        print(f"bench.py: --gpus {n} needs {n} GPUs, {ndev} visible (DCCL_BENCH_BACKEND=gloo or "
+              f"DCCL_BENCH_RCCL_REHEARSAL=1 rehearse N ranks on fewer GPUs)", file=sys.stderr)
         return 2
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -876,6 +881,9 @@ def launch_ranks(a, argv) -> int:
             env = {**os.environ, "RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
                    "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
                    "MASTER_PORT": str(port)}
+            if rehearse_rccl:
+                env.update({"NCCL_HOSTID": f"dccl-rehearsal-{port}-{r}", "NCCL_SOCKET_IFNAME": "lo",
+                            "NCCL_IB_DISABLE": "1"})
             procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
                                           stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
         reader = threading.Thread(target=lambda: out.setdefault("stdout", procs[0].stdout.read()), daemon=True)
@@ -1101,6 +1109,9 @@ def run_rank(a):
                        "op": a.op, "parallelism": f"shard x{world}"},
             "payload_gib_s": round(total_bytes / (ms_per_step * 1e-3) / GIB, 2),
         }
+        if world > torch.cuda.device_count():
+            res["rehearsal"] = (f"{world} ranks on {torch.cuda.device_count()} GPU(s), torch.distributed backend "
+                                f"{backend}: a functional rehearsal, the rates are not scaling numbers")
         if world == 1 and not a.no_configs:
             progress("C4: size sweep 4 KiB - 4 GiB")
             res["c4"] = config_c4(dev, stream)
@@ -1143,10 +1154,14 @@ def launcher_selftest() -> None:
     if world > 1:
         dist.init_process_group("gloo")
     t = torch.tensor([rank], dtype=torch.int64)
+    hostids = [os.environ.get("NCCL_HOSTID")]
     if world > 1:
         dist.all_reduce(t)
+        hostids = [None] * world
+        dist.all_gather_object(hostids, os.environ.get("NCCL_HOSTID"))
     if rank == 0:
         print(json.dumps({"n_gpus": world, "rank_sum": int(t[0]), "local_rank": os.environ.get("LOCAL_RANK"),
+                          "nccl_hostids": hostids,
                           "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
     if world > 1:
         dist.barrier()

@@ -100,6 +100,41 @@ def test_bench_self_launch_two_ranks_one_gpu():
     assert list(res)[-1] == "verified"
 
 
+def test_bench_rccl_two_ranks_one_gpu():
+    """The driver's default N>1 path (torch.distributed on RCCL, the RCCL all-gather of the shards and of C5, the
+    namespace-dccl all_reduce / all_gather / broadcast / reduce over the RCCL p2p ring, RCCL's own all_reduce as
+    the check) rehearsed with plain `python3 bench.py --gpus 2` on the box's one GPU: each rank gets its own
+    NCCL_HOSTID, so RCCL joins the two ranks over its socket transport on loopback instead of refusing a second
+    rank on one device.  rccl_exchange (dccl_amd/csrc/rccl_transport.cpp) runs with two real RCCL ranks."""
+    import json
+    import subprocess
+    import sys
+    import dccl_amd
+    if not dccl_amd.lib.dccl_rccl_available():
+        pytest.skip("librccl not loadable")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update({"DCCL_BENCH_BACKEND": "nccl", "DCCL_BENCH_RCCL_REHEARSAL": "1",
+                "DCCL_BOOTSTRAP_TAG": f"bench_rccl_rehearsal_{_port()}"})
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--mib", "64",
+           "--c5-gib", "0.25", "--no-cpu", "--other-pairs", "2", "--rank-timeout", "240"]
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, p.stdout[-3000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["verified"] is True and "rehearsal" in res, res
+    assert res["allgather"]["ms"] > 0 and res["c5"]["verified"] and res["c5"]["allgather"]["ms"] > 0, res
+    s = res["dccl_allreduce_summary"]
+    assert "error" not in s, s
+    for name in ("ring", "direct"):
+        assert s[name]["int32_sum_bit_exact_vs_rccl"] and s[name]["fp32_within_bound"], s
+        assert s[name]["broadcast_bit_exact"] and s[name]["reduce_bit_exact"], s
+        assert s["dccl_allgather"][name]["bit_exact"], s
+    assert s["fp32_direct_bit_exact_vs_ring"] and s["rccl"]["ms"] > 0, s
+    assert s["c5_allgather"]["direct"]["bit_exact"], s
+
+
 def test_bench_single_gpu_line():
     """bench.py at N=1 prints exactly one JSON line with the contract's keys, the C5 extra and the C3 / C4
     legs (every C3 entry sample-verified)."""

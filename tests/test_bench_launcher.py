@@ -43,6 +43,19 @@ def test_self_launch_starts_n_ranks():
         assert res["local_rank"] == "0" and res["master"].startswith("127.0.0.1:"), res
 
 
+def test_rccl_rehearsal_gives_each_rank_a_host_id():
+    """DCCL_BENCH_RCCL_REHEARSAL=1: N RCCL ranks on fewer GPUs, each rank with its own NCCL_HOSTID (RCCL joins them
+    over loopback sockets instead of refusing two ranks on one device); without it, an RCCL run on too few GPUs is
+    refused (test_self_launch_needs_the_gpus)."""
+    p = _run(["--gpus", "3", "--launcher-selftest"], {"DCCL_BENCH_BACKEND": "nccl", "DCCL_BENCH_RCCL_REHEARSAL": "1"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    ids = res["nccl_hostids"]
+    assert res["n_gpus"] == 3 and len(set(ids)) == 3 and all(i.startswith("dccl-rehearsal-") for i in ids), res
+    p = _run(["--gpus", "2", "--launcher-selftest"], {"DCCL_BENCH_BACKEND": "gloo"})
+    assert json.loads(p.stdout.strip().splitlines()[-1])["nccl_hostids"] == [None, None]
+
+
 def test_self_launch_fails_when_a_rank_fails():
     p = _run(["--gpus", "2", "--launcher-selftest"], {"DCCL_BENCH_BACKEND": "gloo",
                                                        "DCCL_BENCH_SELFTEST_FAIL_RANK": "1"})
