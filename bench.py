@@ -684,7 +684,13 @@ def allgather_compare(comms: dict, world: int, rank: int, dev, st, count: int, i
         torch.cuda.synchronize(dev)
         dccl_amd.check(comm.all_gather(mine.data_ptr(), y.data_ptr(), per, 2, st.cuda_stream), name)
         torch.cuda.synchronize(dev)
-        ok = all(bool(torch.equal(y[p * per:(p + 1) * per], slice_of(p))) for p in range(world))
+        wrong = {}
+        for p in range(world):  # per peer slice: the fraction of elements that differ, and of 128-B lines
+            d = y[p * per:(p + 1) * per] != slice_of(p)
+            if bool(d.any()):
+                lines = d[:per // 32 * 32].view(-1, 32).any(dim=1)
+                wrong[p] = {"elems": round(float(d.float().mean()), 6), "lines": round(float(lines.float().mean()), 6)}
+        ok = not wrong
         dist.barrier()
         each = []
         t0 = time.perf_counter()
@@ -696,6 +702,8 @@ def allgather_compare(comms: dict, world: int, rank: int, dev, st, count: int, i
         t = (time.perf_counter() - t0) / iters
         res[name] = {"bit_exact": ok, "ms": round(t * 1e3, 3), "ms_each": [round(x, 3) for x in each],
                      "busbw_gb_s": round((world - 1) * per * 4 / t / 1e9, 1)}
+        if wrong:
+            res[name]["wrong_slices"] = wrong
     if dist.get_backend() == "nccl":
         dist.all_gather_into_tensor(y, mine)
         torch.cuda.synchronize(dev)
@@ -951,7 +959,7 @@ def allreduce_summary(ar) -> dict:
     for key in ("dccl_allgather", "c5_allgather"):
         ag = ar.get(key)
         if isinstance(ag, dict):
-            out[key] = {name: {k: v[k] for k in ("bit_exact", "ms", "busbw_gb_s") if k in v}
+            out[key] = {name: {k: v[k] for k in ("bit_exact", "ms", "busbw_gb_s", "wrong_slices") if k in v}
                         for name, v in ag.items() if isinstance(v, dict)}
     return out
 

@@ -6,8 +6,10 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -30,11 +32,15 @@ constexpr uint64_t kMagic = 0x3143504943434344ull;  // "DCCIPC1"
 constexpr uint32_t kMaxRanks = 64;
 constexpr size_t kHandleBytes = sizeof(hipIpcMemHandle_t);
 constexpr size_t kMaxOpenPerXport = 256;  // mappings kept open; the oldest is closed beyond this
+// ... or beyond this many bytes of peer memory: a mapping keeps the peer's allocation alive after the peer
+// freed it, so the cache must not hold more than a bounded amount of (possibly freed) peer memory
+constexpr size_t kMaxOpenBytesPerXport = size_t(64) << 30;
 
 struct ShmSlot {
     unsigned char h_in[kHandleBytes];
     unsigned char h_out[kHandleBytes];
     uint64_t off_in, off_out;
+    uint64_t serial_in, serial_out;  // the exporter's serial of each handle (see Export)
 };
 
 struct ShmCtl {
@@ -47,21 +53,43 @@ struct ShmCtl {
     ShmSlot slot[kMaxRanks];
 };
 
+// One export per allocation.  `serial` numbers the exports of this process: a handle's bytes can repeat
+// once the allocation it named is freed (a dmabuf export names a file descriptor, and the number is reused),
+// so importers tell a new allocation from the freed one by the serial, not by the bytes.
 struct Export {
     size_t size;
     uint64_t buffer_id;
+    uint64_t serial;
     hipIpcMemHandle_t handle;
+};
+
+struct Mapping {
+    void* base;
+    uint64_t serial;
+    size_t bytes;
 };
 
 struct IpcXport {
     ShmCtl* ctl = nullptr;
+    uint64_t next_serial = 1;
     std::map<uintptr_t, Export> exported;   // allocation base -> its handle (one export per allocation)
-    std::map<std::string, void*> opened;    // peer handle bytes -> mapped base
+    std::map<std::string, Mapping> opened;  // (peer rank, handle bytes) -> mapped base and the export's serial
     std::deque<std::string> open_order;
+    size_t open_bytes = 0;
     double timeout_s = 300.0;
 };
 
 IpcXport* xport(const dcclComm* c) { return static_cast<IpcXport*>(c->ipc); }
+
+// DCCL_IPC_DEBUG=1: one line on stderr per export made and per peer mapping opened, reused or replaced
+// (read once per process)
+bool ipc_debug() {
+    static const bool on = [] {
+        const char* v = std::getenv("DCCL_IPC_DEBUG");
+        return v != nullptr && *v == '1';
+    }();
+    return on;
+}
 
 // Sense-reversing barrier on the shared counters that also agrees on success: a rank arriving with
 // ok == false raises the segment's abort flag, and every rank returns ncclRemoteError from a barrier that
@@ -100,11 +128,13 @@ ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
     return s->abort.load(std::memory_order_relaxed) ? dccl::ncclRemoteError : dccl::ncclSuccess;
 }
 
-ncclResult_t export_ptr(IpcXport* x, const void* p, unsigned char* handle_out, uint64_t* off_out) {
+ncclResult_t export_ptr(IpcXport* x, const void* p, unsigned char* handle_out, uint64_t* off_out,
+                        uint64_t* serial_out) {
     hipDeviceptr_t base = nullptr;
     size_t size = 0;
-    if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess) {
+    if (const hipError_t e = hipMemGetAddressRange(&base, &size, const_cast<void*>(p)); e != hipSuccess) {
         (void)hipGetLastError();
+        if (ipc_debug()) std::fprintf(stderr, "[dccl ipc %d] hipMemGetAddressRange(%p) -> %d\n", ::getpid(), p, int(e));
         return dccl::ncclInvalidArgument;  // not a device allocation of this process
     }
     uint64_t id = 0;
@@ -114,46 +144,97 @@ ncclResult_t export_ptr(IpcXport* x, const void* p, unsigned char* handle_out, u
     const uintptr_t b = reinterpret_cast<uintptr_t>(base);
     auto it = x->exported.find(b);
     if (it == x->exported.end() || it->second.size != size || it->second.buffer_id != id) {
-        Export e{size, id, {}};
-        if (hipIpcGetMemHandle(&e.handle, base) != hipSuccess) {
+        Export e{size, id, x->next_serial++, {}};
+        if (const hipError_t he = hipIpcGetMemHandle(&e.handle, base); he != hipSuccess) {
             (void)hipGetLastError();
+            if (ipc_debug())
+                std::fprintf(stderr, "[dccl ipc %d] hipIpcGetMemHandle(base=%p size=%zu buffer_id=%llu) -> %d\n",
+                             ::getpid(), base, size, static_cast<unsigned long long>(id), int(he));
             return dccl::ncclUnhandledCudaError;
         }
         it = x->exported.insert_or_assign(b, e).first;
+        if (ipc_debug())
+            std::fprintf(stderr, "[dccl ipc %d] export base=%p size=%zu buffer_id=%llu serial=%llu\n", ::getpid(),
+                         base, size, static_cast<unsigned long long>(id), static_cast<unsigned long long>(e.serial));
     }
     std::memcpy(handle_out, &it->second.handle, kHandleBytes);
     *off_out = reinterpret_cast<uintptr_t>(p) - b;
+    *serial_out = it->second.serial;
     return dccl::ncclSuccess;
 }
 
-// Close the oldest mappings so that this call's imports fit under kMaxOpenPerXport.  Runs before any
-// import of the call (every earlier call's kernels have drained: arrive() synchronised the stream).
+// Close the oldest mappings so that this call's imports fit under kMaxOpenPerXport and the mappings kept
+// from earlier calls under kMaxOpenBytesPerXport.  Runs before any import of the call (every earlier
+// call's kernels have drained: arrive() synchronised the stream).
 void trim_mappings(IpcXport* x, size_t incoming) {
-    while (!x->open_order.empty() && x->opened.size() + incoming > kMaxOpenPerXport) {
+    while (!x->open_order.empty() &&
+           (x->opened.size() + incoming > kMaxOpenPerXport || x->open_bytes > kMaxOpenBytesPerXport)) {
         auto old = x->opened.find(x->open_order.front());
         if (old != x->opened.end()) {
-            (void)hipIpcCloseMemHandle(old->second);
+            (void)hipIpcCloseMemHandle(old->second.base);
+            x->open_bytes -= old->second.bytes;
             x->opened.erase(old);
         }
         x->open_order.pop_front();
     }
 }
 
-ncclResult_t import_ptr(IpcXport* x, const unsigned char* handle, uint64_t off, unsigned char** out) {
-    const std::string key(reinterpret_cast<const char*>(handle), kHandleBytes);
+// Map peer `peer`'s export (handle, serial) once and keep it.  The same handle bytes with another serial
+// name a new allocation that replaced a freed one: the old mapping (which would still show the freed
+// buffer's contents) is closed first, so the open below imports the new allocation.  Runs after a phase
+// point, with this rank's earlier kernels drained, so no launch still reads the closed mapping.
+ncclResult_t import_ptr(IpcXport* x, uint32_t peer, const unsigned char* handle, uint64_t serial, uint64_t off,
+                        unsigned char** out) {
+    std::string key(reinterpret_cast<const char*>(&peer), sizeof(peer));
+    key.append(reinterpret_cast<const char*>(handle), kHandleBytes);
     auto it = x->opened.find(key);
+    if (it != x->opened.end() && it->second.serial != serial) {
+        if (ipc_debug())
+            std::fprintf(stderr, "[dccl ipc %d] peer %u: handle repeats with serial %llu (mapped: %llu), remapping\n",
+                         ::getpid(), peer, static_cast<unsigned long long>(serial),
+                         static_cast<unsigned long long>(it->second.serial));
+        (void)hipIpcCloseMemHandle(it->second.base);
+        x->open_bytes -= it->second.bytes;
+        x->opened.erase(it);
+        for (auto o = x->open_order.begin(); o != x->open_order.end(); ++o)
+            if (*o == key) {
+                x->open_order.erase(o);
+                break;
+            }
+        it = x->opened.end();
+    }
     if (it == x->opened.end()) {
         hipIpcMemHandle_t h;
         std::memcpy(&h, handle, kHandleBytes);
         void* base = nullptr;
-        if (hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+        // Re-opening handle bytes whose previous mapping was closed just above can fail for a moment
+        // (hipErrorInvalidDevicePointer while the runtime still tears the old import down: about one call
+        // in ten in tests/test_direct.py::test_ipc_reallocated_buffers); retry with backoff for up to ~1 s.
+        hipError_t e = hipSuccess;
+        for (int attempt = 0, us = 100;; ++attempt, us = std::min(2 * us, 100000)) {
+            e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+            if (e == hipSuccess) break;
             (void)hipGetLastError();
-            return dccl::ncclUnhandledCudaError;
+            if (ipc_debug())
+                std::fprintf(stderr, "[dccl ipc %d] peer %u: hipIpcOpenMemHandle(serial %llu) -> %d (attempt %d)\n",
+                             ::getpid(), peer, static_cast<unsigned long long>(serial), int(e), attempt);
+            if (attempt == 14) return dccl::ncclUnhandledCudaError;
+            std::this_thread::sleep_for(std::chrono::microseconds(us));
         }
-        it = x->opened.emplace(key, base).first;
+        hipDeviceptr_t mb = nullptr;
+        size_t bytes = 0;
+        if (hipMemGetAddressRange(&mb, &bytes, base) != hipSuccess) {
+            (void)hipGetLastError();
+            bytes = 0;
+        }
+        x->open_bytes += bytes;
+        it = x->opened.emplace(key, Mapping{base, serial, bytes}).first;
         x->open_order.push_back(key);
+        if (ipc_debug())
+            std::fprintf(stderr, "[dccl ipc %d] peer %u: opened serial %llu at %p (%zu bytes, %zu mapped)\n",
+                         ::getpid(), peer, static_cast<unsigned long long>(serial), base, bytes, x->open_bytes);
     }
-    *out = static_cast<unsigned char*>(it->second) + off;
+    *out = static_cast<unsigned char*>(it->second.base) + off;
     return dccl::ncclSuccess;
 }
 
@@ -188,8 +269,8 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
     ncclResult_t rc = dccl::ncclSuccess;
     if (c->ipc) {
         ShmSlot& s = xport(c)->ctl->slot[r];
-        rc = export_ptr(xport(c), in, s.h_in, &s.off_in);
-        if (rc == dccl::ncclSuccess) rc = export_ptr(xport(c), out, s.h_out, &s.off_out);
+        rc = export_ptr(xport(c), in, s.h_in, &s.off_in, &s.serial_in);
+        if (rc == dccl::ncclSuccess) rc = export_ptr(xport(c), out, s.h_out, &s.off_out, &s.serial_out);
     } else {
         c->group->pub_in[r] = in;
         c->group->pub_out[r] = out;
@@ -206,8 +287,8 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
             const ShmSlot& s = xport(c)->ctl->slot[p];
             unsigned char* pi = nullptr;
             unsigned char* po = nullptr;
-            rc = import_ptr(xport(c), s.h_in, s.off_in, &pi);
-            if (rc == dccl::ncclSuccess) rc = import_ptr(xport(c), s.h_out, s.off_out, &po);
+            rc = import_ptr(xport(c), p, s.h_in, s.serial_in, s.off_in, &pi);
+            if (rc == dccl::ncclSuccess) rc = import_ptr(xport(c), p, s.h_out, s.serial_out, s.off_out, &po);
             if (rc != dccl::ncclSuccess) return rc;
             P->in[p] = pi;
             P->out[p] = po;
@@ -317,7 +398,7 @@ ncclResult_t ipc_leave(dcclComm* c) {
     IpcXport* x = xport(c);
     if (x == nullptr) return dccl::ncclInvalidArgument;
     const ncclResult_t rc = shm_barrier(x);  // no peer still reads our buffers
-    for (auto& kv : x->opened) (void)hipIpcCloseMemHandle(kv.second);
+    for (auto& kv : x->opened) (void)hipIpcCloseMemHandle(kv.second.base);
     munmap(x->ctl, sizeof(ShmCtl));
     delete x;
     c->ipc = nullptr;

@@ -371,3 +371,78 @@ def test_ipc_transport_processes(gpu, W, n, dt, op):
         _check(api, [results[r][api] for r in range(W)], W, n, dt, op)
     assert all(results[r]["host_rejected"] for r in range(W))
     assert all(results[r]["finalize"] == 0 for r in range(W))
+
+
+def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q):
+    """All-gathers over fresh allocations: before each round every buffer of the previous round is freed back to
+    the driver (torch.cuda.empty_cache), so the next allocation may reuse its address; every round carries new
+    data.  `grow`: odd rounds send W times as much, so a round's input lands where the previous round's output
+    was (bench.py's all_gather at 256 MiB followed by C5's)."""
+    os.environ["DCCL_BOOTSTRAP_TAG"] = tag
+    try:
+        import torch
+        import dccl_amd
+        torch.cuda.set_device(0)
+        comm = dccl_amd.Comm.ipc(W, r)
+        bad = []  # (round, peer, what it held) of every slice that is wrong
+        try:
+            st = torch.cuda.Stream()
+            for k in range(rounds):
+                n = nbytes // 4 * (W if grow and k % 2 else 1)
+                g = torch.Generator(device="cuda").manual_seed(1000 * k + r)
+                mine = torch.randint(-2**31, 2**31 - 1, (n,), device="cuda", dtype=torch.int32, generator=g)
+                out = torch.zeros(W * n, device="cuda", dtype=torch.int32)
+                torch.cuda.synchronize()
+                rc = comm.all_gather(mine.data_ptr(), out.data_ptr(), n, 2, st.cuda_stream)
+                if rc != 0:
+                    bad.append((k, -1, f"all_gather returned {rc}"))
+                    break
+                st.synchronize()
+                want = [torch.randint(-2**31, 2**31 - 1, (n,), device="cuda", dtype=torch.int32,
+                                      generator=torch.Generator(device="cuda").manual_seed(1000 * k + p))
+                        for p in range(W)]
+                for p in range(W):
+                    got = out[p * n:(p + 1) * n]
+                    if not torch.equal(got, want[p]):  # stale (an earlier round's data) or other
+                        stale = [j for j in range(k) if torch.equal(got, torch.randint(
+                            -2**31, 2**31 - 1, (n,), device="cuda", dtype=torch.int32,
+                            generator=torch.Generator(device="cuda").manual_seed(1000 * j + p)))]
+                        bad.append((k, p, f"round {stale} data" if stale else "other"))
+                del mine, out, want
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
+        finally:
+            fin = comm.finalize()
+        q.put((r, (bad, fin), None))
+    except Exception as e:  # pragma: no cover - reported by the parent
+        q.put((r, None, repr(e)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,nbytes,rounds,grow", [(2, 64 << 20, 4, False), (4, 256 << 20, 4, False),
+                                                  (4, 64 << 20, 4, True), (2, 1 << 20, 140, False)])
+def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow):
+    """A peer's buffer freed and a new one of the same size allocated must be mapped afresh: a cache of peer
+    mappings keyed by the IPC handle alone can hand back the freed buffer's mapping (the handle bytes of a
+    dmabuf export can repeat once the old export is closed), and the collective then reads stale data.
+    140 rounds at W = 2 import 280 peer allocations, past the 256 mappings a rank keeps open (trim_mappings)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    tag = "test_" + uuid.uuid4().hex[:12]
+    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q)) for r in range(W)]
+    for p in ps:
+        p.start()
+    results = {}
+    try:
+        for _ in range(W):
+            r, res, err = q.get(timeout=240)
+            assert err is None, (r, err)
+            results[r] = res
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(W):
+        bad, fin = results[r]
+        assert not bad and fin == 0, (r, bad[:8], len(bad), fin)
