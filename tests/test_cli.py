@@ -225,3 +225,68 @@ def test_cli_apis_against_oracle(api, gpu_flag, device, algo):
                             (8, 8 * 513, "bfloat16", 3), (5, 5 * 77, "uint64", 0), (4, 4 * (1 << 18), "float32", 0),
                             (6, 6 * 4099, "float16", 2), (7, 7 * 1000, "int32", 1)]:
         check_api(api, W, n, dtype, op, gpu_flag, device, env=env)
+
+
+# ------------------------------------------------------------ one process per rank (dccl_cli -p)
+def run_cli_processes(W, args, transport, timeout=240):
+    """W dccl_cli processes in -p mode (one rank each, ncclCommInit from the environment, as the reference's
+    CLI runs under its launcher), over DCCL_TRANSPORT=rccl (each rank its own NCCL_HOSTID, so RCCL joins the
+    ranks on one GPU over loopback sockets) or ipc; returns (exit codes, rows by rank, stderr)."""
+    import uuid
+    if not os.path.exists(CLI):
+        pytest.skip("dccl_cli not built")
+    tag = "cli_p_" + uuid.uuid4().hex[:10]
+    procs = []
+    for r in range(W):
+        env = {**os.environ, "DCCL_TRANSPORT": transport, "DCCL_RANK": str(r), "DCCL_WORLD_SIZE": str(W),
+               "DCCL_BOOTSTRAP_TAG": tag, "DCCL_IPC_TIMEOUT_S": "60"}
+        if transport == "rccl":
+            env.update({"NCCL_HOSTID": f"{tag}-{r}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"})
+        procs.append(subprocess.Popen([CLI, "-p", *map(str, args)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=timeout))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    rows = {}
+    for out, _ in outs:
+        for line in out.splitlines():
+            if line.startswith("{"):
+                row = json.loads(line)
+                rows[row["rank"]] = row
+    return [p.returncode for p in procs], rows, "".join(e for _, e in outs)[-3000:]
+
+
+def test_cli_process_mode_world1_and_env_check_cpu():
+    rc, rows, _ = run_cli("-p", "-a", "all_reduce", "-t", "float32", "-c", 64, "-r", 3,
+                          env={"DCCL_RANK": "0", "DCCL_WORLD_SIZE": "1"})
+    assert rc == 0 and rows == [{**rows[0], "rank": 0, "rc": 0}] and rows[0]["first"] == "0x00000000"
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "DCCL_RANK", "DCCL_WORLD_SIZE")}
+    p = subprocess.run([CLI, "-p", "-a", "all_reduce"], capture_output=True, text=True, env=env, timeout=60)
+    assert p.returncode == 1 and "DCCL_RANK" in p.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
+@pytest.mark.parametrize("kind", ["float32", "uint32"])
+def test_c1_known_answers_processes(transport, kind):
+    """BASELINE C1 as the reference runs it: `dccl_cli -a all_reduce -c 1024` as 4 processes, one rank each,
+    through the reference's ncclCommInit(&comm) (cli.cpp:360) with the transport from DCCL_TRANSPORT, device
+    buffers on the box's one GPU: every rank ends with the survey's bit patterns after 1, 2, 10 and 1000 calls."""
+    import dccl_amd
+    if transport == "rccl" and not dccl_amd.lib.dccl_rccl_available():
+        pytest.skip("librccl not loadable")
+    g = json.load(open(os.path.join(GOLDEN, "c1_ring.json")))
+    W = g["world_size"]
+    for reps in ("1", "2", "10", "1000"):
+        codes, rows, err = run_cli_processes(W, ["-a", "all_reduce", "-t", kind, "-c", g["count"], "-r", reps,
+                                                 "-g", 0], transport)
+        assert codes == [0] * W and sorted(rows) == list(range(W)), (codes, err)
+        for row in rows.values():
+            assert row["rc"] == 0 and row["uniform"] and int(row["first"], 16) == int(g[kind][reps], 16), (reps, row)
+        if reps == "1000":
+            print("C1 processes", transport, kind, "latency us/call", [rows[r]["us_per_call"] for r in range(W)])

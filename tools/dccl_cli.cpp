@@ -1,7 +1,11 @@
 // tools/dccl_cli.cpp — the MI355X build's counterpart of the reference's dccl_cli
 // (/root/reference/src/application/cli.cpp:190-557): a functional + timing driver of the
 // namespace-dccl API.  Ranks are threads of this process (one communicator each, joined with
-// dcclCommInitRank); -n sets the world size (the reference takes it from layout.json).
+// dcclCommInitRank); -n sets the world size (the reference takes it from layout.json).  With -p the
+// process is ONE rank, as the reference's dccl_cli is (one process per rank, README.md:74-101): rank and
+// world come from DCCL_RANK / DCCL_WORLD_SIZE (or RANK / WORLD_SIZE) and the communicator from the
+// reference's own ncclCommInit(&comm) (cli.cpp:360), over the transport DCCL_TRANSPORT names (rccl or ipc;
+// device buffers, -g).
 //
 // Buffers and inputs follow the reference CLI: host buffers are 64-B aligned with
 // sendbuf = memset(rank), recvbuf = memset(rank + 128) (cli.cpp:371-381); device buffers are
@@ -37,6 +41,8 @@ struct Opts {
     bool multi_gpu = false;
     long warmup = 0, repeat = 1000, count = 1024;
     int world = 1;
+    bool process = false;  // -p: this process is one rank (ncclCommInit)
+    int rank = 0;          // -p: from the environment
     ncclDataType_t dtype = ncclUint32;
     ncclRedOp_t op = ncclSum;
 };
@@ -77,7 +83,7 @@ void run_rank(const Opts& o, int rank, Result* out) {
         if (hipSetDevice(o.multi_gpu ? (o.gpu + rank) % ndev : o.gpu) != hipSuccess) { out->rc = 1; return; }
     }
     ncclComm_t comm = nullptr;
-    if ((out->rc = dcclCommInitRank(&comm, o.world, rank)) != ncclSuccess) return;
+    if ((out->rc = o.process ? ncclCommInit(&comm) : dcclCommInitRank(&comm, o.world, rank)) != ncclSuccess) return;
     void *send = nullptr, *recv = nullptr;
     hipStream_t stream = nullptr;
     if (o.gpu < 0) {
@@ -136,9 +142,10 @@ int main(int argc, char** argv) {
                                  {"type", required_argument, 0, 't'},   {"op", required_argument, 0, 'o'},
                                  {"count", required_argument, 0, 'c'},  {"world", required_argument, 0, 'n'},
                                  {"multi-gpu", no_argument, 0, 'm'},    {"help", no_argument, 0, 'h'},
+                                 {"process", no_argument, 0, 'p'},
                                  {0, 0, 0, 0}};
     int c;
-    while ((c = getopt_long(argc, argv, "a:g:w:r:t:o:c:n:mh", lo, nullptr)) != -1) {
+    while ((c = getopt_long(argc, argv, "a:g:w:r:t:o:c:n:mph", lo, nullptr)) != -1) {
         switch (c) {
         case 'a': o.api = optarg; break;
         case 'g': o.gpu = std::atoi(optarg); break;
@@ -147,23 +154,39 @@ int main(int argc, char** argv) {
         case 'c': o.count = std::atol(optarg); break;
         case 'n': o.world = std::atoi(optarg); break;
         case 'm': o.multi_gpu = true; break;
+        case 'p': o.process = true; break;
         case 't': if (!parse_dtype(optarg, &o.dtype)) { std::fprintf(stderr, "unknown type %s\n", optarg); return 1; } break;
         case 'o': if (!parse_op(optarg, &o.op)) { std::fprintf(stderr, "unknown op %s\n", optarg); return 1; } break;
         default:
             std::printf("usage: %s -a {all_reduce,reduce_scatter,all_gather,reduce,broadcast,send,recv} "
-                        "[-t type] [-o op] [-c count] [-w warmup] [-r repeat] [-g gpu|-1] [-n world] [-m]\n", argv[0]);
+                        "[-t type] [-o op] [-c count] [-w warmup] [-r repeat] [-g gpu|-1] [-n world] [-m] [-p]\n", argv[0]);
             return c == 'h' ? 0 : 1;
         }
     }
+    if (o.process) {
+        auto env = [](const char* a, const char* b) {
+            const char* v = std::getenv(a);
+            if (v == nullptr) v = std::getenv(b);
+            return v == nullptr ? -1 : std::atoi(v);
+        };
+        o.rank = env("DCCL_RANK", "RANK");
+        o.world = env("DCCL_WORLD_SIZE", "WORLD_SIZE");
+        if (o.rank < 0 || o.world < 1 || o.rank >= o.world) {
+            std::fprintf(stderr, "-p: set DCCL_RANK / DCCL_WORLD_SIZE (or RANK / WORLD_SIZE)\n");
+            return 1;
+        }
+    }
     if (o.api.empty() || o.world < 1 || o.count < 0) { std::fprintf(stderr, "missing/invalid -a/-n/-c\n"); return 1; }
-    std::vector<Result> res(o.world);
+    const int first_rank = o.process ? o.rank : 0, ranks = o.process ? 1 : o.world;
+    std::vector<Result> res(ranks);
     std::vector<std::thread> th;
-    for (int r = 0; r < o.world; ++r) th.emplace_back(run_rank, std::cref(o), r, &res[r]);
+    for (int i = 0; i < ranks; ++i) th.emplace_back(run_rank, std::cref(o), first_rank + i, &res[i]);
     for (auto& t : th) t.join();
     int rc = 0;
     const size_t esz = dccl_size_of_type(o.dtype);
-    for (int r = 0; r < o.world; ++r) {
-        const Result& x = res[r];
+    for (int i = 0; i < ranks; ++i) {
+        const int r = first_rank + i;
+        const Result& x = res[i];
         uint64_t first = 0;
         bool uniform = true;
         if (!x.bytes.empty()) {
