@@ -432,8 +432,8 @@ def _time_pairs(pairs, n: int, stream, launches: int) -> float:
 def graph_us_per_launch(pairs, n: int, dev, per_graph: int = 200, replays: int = 10) -> float:
     """Average duration (us) of one fp32 Sum combine of n elements when `per_graph` launches (cycling over
     the pointer pairs) are captured in one HIP graph (torch.cuda.CUDAGraph over dccl_local_reduce on the
-    capture stream) and the graph is replayed `replays` times: the device-side cost per launch without the
-    host's issue rate."""
+    capture stream) and the graph is replayed `replays` times, in three timed windows (median): the device-side
+    cost per launch without the host's issue rate."""
     side = torch.cuda.Stream(dev)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(side):
@@ -447,14 +447,16 @@ def graph_us_per_launch(pairs, n: int, dev, per_graph: int = 200, replays: int =
     torch.cuda.synchronize(dev)
     cur = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(cur)
-    for _ in range(replays):
-        g.replay()
-    ev1.record(cur)
-    ev1.synchronize()
-    ms = ev0.elapsed_time(ev1)
+    runs = []
+    for _ in range(3):  # the median of three timed windows: one disturbed window does not set the point
+        ev0.record(cur)
+        for _ in range(replays):
+            g.replay()
+        ev1.record(cur)
+        ev1.synchronize()
+        runs.append(ev0.elapsed_time(ev1))
     del g
-    return ms * 1e3 / (replays * per_graph)
+    return sorted(runs)[1] * 1e3 / (replays * per_graph)
 
 
 MALL_BYTES = 256 << 20  # MI355X Infinity Cache
