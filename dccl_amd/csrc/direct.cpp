@@ -152,7 +152,16 @@ ncclResult_t export_ptr(IpcXport* x, const void* p, unsigned char* handle_out, u
                              ::getpid(), base, size, static_cast<unsigned long long>(id), int(he));
             return dccl::ncclUnhandledCudaError;
         }
-        it = x->exported.insert_or_assign(b, e).first;
+        // entries whose range this allocation now covers name freed allocations: drop them, so the map
+        // holds one entry per address range in use rather than one per allocation ever exported
+        for (auto o = x->exported.lower_bound(b); o != x->exported.begin();) {
+            --o;
+            if (o->first + o->second.size <= b) break;
+            o = x->exported.erase(o);
+        }
+        for (auto o = x->exported.lower_bound(b); o != x->exported.end() && o->first < b + size;)
+            o = x->exported.erase(o);
+        it = x->exported.emplace(b, e).first;
         if (ipc_debug())
             std::fprintf(stderr, "[dccl ipc %d] export base=%p size=%zu buffer_id=%llu serial=%llu\n", ::getpid(),
                          base, size, static_cast<unsigned long long>(id), static_cast<unsigned long long>(e.serial));
