@@ -1,4 +1,4 @@
-"""The namespace-dccl collectives over the RCCL transport (dccl_comm_init_rccl, rccl_transport.cpp) with W real
+"""The namespace-dccl collectives over the RCCL transport (dccl_comm_init_rccl, rccl_transport.cpp) with W = 2-8 real
 RCCL ranks, one process each, on the box's one GPU.
 
 RCCL refuses two ranks on one device of one host ("Duplicate GPU detected"), so every rank process gets its own
@@ -81,7 +81,8 @@ def _run(W, n, dt, op, algo):
     return results
 
 
-@pytest.mark.parametrize("W,n,dt,op", [(2, 2 * 65536, 7, 0), (3, 3 * 4099, 2, 1), (4, 4 * 1000, 9, 3)])
+@pytest.mark.parametrize("W,n,dt,op", [(2, 2 * 65536, 7, 0), (3, 3 * 4099, 2, 1), (4, 4 * 1000, 9, 3),
+                                      (8, 8 * 777, 7, 2)])
 def test_rccl_transport_processes(gpu, W, n, dt, op):
     import dccl_amd
     if not dccl_amd.lib.dccl_rccl_available():
