@@ -13,7 +13,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <iterator>
 #include <map>
+#include <mutex>
 #include <random>
 #include <string>
 #include <thread>
@@ -31,10 +33,11 @@ using dccl::dcclComm;
 constexpr uint64_t kMagic = 0x3143504943434344ull;  // "DCCIPC1"
 constexpr uint32_t kMaxRanks = 64;
 constexpr size_t kHandleBytes = sizeof(hipIpcMemHandle_t);
-constexpr size_t kMaxOpenPerXport = 256;  // mappings kept open; the oldest is closed beyond this
-// ... or beyond this many bytes of peer memory: a mapping keeps the peer's allocation alive after the peer
-// freed it, so the cache must not hold more than a bounded amount of (possibly freed) peer memory
-constexpr size_t kMaxOpenBytesPerXport = size_t(64) << 30;
+// Peer mappings are kept for later calls, in one cache per process (below); the oldest unused one is
+// closed beyond this many, or beyond this many bytes of peer memory: a mapping keeps the peer's allocation
+// alive after the peer freed it, so the cache must not hold more than a bounded amount of it.
+constexpr size_t kMaxOpenMappings = 256;
+constexpr size_t kMaxOpenBytes = size_t(64) << 30;
 
 struct ShmSlot {
     unsigned char h_in[kHandleBytes];
@@ -53,9 +56,9 @@ struct ShmCtl {
     ShmSlot slot[kMaxRanks];
 };
 
-// One export per allocation.  `serial` numbers the exports of this process: a handle's bytes can repeat
-// once the allocation it named is freed (a dmabuf export names a file descriptor, and the number is reused),
-// so importers tell a new allocation from the freed one by the serial, not by the bytes.
+// One export per allocation.  `serial` numbers this process's exports: the handle bytes of a new allocation
+// at a freed one's address and size repeat (observed on ROCm 7.2), so importers tell a new
+// allocation from the freed one by the serial, not by the bytes.
 struct Export {
     size_t size;
     uint64_t buffer_id;
@@ -67,15 +70,30 @@ struct Mapping {
     void* base;
     uint64_t serial;
     size_t bytes;
+    uint32_t users;  // collectives of this process between their import and their last phase point
 };
+
+// Exports and peer mappings are per PROCESS, shared by every IPC communicator in it: the runtime hands out
+// one import per handle per process (opening handle bytes that are already open returns that mapping), so
+// a cache per communicator could not replace a stale mapping another communicator still holds.  Handle
+// bytes name the exporting process, so they key the mappings of every peer of every communicator.
+struct ProcCache {
+    std::mutex mu;
+    uint64_t next_serial = 1;
+    std::map<uintptr_t, Export> exported;  // allocation base -> its export
+    std::map<std::string, Mapping> opened;  // handle bytes -> mapping
+    std::deque<std::string> open_order;     // oldest first
+    size_t open_bytes = 0;
+    uint32_t comms = 0;                     // live IPC communicators of this process
+};
+
+ProcCache& cache() {
+    static ProcCache* c = new ProcCache;  // never destroyed: communicators may outlive static destructors
+    return *c;
+}
 
 struct IpcXport {
     ShmCtl* ctl = nullptr;
-    uint64_t next_serial = 1;
-    std::map<uintptr_t, Export> exported;   // allocation base -> its handle (one export per allocation)
-    std::map<std::string, Mapping> opened;  // (peer rank, handle bytes) -> mapped base and the export's serial
-    std::deque<std::string> open_order;
-    size_t open_bytes = 0;
     double timeout_s = 300.0;
 };
 
@@ -128,8 +146,7 @@ ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
     return s->abort.load(std::memory_order_relaxed) ? dccl::ncclRemoteError : dccl::ncclSuccess;
 }
 
-ncclResult_t export_ptr(IpcXport* x, const void* p, unsigned char* handle_out, uint64_t* off_out,
-                        uint64_t* serial_out) {
+ncclResult_t export_ptr(const void* p, unsigned char* handle_out, uint64_t* off_out, uint64_t* serial_out) {
     hipDeviceptr_t base = nullptr;
     size_t size = 0;
     if (const hipError_t e = hipMemGetAddressRange(&base, &size, const_cast<void*>(p)); e != hipSuccess) {
@@ -142,9 +159,11 @@ ncclResult_t export_ptr(IpcXport* x, const void* p, unsigned char* handle_out, u
         hipSuccess)
         (void)hipGetLastError();
     const uintptr_t b = reinterpret_cast<uintptr_t>(base);
-    auto it = x->exported.find(b);
-    if (it == x->exported.end() || it->second.size != size || it->second.buffer_id != id) {
-        Export e{size, id, x->next_serial++, {}};
+    ProcCache& pc = cache();
+    std::lock_guard<std::mutex> lock(pc.mu);
+    auto it = pc.exported.find(b);
+    if (it == pc.exported.end() || it->second.size != size || it->second.buffer_id != id) {
+        Export e{size, id, pc.next_serial++, {}};
         if (const hipError_t he = hipIpcGetMemHandle(&e.handle, base); he != hipSuccess) {
             (void)hipGetLastError();
             if (ipc_debug())
@@ -154,14 +173,14 @@ ncclResult_t export_ptr(IpcXport* x, const void* p, unsigned char* handle_out, u
         }
         // entries whose range this allocation now covers name freed allocations: drop them, so the map
         // holds one entry per address range in use rather than one per allocation ever exported
-        for (auto o = x->exported.lower_bound(b); o != x->exported.begin();) {
+        for (auto o = pc.exported.lower_bound(b); o != pc.exported.begin();) {
             --o;
             if (o->first + o->second.size <= b) break;
-            o = x->exported.erase(o);
+            o = pc.exported.erase(o);
         }
-        for (auto o = x->exported.lower_bound(b); o != x->exported.end() && o->first < b + size;)
-            o = x->exported.erase(o);
-        it = x->exported.emplace(b, e).first;
+        for (auto o = pc.exported.lower_bound(b); o != pc.exported.end() && o->first < b + size;)
+            o = pc.exported.erase(o);
+        it = pc.exported.emplace(b, e).first;
         if (ipc_debug())
             std::fprintf(stderr, "[dccl ipc %d] export base=%p size=%zu buffer_id=%llu serial=%llu\n", ::getpid(),
                          base, size, static_cast<unsigned long long>(id), static_cast<unsigned long long>(e.serial));
@@ -172,56 +191,58 @@ ncclResult_t export_ptr(IpcXport* x, const void* p, unsigned char* handle_out, u
     return dccl::ncclSuccess;
 }
 
-// Close the oldest mappings so that this call's imports fit under kMaxOpenPerXport and the mappings kept
-// from earlier calls under kMaxOpenBytesPerXport.  Runs before any import of the call (every earlier
-// call's kernels have drained: arrive() synchronised the stream).
-void trim_mappings(IpcXport* x, size_t incoming) {
-    while (!x->open_order.empty() &&
-           (x->opened.size() + incoming > kMaxOpenPerXport || x->open_bytes > kMaxOpenBytesPerXport)) {
-        auto old = x->opened.find(x->open_order.front());
-        if (old != x->opened.end()) {
-            (void)hipIpcCloseMemHandle(old->second.base);
-            x->open_bytes -= old->second.bytes;
-            x->opened.erase(old);
+void close_mapping(ProcCache& pc, std::map<std::string, Mapping>::iterator it) {
+    (void)hipIpcCloseMemHandle(it->second.base);
+    pc.open_bytes -= it->second.bytes;
+    const std::string key = it->first;
+    pc.opened.erase(it);
+    for (auto o = pc.open_order.begin(); o != pc.open_order.end(); ++o)
+        if (*o == key) {
+            pc.open_order.erase(o);
+            break;
         }
-        x->open_order.pop_front();
+}
+
+// Close the oldest unused mappings so that this call's imports fit under kMaxOpenMappings and the
+// mappings kept from earlier calls under kMaxOpenBytes.  A mapping in use by a collective of this process
+// (another communicator, another thread) is never closed.  Caller holds pc.mu.
+void trim_mappings(ProcCache& pc, size_t incoming) {
+    for (size_t i = 0; i < pc.open_order.size() &&
+                       (pc.opened.size() + incoming > kMaxOpenMappings || pc.open_bytes > kMaxOpenBytes);) {
+        auto it = pc.opened.find(pc.open_order[i]);
+        if (it != pc.opened.end() && it->second.users == 0) close_mapping(pc, it);
+        else ++i;
     }
 }
 
-// Map peer `peer`'s export (handle, serial) once and keep it.  The same handle bytes with another serial
-// name a new allocation that replaced a freed one: the old mapping (which would still show the freed
-// buffer's contents) is closed first, so the open below imports the new allocation.  Runs after a phase
-// point, with this rank's earlier kernels drained, so no launch still reads the closed mapping.
-ncclResult_t import_ptr(IpcXport* x, uint32_t peer, const unsigned char* handle, uint64_t serial, uint64_t off,
-                        unsigned char** out) {
-    std::string key(reinterpret_cast<const char*>(&peer), sizeof(peer));
-    key.append(reinterpret_cast<const char*>(handle), kHandleBytes);
-    auto it = x->opened.find(key);
-    if (it != x->opened.end() && it->second.serial != serial) {
+// Map a peer's export (handle, serial) once and keep it; the caller holds a use of it (users) until its
+// last phase point.  The same handle bytes with another serial name a new allocation that replaced a freed
+// one: the old mapping (which would still show the freed buffer's contents) is closed first, so the open
+// below imports the new allocation.  No collective of this process can still be using the old mapping:
+// the exporter freed that allocation, which it does only after every collective on it has completed on
+// every rank.  Caller holds pc.mu.
+ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, const unsigned char* handle, uint64_t serial, uint64_t off,
+                        unsigned char** out, std::vector<std::string>* held) {
+    const std::string key(reinterpret_cast<const char*>(handle), kHandleBytes);
+    auto it = pc.opened.find(key);
+    if (it != pc.opened.end() && it->second.serial != serial) {
         if (ipc_debug())
-            std::fprintf(stderr, "[dccl ipc %d] peer %u: handle repeats with serial %llu (mapped: %llu), remapping\n",
-                         ::getpid(), peer, static_cast<unsigned long long>(serial),
-                         static_cast<unsigned long long>(it->second.serial));
-        (void)hipIpcCloseMemHandle(it->second.base);
-        x->open_bytes -= it->second.bytes;
-        x->opened.erase(it);
-        for (auto o = x->open_order.begin(); o != x->open_order.end(); ++o)
-            if (*o == key) {
-                x->open_order.erase(o);
-                break;
-            }
-        it = x->opened.end();
+            std::fprintf(stderr, "[dccl ipc %d] peer %u: handle repeats with serial %llu (mapped: %llu, users %u), "
+                         "remapping\n", ::getpid(), peer, static_cast<unsigned long long>(serial),
+                         static_cast<unsigned long long>(it->second.serial), it->second.users);
+        if (it->second.users != 0) return dccl::ncclInternalError;  // see above: cannot happen
+        close_mapping(pc, it);
+        it = pc.opened.end();
     }
-    if (it == x->opened.end()) {
+    if (it == pc.opened.end()) {
         hipIpcMemHandle_t h;
         std::memcpy(&h, handle, kHandleBytes);
         void* base = nullptr;
         // Re-opening handle bytes whose previous mapping was closed just above can fail for a moment
         // (hipErrorInvalidDevicePointer while the runtime still tears the old import down: about one call
-        // in ten in tests/test_direct.py::test_ipc_reallocated_buffers); retry with backoff for up to ~1 s.
-        hipError_t e = hipSuccess;
+        // in six in tests/test_direct.py::test_ipc_reallocated_buffers); retry with backoff for ~0.5 s.
         for (int attempt = 0, us = 100;; ++attempt, us = std::min(2 * us, 100000)) {
-            e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+            const hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
             if (e == hipSuccess) break;
             (void)hipGetLastError();
             if (ipc_debug())
@@ -234,23 +255,39 @@ ncclResult_t import_ptr(IpcXport* x, uint32_t peer, const unsigned char* handle,
         size_t bytes = 0;
         if (hipMemGetAddressRange(&mb, &bytes, base) != hipSuccess) {
             (void)hipGetLastError();
-            bytes = 0;
+            bytes = 0;  // not counted against kMaxOpenBytes
         }
-        x->open_bytes += bytes;
-        it = x->opened.emplace(key, Mapping{base, serial, bytes}).first;
-        x->open_order.push_back(key);
+        pc.open_bytes += bytes;
+        it = pc.opened.emplace(key, Mapping{base, serial, bytes, 0}).first;
+        pc.open_order.push_back(key);
         if (ipc_debug())
             std::fprintf(stderr, "[dccl ipc %d] peer %u: opened serial %llu at %p (%zu bytes, %zu mapped)\n",
-                         ::getpid(), peer, static_cast<unsigned long long>(serial), base, bytes, x->open_bytes);
+                         ::getpid(), peer, static_cast<unsigned long long>(serial), base, bytes, pc.open_bytes);
     }
+    ++it->second.users;
+    held->push_back(key);
     *out = static_cast<unsigned char*>(it->second.base) + off;
     return dccl::ncclSuccess;
 }
 
-// Peer addresses of one collective's two buffers, own rank included.
+// Peer addresses of one collective's two buffers, own rank included.  On the IPC transport it holds a use
+// of every peer mapping it resolved, released when the collective returns (after its last phase point).
 struct Peers {
     std::vector<const unsigned char*> in;
     std::vector<unsigned char*> out;
+    std::vector<std::string> held;
+    Peers() = default;
+    Peers(const Peers&) = delete;
+    Peers& operator=(const Peers&) = delete;
+    ~Peers() {
+        if (held.empty()) return;
+        ProcCache& pc = cache();
+        std::lock_guard<std::mutex> lock(pc.mu);
+        for (const std::string& k : held) {
+            auto it = pc.opened.find(k);
+            if (it != pc.opened.end() && it->second.users > 0) --it->second.users;
+        }
+    }
 };
 
 // A phase point of a direct collective: this rank's stream has drained (its inputs / outputs are
@@ -278,8 +315,8 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
     ncclResult_t rc = dccl::ncclSuccess;
     if (c->ipc) {
         ShmSlot& s = xport(c)->ctl->slot[r];
-        rc = export_ptr(xport(c), in, s.h_in, &s.off_in, &s.serial_in);
-        if (rc == dccl::ncclSuccess) rc = export_ptr(xport(c), out, s.h_out, &s.off_out, &s.serial_out);
+        rc = export_ptr(in, s.h_in, &s.off_in, &s.serial_in);
+        if (rc == dccl::ncclSuccess) rc = export_ptr(out, s.h_out, &s.off_out, &s.serial_out);
     } else {
         c->group->pub_in[r] = in;
         c->group->pub_out[r] = out;
@@ -287,7 +324,12 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
     rc = arrive(c, st, rc);
     *met = rc == dccl::ncclSuccess;
     if (!*met) return rc;
-    if (c->ipc) trim_mappings(xport(c), 2 * size_t(W));
+    ProcCache& pc = cache();
+    std::unique_lock<std::mutex> lock(pc.mu, std::defer_lock);
+    if (c->ipc) {
+        lock.lock();
+        trim_mappings(pc, 2 * size_t(W));
+    }
     for (uint32_t p = 0; p < W; ++p) {
         if (p == r) {
             P->in[p] = static_cast<const unsigned char*>(in);
@@ -296,8 +338,8 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
             const ShmSlot& s = xport(c)->ctl->slot[p];
             unsigned char* pi = nullptr;
             unsigned char* po = nullptr;
-            rc = import_ptr(xport(c), p, s.h_in, s.serial_in, s.off_in, &pi);
-            if (rc == dccl::ncclSuccess) rc = import_ptr(xport(c), p, s.h_out, s.serial_out, s.off_out, &po);
+            rc = import_ptr(pc, p, s.h_in, s.serial_in, s.off_in, &pi, &P->held);
+            if (rc == dccl::ncclSuccess) rc = import_ptr(pc, p, s.h_out, s.serial_out, s.off_out, &po, &P->held);
             if (rc != dccl::ncclSuccess) return rc;
             P->in[p] = pi;
             P->out[p] = po;
@@ -392,6 +434,10 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
     x->ctl = ctl;
     if (const char* t = std::getenv("DCCL_IPC_TIMEOUT_S")) x->timeout_s = std::strtod(t, nullptr);
     ctl->joined.fetch_add(1);
+    {
+        std::lock_guard<std::mutex> lock(cache().mu);
+        ++cache().comms;
+    }
     c->ipc = x;
     c->rank = rank;
     c->world = world;
@@ -407,7 +453,18 @@ ncclResult_t ipc_leave(dcclComm* c) {
     IpcXport* x = xport(c);
     if (x == nullptr) return dccl::ncclInvalidArgument;
     const ncclResult_t rc = shm_barrier(x);  // no peer still reads our buffers
-    for (auto& kv : x->opened) (void)hipIpcCloseMemHandle(kv.second.base);
+    {
+        // the last IPC communicator of the process releases the peer mappings (and with them the peers'
+        // freed allocations they kept alive)
+        ProcCache& pc = cache();
+        std::lock_guard<std::mutex> lock(pc.mu);
+        if (pc.comms > 0 && --pc.comms == 0)
+            for (auto it = pc.opened.begin(); it != pc.opened.end();) {
+                auto next = std::next(it);
+                if (it->second.users == 0) close_mapping(pc, it);
+                it = next;
+            }
+    }
     munmap(x->ctl, sizeof(ShmCtl));
     delete x;
     c->ipc = nullptr;

@@ -381,17 +381,23 @@ def test_ipc_transport_processes(gpu, W, n, dt, op, gather):
     assert all(results[r]["finalize"] == 0 for r in range(W))
 
 
-def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q):
+def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False):
     """All-gathers over fresh allocations: before each round every buffer of the previous round is freed back to
     the driver (torch.cuda.empty_cache), so the next allocation may reuse its address; every round carries new
     data.  `grow`: odd rounds send W times as much, so a round's input lands where the previous round's output
-    was (bench.py's all_gather at 256 MiB followed by C5's)."""
+    was (bench.py's all_gather at 256 MiB followed by C5's).  `two_comms`: every round runs on two IPC
+    communicators of the same ranks (the second pushing its gather), as bench.py's collective child does."""
     os.environ["DCCL_BOOTSTRAP_TAG"] = tag
     try:
         import torch
         import dccl_amd
         torch.cuda.set_device(0)
         comm = dccl_amd.Comm.ipc(W, r)
+        comms = [comm]
+        if two_comms:
+            os.environ["DCCL_DIRECT_GATHER"] = "push"
+            comms.append(dccl_amd.Comm.ipc(W, r))
+            os.environ.pop("DCCL_DIRECT_GATHER")
         bad = []  # (round, peer, what it held) of every slice that is wrong
         try:
             st = torch.cuda.Stream()
@@ -401,43 +407,51 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q):
                 mine = torch.randint(-2**31, 2**31 - 1, (n,), device="cuda", dtype=torch.int32, generator=g)
                 out = torch.zeros(W * n, device="cuda", dtype=torch.int32)
                 torch.cuda.synchronize()
-                rc = comm.all_gather(mine.data_ptr(), out.data_ptr(), n, 2, st.cuda_stream)
-                if rc != 0:
-                    bad.append((k, -1, f"all_gather returned {rc}"))
-                    break
-                st.synchronize()
                 want = [torch.randint(-2**31, 2**31 - 1, (n,), device="cuda", dtype=torch.int32,
                                       generator=torch.Generator(device="cuda").manual_seed(1000 * k + p))
                         for p in range(W)]
-                for p in range(W):
-                    got = out[p * n:(p + 1) * n]
-                    if not torch.equal(got, want[p]):  # stale (an earlier round's data) or other
-                        stale = [j for j in range(k) if torch.equal(got, torch.randint(
-                            -2**31, 2**31 - 1, (n,), device="cuda", dtype=torch.int32,
-                            generator=torch.Generator(device="cuda").manual_seed(1000 * j + p)))]
-                        bad.append((k, p, f"round {stale} data" if stale else "other"))
+                for ci, cm in enumerate(comms):
+                    out.zero_()
+                    torch.cuda.synchronize()
+                    rc = cm.all_gather(mine.data_ptr(), out.data_ptr(), n, 2, st.cuda_stream)
+                    if rc != 0:
+                        bad.append((k, -1, f"comm {ci}: all_gather returned {rc}"))
+                        break
+                    st.synchronize()
+                    for p in range(W):
+                        got = out[p * n:(p + 1) * n]
+                        if not torch.equal(got, want[p]):  # stale (an earlier round's data) or other
+                            stale = [j for j in range(k) if torch.equal(got, torch.randint(
+                                -2**31, 2**31 - 1, (n,), device="cuda", dtype=torch.int32,
+                                generator=torch.Generator(device="cuda").manual_seed(1000 * j + p)))]
+                            bad.append((k, p, f"comm {ci}: round {stale} data" if stale else f"comm {ci}: other"))
+                if bad and bad[-1][1] == -1:
+                    break
                 del mine, out, want
                 torch.cuda.synchronize()
                 torch.cuda.empty_cache()
         finally:
-            fin = comm.finalize()
+            fin = max(cm.finalize() for cm in comms)
         q.put((r, (bad, fin), None))
     except Exception as e:  # pragma: no cover - reported by the parent
         q.put((r, None, repr(e)))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,nbytes,rounds,grow", [(2, 64 << 20, 4, False), (4, 256 << 20, 4, False),
-                                                  (4, 64 << 20, 4, True), (2, 1 << 20, 140, False)])
-def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow):
+@pytest.mark.parametrize("W,nbytes,rounds,grow,two", [(2, 64 << 20, 4, False, False), (4, 256 << 20, 4, False, False),
+                                                      (4, 64 << 20, 4, True, False), (2, 1 << 20, 140, False, False),
+                                                      (4, 64 << 20, 4, True, True), (2, 64 << 20, 6, False, True)])
+def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two):
     """A peer's buffer freed and a new one of the same size allocated must be mapped afresh: a cache of peer
     mappings keyed by the IPC handle alone can hand back the freed buffer's mapping (the handle bytes of a
     dmabuf export can repeat once the old export is closed), and the collective then reads stale data.
-    140 rounds at W = 2 import 280 peer allocations, past the 256 mappings a rank keeps open (trim_mappings)."""
+    140 rounds at W = 2 import 280 peer allocations, past the 256 mappings a rank keeps open (trim_mappings).
+    `two`: two communicators of the same ranks share the process's mappings (a stale mapping one of them still
+    held used to shadow the other's re-import)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     tag = "test_" + uuid.uuid4().hex[:12]
-    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q)) for r in range(W)]
+    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q, two)) for r in range(W)]
     for p in ps:
         p.start()
     results = {}
