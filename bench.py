@@ -553,10 +553,9 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
     through both cross-process transports:
       ring    ring RS with the gfx950 combine + ring AG, chunks moved by RCCL send/recv;
       direct  each GPU reduces its chunk from all peers' buffers at once over xGMI (IPC-mapped,
-              dccl_local_reduce_chain in the ring's order) and pulls the other chunks (DESIGN.md §7.3);
-      direct_push  the same, each GPU pushing its reduced chunk into the peers' buffers instead.
-    Each is checked against RCCL's own all_reduce (int32: bit-exact; fp32: |d| <= (W-1) eps sum|x|, a
-    different association order) and against the others (fp32: bit-exact, same order), and timed."""
+              dccl_local_reduce_chain in the ring's order) and pulls the other chunks.
+    Both are checked against RCCL's own all_reduce (int32: bit-exact; fp32: |d| <= (W-1) eps sum|x|, a
+    different association order) and against each other (fp32: bit-exact, same order), and timed."""
     _native()
     os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")
     transports = os.environ.get("DCCL_BENCH_AR_TRANSPORTS", "ring,direct").split(",")
@@ -573,14 +572,6 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
         comms["ring"] = dccl_amd.Comm.rccl(world, rank, obj[0])
     if "direct" in transports:
         comms["direct"] = dccl_amd.Comm.ipc(world, rank)
-        # the same transport with the all-gather step pushing chunks into the peers' buffers instead of pulling
-        # them (DCCL_DIRECT_GATHER=push, read when the communicator is created): which one xGMI moves faster
-        # is what this run measures
-        os.environ["DCCL_DIRECT_GATHER"] = "push"
-        try:
-            comms["direct_push"] = dccl_amd.Comm.ipc(world, rank)
-        finally:
-            os.environ.pop("DCCL_DIRECT_GATHER", None)
     out = {"count": count, "world": world, "bytes": count * 4}
     try:
         st = torch.cuda.current_stream(dev)
@@ -609,8 +600,7 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
             torch.cuda.synchronize(dev)
             t = (time.perf_counter() - t0) / iters
             res.update({"ms": round(t * 1e3, 3), "busbw_gb_s": round(2 * (world - 1) / world * count * 4 / t / 1e9, 1)})
-            if name != "direct_push":  # broadcast and reduce do not depend on the gather mode
-                res.update(root_ops(comm, world, rank, dev, st, xi, ri, iters))
+            res.update(root_ops(comm, world, rank, dev, st, xi, ri, iters))
             out[name] = res
             yf_by[name] = yf
         if "ring" in yf_by and "direct" in yf_by:
@@ -621,15 +611,6 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
             dccl_amd.check(comms["direct"].all_reduce(b_.data_ptr(), b_.data_ptr(), count, 7, 0, st.cuda_stream), "d")
             torch.cuda.synchronize(dev)
             out["fp32_direct_bit_exact_vs_ring"] = bool(torch.equal(a_.view(torch.int32), b_.view(torch.int32)))
-        if "direct" in yf_by and "direct_push" in yf_by:
-            # the gather mode moves the same bytes: pull and push must agree bit for bit
-            b2, c_ = xf.clone(), xf.clone()
-            torch.cuda.synchronize(dev)
-            dccl_amd.check(comms["direct"].all_reduce(b2.data_ptr(), b2.data_ptr(), count, 7, 0, st.cuda_stream), "d")
-            dccl_amd.check(comms["direct_push"].all_reduce(c_.data_ptr(), c_.data_ptr(), count, 7, 0, st.cuda_stream),
-                           "p")
-            torch.cuda.synchronize(dev)
-            out["fp32_push_bit_exact_vs_pull"] = bool(torch.equal(c_.view(torch.int32), b2.view(torch.int32)))
         dist.barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
@@ -648,8 +629,7 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
         if c5_gib > 0 and "direct" in comms:
             c5_count = int(c5_gib * GIB) // 4 // world * world
             torch.cuda.empty_cache()
-            out["c5_allgather"] = allgather_compare({k: comms[k] for k in ("direct", "direct_push") if k in comms},
-                                                    world, rank, dev, st, c5_count, 3)
+            out["c5_allgather"] = allgather_compare({"direct": comms["direct"]}, world, rank, dev, st, c5_count, 3)
     finally:
         for comm in comms.values():
             comm.finalize()
@@ -970,8 +950,8 @@ def allreduce_summary(ar) -> dict:
     """The bit-exactness flags and rates of dccl_allreduce (N > 1), small enough for the line's tail."""
     if not isinstance(ar, dict):
         return {"error": repr(ar)}
-    out = {k: ar[k] for k in ("error", "fp32_direct_bit_exact_vs_ring", "fp32_push_bit_exact_vs_pull") if k in ar}
-    for name in ("ring", "direct", "direct_push"):
+    out = {k: ar[k] for k in ("error", "fp32_direct_bit_exact_vs_ring") if k in ar}
+    for name in ("ring", "direct"):
         if isinstance(ar.get(name), dict):
             out[name] = {k: ar[name][k] for k in ("int32_sum_bit_exact_vs_rccl", "fp32_within_bound", "ms",
                                                   "busbw_gb_s", "broadcast_bit_exact", "broadcast_ms",

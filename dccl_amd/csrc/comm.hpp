@@ -22,8 +22,6 @@
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
-#include <cstdlib>
-#include <cstring>
 #include <deque>
 #include <memory>
 #include <mutex>
@@ -91,12 +89,6 @@ private:
     std::atomic<uint64_t> barrier_gen_{0};  // written under bmu_, polled without it
 };
 
-// DCCL_DIRECT_GATHER=push, read when a communicator is created: see dcclComm::gather_push.
-inline bool direct_gather_push_env() {
-    const char* v = std::getenv("DCCL_DIRECT_GATHER");
-    return v != nullptr && std::strcmp(v, "push") == 0;
-}
-
 }  // namespace dccl_amd
 
 // The opaque communicator of include/dccl/dccl.hpp.
@@ -113,11 +105,6 @@ struct dccl::dcclComm {
     bool p2p_host = false;    // the p2p transport moves host memory (RCCL: no)
     bool p2p_device = true;   // the p2p transport moves device memory (RCCL: yes)
     void* ipc = nullptr;   // non-null: cross-process IPC peer-read transport (direct.hpp), device buffers only
-    // The all-gather step of the direct collectives (direct_all_gather, the second half of direct_all_reduce):
-    // false = every rank pulls the other chunks from their owners (peer reads, the default); true = every
-    // owner pushes its chunk into the other ranks' buffers (peer writes).  Same bytes, same result; which one
-    // an xGMI mesh moves faster is measured by bench.py's N > 1 run (`direct_push`).
-    bool gather_push = dccl_amd::direct_gather_push_env();
     // Events of the stream-ordered device transport: a ring of `event_ring` per peer, indexed by the
     // channel's message count, so that no event is recorded again before every wait on its previous
     // record has been enqueued.  A ring phase posts at most W-1 messages to one peer before it

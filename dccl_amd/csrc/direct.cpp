@@ -502,19 +502,12 @@ ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t
     if ((rc = arrive(c, st, rc)) != dccl::ncclSuccess) return rc;  // every chunk reduced by its owner
     std::vector<const void*> src;
     std::vector<void*> dst;
-    for (uint32_t p = 0; p < W; ++p) {
-        if (p == r) continue;
-        if (c->gather_push) {  // our chunk into every peer's buffer
-            src.push_back(P.out[r] + mine * slot);
-            dst.push_back(P.out[p] + mine * slot);
-        } else {  // chunk p+1 from its owner, rank p
-            const uint32_t k = (p + 1) % W;
-            src.push_back(P.out[p] + k * slot);
-            dst.push_back(P.out[r] + k * slot);
-        }
+    for (uint32_t k = 0; k < W; ++k) {
+        if (k == mine) continue;
+        src.push_back(P.out[(k + W - 1) % W] + k * slot);  // chunk k lives on rank k-1
+        dst.push_back(P.out[r] + k * slot);
     }
-    // pull: peers are done reading our buffers; push: every chunk has landed in ours
-    return arrive(c, st, copy_pairs(src, dst, slot, st));
+    return arrive(c, st, copy_pairs(src, dst, slot, st));  // peers are done reading our buffers
 }
 
 bool host_direct_selected(const dcclComm* c, size_t slot_bytes) {
@@ -626,13 +619,8 @@ ncclResult_t direct_all_gather(dcclComm* c, const void* send, void* recv, size_t
         std::vector<void*> dst;
         for (uint32_t p = 0; p < W; ++p) {
             if (p == r && P.in[r] == P.out[r] + r * slot) continue;  // already in place
-            if (c->gather_push) {  // our slice into rank p's buffer
-                src.push_back(P.in[r]);
-                dst.push_back(P.out[p] + r * slot);
-            } else {  // rank p's slice into ours
-                src.push_back(P.in[p]);
-                dst.push_back(P.out[r] + p * slot);
-            }
+            src.push_back(P.in[p]);
+            dst.push_back(P.out[r] + p * slot);
         }
         rc = copy_pairs(src, dst, slot, st);
     }

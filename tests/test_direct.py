@@ -294,17 +294,12 @@ APIS = ["all_reduce_inplace", "all_reduce", "reduce_scatter", "reduce", "all_gat
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,n,dt,op,gather", [(2, 2 * 4099, 7, 0, "pull"), (4, 4 * 65536, 9, 2, "pull"),
-                                              (8, 8 * 1001, 4, 1, "pull"), (3, 3 * 777, 6, 3, "pull"),
-                                              (5, 5 * 77, 5, 0, "pull"), (4, 4 * 4099, 7, 0, "push"),
-                                              (8, 8 * 1001, 2, 3, "push")])
-def test_direct_in_process(gpu, monkeypatch, W, n, dt, op, gather):
-    """Every direct collective with thread ranks, the all-gather step pulling (default) or pushing
-    (DCCL_DIRECT_GATHER=push)."""
+@pytest.mark.parametrize("W,n,dt,op", [(2, 2 * 4099, 7, 0), (4, 4 * 65536, 9, 2), (8, 8 * 1001, 4, 1),
+                                       (3, 3 * 777, 6, 3), (5, 5 * 77, 5, 0)])
+def test_direct_in_process(gpu, monkeypatch, W, n, dt, op):
     import torch
     import dccl_amd
     monkeypatch.setenv("DCCL_ALLREDUCE_ALGORITHM", "direct")
-    monkeypatch.setenv("DCCL_DIRECT_GATHER", gather)
     for api in APIS:
         outs, errs = [None] * W, []
 
@@ -328,9 +323,8 @@ def test_direct_in_process(gpu, monkeypatch, W, n, dt, op, gather):
         _check(api, outs, W, n, dt, op)
 
 
-def _ipc_rank(r, W, n, dt, op, tag, q, gather="pull"):
+def _ipc_rank(r, W, n, dt, op, tag, q):
     os.environ["DCCL_BOOTSTRAP_TAG"] = tag
-    os.environ["DCCL_DIRECT_GATHER"] = gather
     try:
         import torch
         import dccl_amd
@@ -351,17 +345,15 @@ def _ipc_rank(r, W, n, dt, op, tag, q, gather="pull"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,n,dt,op,gather", [(2, 2 * 65536, 7, 0, "pull"), (4, 4 * 4099, 2, 1, "pull"),
-                                              (3, 3 * 1000, 9, 3, "pull"), (8, 8 * 65536, 7, 0, "pull"),
-                                              (2, 2 * 65536, 7, 0, "push"), (4, 4 * 4099, 9, 2, "push")])
-def test_ipc_transport_processes(gpu, W, n, dt, op, gather):
+@pytest.mark.parametrize("W,n,dt,op", [(2, 2 * 65536, 7, 0), (4, 4 * 4099, 2, 1), (3, 3 * 1000, 9, 3),
+                                      (8, 8 * 65536, 7, 0)])
+def test_ipc_transport_processes(gpu, W, n, dt, op):
     """One process per rank (all on the box's one GPU), buffers exported with hipIpcGetMemHandle and
-    read (or, DCCL_DIRECT_GATHER=push, written) by the peers: every direct collective bit-exact against
-    the ring simulation."""
+    read by the peers: every direct collective bit-exact against the ring simulation."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     tag = "test_" + uuid.uuid4().hex[:12]
-    ps = [ctx.Process(target=_ipc_rank, args=(r, W, n, dt, op, tag, q, gather)) for r in range(W)]
+    ps = [ctx.Process(target=_ipc_rank, args=(r, W, n, dt, op, tag, q)) for r in range(W)]
     for p in ps:
         p.start()
     results = {}
@@ -386,7 +378,7 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False):
     the driver (torch.cuda.empty_cache), so the next allocation may reuse its address; every round carries new
     data.  `grow`: odd rounds send W times as much, so a round's input lands where the previous round's output
     was (bench.py's all_gather at 256 MiB followed by C5's).  `two_comms`: every round runs on two IPC
-    communicators of the same ranks (the second pushing its gather), as bench.py's collective child does."""
+    communicators of the same ranks, which share the process's peer mappings."""
     os.environ["DCCL_BOOTSTRAP_TAG"] = tag
     try:
         import torch
@@ -395,9 +387,7 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False):
         comm = dccl_amd.Comm.ipc(W, r)
         comms = [comm]
         if two_comms:
-            os.environ["DCCL_DIRECT_GATHER"] = "push"
             comms.append(dccl_amd.Comm.ipc(W, r))
-            os.environ.pop("DCCL_DIRECT_GATHER")
         bad = []  # (round, peer, what it held) of every slice that is wrong
         try:
             st = torch.cuda.Stream()
