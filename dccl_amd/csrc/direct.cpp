@@ -109,6 +109,15 @@ bool ipc_debug() {
     return on;
 }
 
+// DCCL_IPC_CACHE=0: no peer mapping outlives the collective that opened it (read once per process)
+bool ipc_cache_off() {
+    static const bool off = [] {
+        const char* v = std::getenv("DCCL_IPC_CACHE");
+        return v != nullptr && *v == '0';
+    }();
+    return off;
+}
+
 // Sense-reversing barrier on the shared counters that also agrees on success: a rank arriving with
 // ok == false raises the segment's abort flag, and every rank returns ncclRemoteError from a barrier that
 // completes with the flag up.  The flag is sticky (the transport is unusable after a failed collective,
@@ -164,12 +173,19 @@ ncclResult_t export_ptr(const void* p, unsigned char* handle_out, uint64_t* off_
     auto it = pc.exported.find(b);
     if (it == pc.exported.end() || it->second.size != size || it->second.buffer_id != id) {
         Export e{size, id, pc.next_serial++, {}};
-        if (const hipError_t he = hipIpcGetMemHandle(&e.handle, base); he != hipSuccess) {
+        // Exporting an allocation at the address of a freed one that a peer still maps can fail for a moment
+        // (hipErrorInvalidValue; seen about once in 600 re-allocations in tests/test_direct.py::
+        // test_ipc_reallocated_buffers); retry with backoff for ~0.5 s, like the re-open in import_ptr.
+        for (int attempt = 0, us = 100;; ++attempt, us = std::min(2 * us, 100000)) {
+            const hipError_t he = hipIpcGetMemHandle(&e.handle, base);
+            if (he == hipSuccess) break;
             (void)hipGetLastError();
             if (ipc_debug())
-                std::fprintf(stderr, "[dccl ipc %d] hipIpcGetMemHandle(base=%p size=%zu buffer_id=%llu) -> %d\n",
-                             ::getpid(), base, size, static_cast<unsigned long long>(id), int(he));
-            return dccl::ncclUnhandledCudaError;
+                std::fprintf(stderr, "[dccl ipc %d] hipIpcGetMemHandle(base=%p size=%zu buffer_id=%llu) -> %d "
+                             "(attempt %d)\n", ::getpid(), base, size, static_cast<unsigned long long>(id), int(he),
+                             attempt);
+            if (attempt == 14) return dccl::ncclUnhandledCudaError;
+            std::this_thread::sleep_for(std::chrono::microseconds(us));
         }
         // entries whose range this allocation now covers name freed allocations: drop them, so the map
         // holds one entry per address range in use rather than one per allocation ever exported
@@ -210,8 +226,15 @@ void trim_mappings(ProcCache& pc, size_t incoming) {
     for (size_t i = 0; i < pc.open_order.size() &&
                        (pc.opened.size() + incoming > kMaxOpenMappings || pc.open_bytes > kMaxOpenBytes);) {
         auto it = pc.opened.find(pc.open_order[i]);
-        if (it != pc.opened.end() && it->second.users == 0) close_mapping(pc, it);
-        else ++i;
+        if (it != pc.opened.end() && it->second.users == 0) {
+            if (ipc_debug())
+                std::fprintf(stderr, "[dccl ipc %d] trim: closing serial %llu at %p (%zu open, %zu bytes)\n", ::getpid(),
+                             static_cast<unsigned long long>(it->second.serial), it->second.base, pc.opened.size(),
+                             pc.open_bytes);
+            close_mapping(pc, it);
+        } else {
+            ++i;
+        }
     }
 }
 
@@ -285,7 +308,8 @@ struct Peers {
         std::lock_guard<std::mutex> lock(pc.mu);
         for (const std::string& k : held) {
             auto it = pc.opened.find(k);
-            if (it != pc.opened.end() && it->second.users > 0) --it->second.users;
+            if (it != pc.opened.end() && it->second.users > 0 && --it->second.users == 0 && ipc_cache_off())
+                close_mapping(pc, it);
         }
     }
 };

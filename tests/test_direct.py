@@ -373,12 +373,13 @@ def test_ipc_transport_processes(gpu, W, n, dt, op):
     assert all(results[r]["finalize"] == 0 for r in range(W))
 
 
-def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False):
+def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=False):
     """All-gathers over fresh allocations: before each round every buffer of the previous round is freed back to
     the driver (torch.cuda.empty_cache), so the next allocation may reuse its address; every round carries new
     data.  `grow`: odd rounds send W times as much, so a round's input lands where the previous round's output
     was (bench.py's all_gather at 256 MiB followed by C5's).  `two_comms`: every round runs on two IPC
-    communicators of the same ranks, which share the process's peer mappings."""
+    communicators of the same ranks, which share the process's peer mappings.  `hold`: nothing is freed, so
+    every round's buffers are new allocations and the peer mappings pile up past the cache's bound."""
     os.environ["DCCL_BOOTSTRAP_TAG"] = tag
     try:
         import torch
@@ -389,6 +390,7 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False):
         if two_comms:
             comms.append(dccl_amd.Comm.ipc(W, r))
         bad = []  # (round, peer, what it held) of every slice that is wrong
+        kept = []
         try:
             st = torch.cuda.Stream()
             for k in range(rounds):
@@ -414,12 +416,17 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False):
                             stale = [j for j in range(k) if torch.equal(got, torch.randint(
                                 -2**31, 2**31 - 1, (n,), device="cuda", dtype=torch.int32,
                                 generator=torch.Generator(device="cuda").manual_seed(1000 * j + p)))]
-                            bad.append((k, p, f"comm {ci}: round {stale} data" if stale else f"comm {ci}: other"))
+                            d = got != want[p]
+                            frac = f"{float(d.float().mean()):.4f} of elements"
+                            bad.append((k, p, f"comm {ci}: round {stale} data" if stale else f"comm {ci}: other, {frac}"))
                 if bad and bad[-1][1] == -1:
                     break
+                if hold:
+                    kept.append((mine, out))
                 del mine, out, want
                 torch.cuda.synchronize()
-                torch.cuda.empty_cache()
+                if not hold:
+                    torch.cuda.empty_cache()
         finally:
             fin = max(cm.finalize() for cm in comms)
         q.put((r, (bad, fin), None))
@@ -428,20 +435,21 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,nbytes,rounds,grow,two", [(2, 64 << 20, 4, False, False), (4, 256 << 20, 4, False, False),
-                                                      (4, 64 << 20, 4, True, False), (2, 1 << 20, 140, False, False),
-                                                      (4, 64 << 20, 4, True, True), (2, 64 << 20, 6, False, True)])
-def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two):
+@pytest.mark.parametrize("W,nbytes,rounds,grow,two,hold", [
+    (2, 64 << 20, 4, False, False, False), (4, 256 << 20, 4, False, False, False), (4, 64 << 20, 4, True, False, False),
+    (4, 64 << 20, 4, True, True, False), (2, 64 << 20, 6, False, True, False), (2, 16 << 20, 140, False, False, True)])
+def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold):
     """A peer's buffer freed and a new one of the same size allocated must be mapped afresh: a cache of peer
     mappings keyed by the IPC handle alone can hand back the freed buffer's mapping (the handle bytes of a
     dmabuf export can repeat once the old export is closed), and the collective then reads stale data.
-    140 rounds at W = 2 import 280 peer allocations, past the 256 mappings a rank keeps open (trim_mappings).
+    140 rounds at W = 2 with every buffer kept (16 MiB inputs, 32 MiB outputs: one allocation each) import 280
+    peer allocations, past the 256 mappings a process keeps open (trim_mappings closes the oldest unused ones).
     `two`: two communicators of the same ranks share the process's mappings (a stale mapping one of them still
     held used to shadow the other's re-import)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     tag = "test_" + uuid.uuid4().hex[:12]
-    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q, two)) for r in range(W)]
+    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q, two, hold)) for r in range(W)]
     for p in ps:
         p.start()
     results = {}
