@@ -164,14 +164,19 @@ ncclResult_t export_ptr(const void* p, unsigned char* handle_out, uint64_t* off_
         return dccl::ncclInvalidArgument;  // not a device allocation of this process
     }
     uint64_t id = 0;
-    if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, reinterpret_cast<hipDeviceptr_t>(base)) !=
-        hipSuccess)
+    const bool have_id = hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
+                                                reinterpret_cast<hipDeviceptr_t>(base)) == hipSuccess;
+    if (!have_id) {
         (void)hipGetLastError();
+        if (ipc_debug()) std::fprintf(stderr, "[dccl ipc %d] no buffer id for %p: exported afresh\n", ::getpid(), base);
+    }
     const uintptr_t b = reinterpret_cast<uintptr_t>(base);
     ProcCache& pc = cache();
     std::lock_guard<std::mutex> lock(pc.mu);
     auto it = pc.exported.find(b);
-    if (it == pc.exported.end() || it->second.size != size || it->second.buffer_id != id) {
+    // without the allocation's buffer id the cached export cannot be told from a freed allocation's at the
+    // same address and size: export again (a new serial makes the peers re-map)
+    if (!have_id || it == pc.exported.end() || it->second.size != size || it->second.buffer_id != id) {
         Export e{size, id, pc.next_serial++, {}};
         // Exporting an allocation at the address of a freed one that a peer still maps can fail for a moment
         // (hipErrorInvalidValue; seen about once in 600 re-allocations in tests/test_direct.py::
