@@ -44,6 +44,8 @@ struct ShmSlot {
     unsigned char h_out[kHandleBytes];
     uint64_t off_in, off_out;
     uint64_t serial_in, serial_out;  // the exporter's serial of each handle (see Export)
+    uint64_t base_in, base_out;      // the exported allocations' base addresses in the exporter
+    int64_t pid;                     // the exporter
 };
 
 struct ShmCtl {
@@ -70,18 +72,29 @@ struct Mapping {
     void* base;
     uint64_t serial;
     size_t bytes;
-    uint32_t users;  // collectives of this process between their import and their last phase point
+    uint32_t users;      // collectives of this process between their import and their last phase point
+    uint64_t import_id;  // the runtime's buffer id of this import (0: unknown)
 };
+
+uint64_t buffer_id_of(void* p) {
+    uint64_t id = 0;
+    if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, reinterpret_cast<hipDeviceptr_t>(p)) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return id;
+}
 
 // Exports and peer mappings are per PROCESS, shared by every IPC communicator in it: the runtime hands out
 // one import per handle per process (opening handle bytes that are already open returns that mapping), so
-// a cache per communicator could not replace a stale mapping another communicator still holds.  Handle
-// bytes name the exporting process, so they key the mappings of every peer of every communicator.
+// a cache per communicator could not replace a stale mapping another communicator still holds.  Mappings
+// are keyed by the exporting process and the allocation's address there, for every peer of every communicator.
 struct ProcCache {
     std::mutex mu;
     uint64_t next_serial = 1;
     std::map<uintptr_t, Export> exported;  // allocation base -> its export
-    std::map<std::string, Mapping> opened;  // handle bytes -> mapping
+    std::map<std::string, Mapping> opened;  // (exporter pid, allocation base) -> mapping
     std::deque<std::string> open_order;     // oldest first
     size_t open_bytes = 0;
     uint32_t comms = 0;                     // live IPC communicators of this process
@@ -155,7 +168,8 @@ ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
     return s->abort.load(std::memory_order_relaxed) ? dccl::ncclRemoteError : dccl::ncclSuccess;
 }
 
-ncclResult_t export_ptr(const void* p, unsigned char* handle_out, uint64_t* off_out, uint64_t* serial_out) {
+ncclResult_t export_ptr(const void* p, unsigned char* handle_out, uint64_t* off_out, uint64_t* serial_out,
+                        uint64_t* base_out) {
     hipDeviceptr_t base = nullptr;
     size_t size = 0;
     if (const hipError_t e = hipMemGetAddressRange(&base, &size, const_cast<void*>(p)); e != hipSuccess) {
@@ -209,6 +223,7 @@ ncclResult_t export_ptr(const void* p, unsigned char* handle_out, uint64_t* off_
     std::memcpy(handle_out, &it->second.handle, kHandleBytes);
     *off_out = reinterpret_cast<uintptr_t>(p) - b;
     *serial_out = it->second.serial;
+    *base_out = b;
     return dccl::ncclSuccess;
 }
 
@@ -244,14 +259,20 @@ void trim_mappings(ProcCache& pc, size_t incoming) {
 }
 
 // Map a peer's export (handle, serial) once and keep it; the caller holds a use of it (users) until its
-// last phase point.  The same handle bytes with another serial name a new allocation that replaced a freed
-// one: the old mapping (which would still show the freed buffer's contents) is closed first, so the open
-// below imports the new allocation.  No collective of this process can still be using the old mapping:
+// last phase point.  The same exporter address with another serial names a new allocation that replaced a
+// freed one: the old mapping (which would still show the freed buffer's contents) is closed first, so the
+// open below imports the new allocation.  No collective of this process can still be using the old mapping:
 // the exporter freed that allocation, which it does only after every collective on it has completed on
 // every rank.  Caller holds pc.mu.
-ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, const unsigned char* handle, uint64_t serial, uint64_t off,
-                        unsigned char** out, std::vector<std::string>* held) {
-    const std::string key(reinterpret_cast<const char*>(handle), kHandleBytes);
+ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, int64_t pid, uint64_t base, const unsigned char* handle,
+                        uint64_t serial, uint64_t off, unsigned char** out, std::vector<std::string>* held) {
+    // the key is the exporter's process and allocation address, not the handle bytes: a new allocation at a
+    // freed one's address is the same key with another serial whatever its handle bytes, so the freed
+    // allocation's mapping is closed before the new one is opened (the runtime may otherwise hand back its
+    // import of that address)
+    std::string key(reinterpret_cast<const char*>(&pid), sizeof(pid));
+    key.append(reinterpret_cast<const char*>(&base), sizeof(base));
+    uint64_t stale_id = 0;
     auto it = pc.opened.find(key);
     if (it != pc.opened.end() && it->second.serial != serial) {
         if (ipc_debug())
@@ -259,6 +280,7 @@ ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, const unsigned char* handl
                          "remapping\n", ::getpid(), peer, static_cast<unsigned long long>(serial),
                          static_cast<unsigned long long>(it->second.serial), it->second.users);
         if (it->second.users != 0) return dccl::ncclInternalError;  // see above: cannot happen
+        stale_id = it->second.import_id;
         close_mapping(pc, it);
         it = pc.opened.end();
     }
@@ -266,11 +288,17 @@ ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, const unsigned char* handl
         hipIpcMemHandle_t h;
         std::memcpy(&h, handle, kHandleBytes);
         void* base = nullptr;
-        // Re-opening handle bytes whose previous mapping was closed just above can fail for a moment
-        // (hipErrorInvalidDevicePointer while the runtime still tears the old import down: about one call
-        // in six in tests/test_direct.py::test_ipc_reallocated_buffers); retry with backoff for ~0.5 s.
+        // Re-opening an address whose previous mapping was closed just above races with the runtime's
+        // release of the old import: the open can fail for a moment (hipErrorInvalidDevicePointer, about
+        // one call in six in tests/test_direct.py::test_ipc_reallocated_buffers).  It is retried with
+        // backoff for ~0.5 s, and so is an open that hands back the closed import itself (the same runtime
+        // buffer id; never seen in tools/ipc_churn_stress.py runs, checked because it would be silent).
         for (int attempt = 0, us = 100;; ++attempt, us = std::min(2 * us, 100000)) {
-            const hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+            hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+            if (e == hipSuccess && stale_id != 0 && buffer_id_of(base) == stale_id) {
+                (void)hipIpcCloseMemHandle(base);
+                e = hipErrorInvalidHandle;  // the old import again: not ours to use
+            }
             if (e == hipSuccess) break;
             (void)hipGetLastError();
             if (ipc_debug())
@@ -286,11 +314,13 @@ ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, const unsigned char* handl
             bytes = 0;  // not counted against kMaxOpenBytes
         }
         pc.open_bytes += bytes;
-        it = pc.opened.emplace(key, Mapping{base, serial, bytes, 0}).first;
+        it = pc.opened.emplace(key, Mapping{base, serial, bytes, 0, buffer_id_of(base)}).first;
         pc.open_order.push_back(key);
         if (ipc_debug())
-            std::fprintf(stderr, "[dccl ipc %d] peer %u: opened serial %llu at %p (%zu bytes, %zu mapped)\n",
-                         ::getpid(), peer, static_cast<unsigned long long>(serial), base, bytes, pc.open_bytes);
+            std::fprintf(stderr, "[dccl ipc %d] peer %u: opened serial %llu at %p (%zu bytes, %zu mapped, import %llu, "
+                         "replaced %llu)\n", ::getpid(), peer, static_cast<unsigned long long>(serial), base, bytes,
+                         pc.open_bytes, static_cast<unsigned long long>(it->second.import_id),
+                         static_cast<unsigned long long>(stale_id));
     }
     ++it->second.users;
     held->push_back(key);
@@ -344,8 +374,9 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
     ncclResult_t rc = dccl::ncclSuccess;
     if (c->ipc) {
         ShmSlot& s = xport(c)->ctl->slot[r];
-        rc = export_ptr(in, s.h_in, &s.off_in, &s.serial_in);
-        if (rc == dccl::ncclSuccess) rc = export_ptr(out, s.h_out, &s.off_out, &s.serial_out);
+        s.pid = ::getpid();
+        rc = export_ptr(in, s.h_in, &s.off_in, &s.serial_in, &s.base_in);
+        if (rc == dccl::ncclSuccess) rc = export_ptr(out, s.h_out, &s.off_out, &s.serial_out, &s.base_out);
     } else {
         c->group->pub_in[r] = in;
         c->group->pub_out[r] = out;
@@ -367,8 +398,9 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
             const ShmSlot& s = xport(c)->ctl->slot[p];
             unsigned char* pi = nullptr;
             unsigned char* po = nullptr;
-            rc = import_ptr(pc, p, s.h_in, s.serial_in, s.off_in, &pi, &P->held);
-            if (rc == dccl::ncclSuccess) rc = import_ptr(pc, p, s.h_out, s.serial_out, s.off_out, &po, &P->held);
+            rc = import_ptr(pc, p, s.pid, s.base_in, s.h_in, s.serial_in, s.off_in, &pi, &P->held);
+            if (rc == dccl::ncclSuccess)
+                rc = import_ptr(pc, p, s.pid, s.base_out, s.h_out, s.serial_out, s.off_out, &po, &P->held);
             if (rc != dccl::ncclSuccess) return rc;
             P->in[p] = pi;
             P->out[p] = po;

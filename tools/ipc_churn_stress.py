@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Churn stress of the IPC transport's peer-mapping cache: tests/test_direct.py's
+re-allocation rank body (all-gathers over buffers freed back to the driver and re-allocated every round, every
+round's data checked) run `--runs` times at W ranks on the box's one GPU.  One JSON line on stdout: runs, runs
+with a wrong slice or an error, and the first few reports.
+
+    python tools/ipc_churn_stress.py [--runs 20] [--world 2] [--mib 1] [--rounds 140] [--grow] [--two]
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import uuid
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    from tests.test_direct import _ipc_realloc_rank
+    p = argparse.ArgumentParser()
+    p.add_argument("--runs", type=int, default=20)
+    p.add_argument("--world", type=int, default=2)
+    p.add_argument("--mib", type=int, default=1)
+    p.add_argument("--rounds", type=int, default=140)
+    p.add_argument("--grow", action="store_true")
+    p.add_argument("--two", action="store_true")
+    a = p.parse_args()
+    ctx = mp.get_context("spawn")
+    failed, reports = 0, []
+    for run in range(a.runs):
+        q = ctx.Queue()
+        tag = "stress_" + uuid.uuid4().hex[:10]
+        ps = [ctx.Process(target=_ipc_realloc_rank,
+                          args=(r, a.world, a.mib << 20, a.rounds, a.grow, tag, q, a.two, False))
+              for r in range(a.world)]
+        for x in ps:
+            x.start()
+        bad = []
+        for _ in range(a.world):
+            r, res, err = q.get(timeout=300)
+            if err is not None:
+                bad.append((r, err))
+            elif res[0] or res[1] != 0:
+                bad.append((r, res[0][:4], res[1]))
+        for x in ps:
+            x.join(60)
+            if x.is_alive():
+                x.kill()
+        if bad:
+            failed += 1
+            reports.append({"run": run, "bad": bad})
+        print(f"run {run}: {'FAILED ' + repr(bad) if bad else 'ok'}", file=sys.stderr, flush=True)
+    print(json.dumps({"runs": a.runs, "world": a.world, "mib": a.mib, "rounds": a.rounds, "grow": a.grow,
+                      "two": a.two, "failed_runs": failed, "reports": reports[:5]}, default=str), flush=True)
+
+
+if __name__ == "__main__":
+    main()
