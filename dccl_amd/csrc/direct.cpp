@@ -45,6 +45,7 @@ struct ShmSlot {
     uint64_t off_in, off_out;
     uint64_t serial_in, serial_out;  // the exporter's serial of each handle (see Export)
     uint64_t base_in, base_out;      // the exported allocations' base addresses in the exporter
+    uint64_t size_in, size_out;      // and their sizes
     int64_t pid;                     // the exporter
 };
 
@@ -169,7 +170,7 @@ ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
 }
 
 ncclResult_t export_ptr(const void* p, unsigned char* handle_out, uint64_t* off_out, uint64_t* serial_out,
-                        uint64_t* base_out) {
+                        uint64_t* base_out, uint64_t* size_out) {
     hipDeviceptr_t base = nullptr;
     size_t size = 0;
     if (const hipError_t e = hipMemGetAddressRange(&base, &size, const_cast<void*>(p)); e != hipSuccess) {
@@ -224,6 +225,7 @@ ncclResult_t export_ptr(const void* p, unsigned char* handle_out, uint64_t* off_
     *off_out = reinterpret_cast<uintptr_t>(p) - b;
     *serial_out = it->second.serial;
     *base_out = b;
+    *size_out = it->second.size;
     return dccl::ncclSuccess;
 }
 
@@ -264,8 +266,9 @@ void trim_mappings(ProcCache& pc, size_t incoming) {
 // open below imports the new allocation.  No collective of this process can still be using the old mapping:
 // the exporter freed that allocation, which it does only after every collective on it has completed on
 // every rank.  Caller holds pc.mu.
-ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, int64_t pid, uint64_t base, const unsigned char* handle,
-                        uint64_t serial, uint64_t off, unsigned char** out, std::vector<std::string>* held) {
+ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, int64_t pid, uint64_t base, uint64_t size,
+                        const unsigned char* handle, uint64_t serial, uint64_t off, unsigned char** out,
+                        std::vector<std::string>* held) {
     // the key is the exporter's process and allocation address, not the handle bytes: a new allocation at a
     // freed one's address is the same key with another serial whatever its handle bytes, so the freed
     // allocation's mapping is closed before the new one is opened (the runtime may otherwise hand back its
@@ -287,17 +290,29 @@ ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, int64_t pid, uint64_t base
     if (it == pc.opened.end()) {
         hipIpcMemHandle_t h;
         std::memcpy(&h, handle, kHandleBytes);
-        void* base = nullptr;
+        void* mapped = nullptr;
         // Re-opening an address whose previous mapping was closed just above races with the runtime's
         // release of the old import: the open can fail for a moment (hipErrorInvalidDevicePointer, about
         // one call in six in tests/test_direct.py::test_ipc_reallocated_buffers).  It is retried with
         // backoff for ~0.5 s, and so is an open that hands back the closed import itself (the same runtime
         // buffer id; never seen in tools/ipc_churn_stress.py runs, checked because it would be silent).
         for (int attempt = 0, us = 100;; ++attempt, us = std::min(2 * us, 100000)) {
-            hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
-            if (e == hipSuccess && stale_id != 0 && buffer_id_of(base) == stale_id) {
-                (void)hipIpcCloseMemHandle(base);
+            hipError_t e = hipIpcOpenMemHandle(&mapped, h, hipIpcMemLazyEnablePeerAccess);
+            if (e == hipSuccess && stale_id != 0 && buffer_id_of(mapped) == stale_id) {
+                (void)hipIpcCloseMemHandle(mapped);
                 e = hipErrorInvalidHandle;  // the old import again: not ours to use
+            }
+            if (e == hipSuccess) {  // an import of another size is another allocation: not ours either
+                hipDeviceptr_t mb = nullptr;
+                size_t got = 0;
+                if (hipMemGetAddressRange(&mb, &got, mapped) == hipSuccess && got != size) {
+                    if (ipc_debug())
+                        std::fprintf(stderr, "[dccl ipc %d] peer %u: import of serial %llu is %zu bytes, not %llu\n",
+                                     ::getpid(), peer, static_cast<unsigned long long>(serial), got,
+                                     static_cast<unsigned long long>(size));
+                    (void)hipIpcCloseMemHandle(mapped);
+                    e = hipErrorInvalidHandle;
+                }
             }
             if (e == hipSuccess) break;
             (void)hipGetLastError();
@@ -309,16 +324,16 @@ ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, int64_t pid, uint64_t base
         }
         hipDeviceptr_t mb = nullptr;
         size_t bytes = 0;
-        if (hipMemGetAddressRange(&mb, &bytes, base) != hipSuccess) {
+        if (hipMemGetAddressRange(&mb, &bytes, mapped) != hipSuccess) {
             (void)hipGetLastError();
             bytes = 0;  // not counted against kMaxOpenBytes
         }
         pc.open_bytes += bytes;
-        it = pc.opened.emplace(key, Mapping{base, serial, bytes, 0, buffer_id_of(base)}).first;
+        it = pc.opened.emplace(key, Mapping{mapped, serial, bytes, 0, buffer_id_of(mapped)}).first;
         pc.open_order.push_back(key);
         if (ipc_debug())
             std::fprintf(stderr, "[dccl ipc %d] peer %u: opened serial %llu at %p (%zu bytes, %zu mapped, import %llu, "
-                         "replaced %llu)\n", ::getpid(), peer, static_cast<unsigned long long>(serial), base, bytes,
+                         "replaced %llu)\n", ::getpid(), peer, static_cast<unsigned long long>(serial), mapped, bytes,
                          pc.open_bytes, static_cast<unsigned long long>(it->second.import_id),
                          static_cast<unsigned long long>(stale_id));
     }
@@ -375,8 +390,9 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
     if (c->ipc) {
         ShmSlot& s = xport(c)->ctl->slot[r];
         s.pid = ::getpid();
-        rc = export_ptr(in, s.h_in, &s.off_in, &s.serial_in, &s.base_in);
-        if (rc == dccl::ncclSuccess) rc = export_ptr(out, s.h_out, &s.off_out, &s.serial_out, &s.base_out);
+        rc = export_ptr(in, s.h_in, &s.off_in, &s.serial_in, &s.base_in, &s.size_in);
+        if (rc == dccl::ncclSuccess)
+            rc = export_ptr(out, s.h_out, &s.off_out, &s.serial_out, &s.base_out, &s.size_out);
     } else {
         c->group->pub_in[r] = in;
         c->group->pub_out[r] = out;
@@ -398,9 +414,10 @@ ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Pe
             const ShmSlot& s = xport(c)->ctl->slot[p];
             unsigned char* pi = nullptr;
             unsigned char* po = nullptr;
-            rc = import_ptr(pc, p, s.pid, s.base_in, s.h_in, s.serial_in, s.off_in, &pi, &P->held);
+            rc = import_ptr(pc, p, s.pid, s.base_in, s.size_in, s.h_in, s.serial_in, s.off_in, &pi, &P->held);
             if (rc == dccl::ncclSuccess)
-                rc = import_ptr(pc, p, s.pid, s.base_out, s.h_out, s.serial_out, s.off_out, &po, &P->held);
+                rc = import_ptr(pc, p, s.pid, s.base_out, s.size_out, s.h_out, s.serial_out, s.off_out, &po,
+                                &P->held);
             if (rc != dccl::ncclSuccess) return rc;
             P->in[p] = pi;
             P->out[p] = po;
@@ -519,12 +536,13 @@ ncclResult_t ipc_leave(dcclComm* c) {
         // freed allocations they kept alive)
         ProcCache& pc = cache();
         std::lock_guard<std::mutex> lock(pc.mu);
-        if (pc.comms > 0 && --pc.comms == 0)
+        if (pc.comms > 0 && --pc.comms == 0) {
             for (auto it = pc.opened.begin(); it != pc.opened.end();) {
                 auto next = std::next(it);
                 if (it->second.users == 0) close_mapping(pc, it);
                 it = next;
             }
+        }
     }
     munmap(x->ctl, sizeof(ShmCtl));
     delete x;
