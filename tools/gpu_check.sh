@@ -20,7 +20,7 @@ timeout -k 10 600 python bench.py > "$out/bench.json" 2> "$out/bench.err"
 cat "$out/bench.json"
 if [[ "${PROF:-1}" != 0 ]]; then
   echo "== rocprof kernel trace"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --no-cpu --no-host-staged --no-other-layout --no-pmc --c5-gib 0 > "$out/prof.log" 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --no-cpu --no-host-staged --no-other-layout --no-pmc --no-configs --c5-gib 0 > "$out/prof.log" 2>&1
   echo "== pmc FETCH_SIZE"
   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc_fetch" -o fetch -- python3 tools/pmc_probe.py > "$out/pmc_fetch.log" 2>&1
   echo "== pmc WRITE_SIZE"
