@@ -123,15 +123,6 @@ bool ipc_debug() {
     return on;
 }
 
-// DCCL_IPC_CACHE=0: no peer mapping outlives the collective that opened it (read once per process)
-bool ipc_cache_off() {
-    static const bool off = [] {
-        const char* v = std::getenv("DCCL_IPC_CACHE");
-        return v != nullptr && *v == '0';
-    }();
-    return off;
-}
-
 // Sense-reversing barrier on the shared counters that also agrees on success: a rank arriving with
 // ok == false raises the segment's abort flag, and every rank returns ncclRemoteError from a barrier that
 // completes with the flag up.  The flag is sticky (the transport is unusable after a failed collective,
@@ -358,8 +349,7 @@ struct Peers {
         std::lock_guard<std::mutex> lock(pc.mu);
         for (const std::string& k : held) {
             auto it = pc.opened.find(k);
-            if (it != pc.opened.end() && it->second.users > 0 && --it->second.users == 0 && ipc_cache_off())
-                close_mapping(pc, it);
+            if (it != pc.opened.end() && it->second.users > 0) --it->second.users;
         }
     }
 };
