@@ -27,6 +27,8 @@ def main():
     p.add_argument("--grow", action="store_true")
     p.add_argument("--two", action="store_true")
     a = p.parse_args()
+    # a rank that fails leaves its peers at a barrier: let them give up well before a pool's silence limit
+    os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")
     ctx = mp.get_context("spawn")
     failed, reports = 0, []
     for run in range(a.runs):
@@ -39,7 +41,7 @@ def main():
             x.start()
         bad = []
         for _ in range(a.world):
-            r, res, err = q.get(timeout=300)
+            r, res, err = q.get(timeout=150)
             if err is not None:
                 bad.append((r, err))
             elif res[0] or res[1] != 0:
