@@ -325,6 +325,7 @@ def test_direct_in_process(gpu, monkeypatch, W, n, dt, op):
 
 def _ipc_rank(r, W, n, dt, op, tag, q):
     os.environ["DCCL_BOOTSTRAP_TAG"] = tag
+    os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")  # a failed peer ends the others' barriers early
     try:
         import torch
         import dccl_amd
@@ -381,6 +382,7 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=
     communicators of the same ranks, which share the process's peer mappings.  `hold`: nothing is freed, so
     every round's buffers are new allocations and the peer mappings pile up past the cache's bound."""
     os.environ["DCCL_BOOTSTRAP_TAG"] = tag
+    os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")
     try:
         import torch
         import dccl_amd
