@@ -505,6 +505,38 @@ def config_c4(dev, stream) -> list:
     return out
 
 
+def ring_step(dev, stream, sizes_mib=(512, 256, 128, 64, 32, 8)) -> dict:
+    """DCCL's own ring-step operand shape (reduce_scatter_ring.cpp:64-67, 84-94): `send` is the library's
+    scratchpad (one separate allocation, dccl.cpp:170-237) and `recv` is chunk k of the user's all-reduce
+    buffer, count/W elements.  Sizes are the chunks of a 1 GiB all-reduce at W = 2, 4, 8 (512, 256, 128 MiB)
+    and of a 256 MiB one (128, 64, 32 MiB), plus 8 MiB.  Below a 512 MiB working set the launches rotate
+    over `sets` scratch slots and user chunks (as in C4), so the Infinity Cache does not hold the operands.
+    Per size: eager (Python-issued, back-to-back) and graph-replayed time per combine and their fraction of
+    the HBM roofline (3 * bytes per combine).  Reporting only."""
+    user_bytes = 2 << 30
+    user = torch.empty(user_bytes, dtype=torch.uint8, device=dev)
+    synth_into(user.view(torch.float32), user_bytes // 4, 7, 0, 40)
+    points = []
+    for mib in sizes_mib:
+        nb = mib << 20
+        n = nb // 4
+        sets = 1 if 2 * nb >= (512 << 20) else max(2, -(-(512 << 20) // (2 * nb)))
+        scratch = torch.empty(sets * nb, dtype=torch.uint8, device=dev)  # the library's scratchpad
+        synth_into(scratch.view(torch.float32), sets * n, 7, 0, 41)
+        pairs = [(scratch.data_ptr() + j * nb, user.data_ptr() + ((2 * j + 1) * nb) % user_bytes) for j in range(sets)]
+        k = _time_pairs(pairs, n, stream, 5)
+        k = _time_pairs(pairs, n, stream, int(min(2000, max(10, 20.0 / max(k, 1e-4)))))
+        g = graph_us_per_launch(pairs, n, dev, per_graph=min(200, max(20, int(20e3 / max(k * 1e3, 1.0)))))
+        points.append({"mib": mib, "sets": sets, "eager_us": round(k * 1e3, 1),
+                       "eager_frac": round(3 * nb / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                       "graph_us": round(g, 1), "graph_frac": round(3 * nb / (g * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)})
+        del scratch
+    del user
+    torch.cuda.empty_cache()
+    return {"shape": "send = separately allocated scratchpad slot, recv = chunk of a 2 GiB user buffer, fp32 Sum",
+            "points": points}
+
+
 def native_c4(max_log2: int = 26) -> dict:
     """C4 up to 2^max_log2 bytes per operand issued from a C++ loop (dccl_amd/bin/c4_native, the same rotation
     over operand sets): the eager per-launch time a native caller such as DCCL's ring step loop sees, without
@@ -600,6 +632,29 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
             torch.cuda.synchronize(dev)
             t = (time.perf_counter() - t0) / iters
             res.update({"ms": round(t * 1e3, 3), "busbw_gb_s": round(2 * (world - 1) / world * count * 4 / t / 1e9, 1)})
+            if name == "direct":
+                # the same all_reduce with the buffer registered (dcclRegisterCacheMemory): peers read it in
+                # place instead of through the communicator's scratch copy
+                dccl_amd.check(comm.register(yf.data_ptr(), count * 4), "register")
+                yr, zr = xf.clone(), xf.clone()
+                dccl_amd.check(comm.register(yr.data_ptr(), count * 4), "register")
+                torch.cuda.synchronize(dev)
+                dccl_amd.check(comm.all_reduce(yr.data_ptr(), yr.data_ptr(), count, 7, 0, st.cuda_stream), name)
+                dccl_amd.check(comm.all_reduce(zr.data_ptr(), zr.data_ptr(), count, 7, 0, st.cuda_stream), name)
+                torch.cuda.synchronize(dev)
+                res["registered_fp32_bit_exact_vs_scratch"] = bool(torch.equal(
+                    zr.view(torch.int32), yr.view(torch.int32)))
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    dccl_amd.check(comm.all_reduce(yf.data_ptr(), yf.data_ptr(), count, 7, 0, st.cuda_stream), name)
+                torch.cuda.synchronize(dev)
+                t = (time.perf_counter() - t0) / iters
+                res["registered_ms"] = round(t * 1e3, 3)
+                res["registered_busbw_gb_s"] = round(2 * (world - 1) / world * count * 4 / t / 1e9, 1)
+                for buf in (yf, yr):
+                    dccl_amd.check(comm.deregister(buf.data_ptr()), "deregister")
+                del yr, zr
             res.update(root_ops(comm, world, rank, dev, st, xi, ri, iters))
             out[name] = res
             yf_by[name] = yf
@@ -633,6 +688,10 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
     finally:
         for comm in comms.values():
             comm.finalize()
+    if "direct" in comms:  # the IPC transport's counters, summed over the ranks (alias_errors must be 0)
+        every = [None] * world
+        dist.all_gather_object(every, dccl_amd.ipc_stats())
+        out["ipc_stats"] = {k: sum(d[k] for d in every) for k in every[0]}
     return out
 
 
@@ -692,7 +751,10 @@ def allgather_compare(comms: dict, world: int, rank: int, dev, st, count: int, i
             if bool(d.any()):
                 lines = d[:per // 32 * 32].view(-1, 32).any(dim=1)
                 wrong[p] = {"elems": round(float(d.float().mean()), 6), "lines": round(float(lines.float().mean()), 6)}
-        ok = not wrong
+        # every rank checked its own copy: agree on the result and count the wrong slices over all ranks
+        nwrong = torch.tensor([len(wrong)], dtype=torch.int64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(nwrong)
+        ok = int(nwrong[0]) == 0
         dist.barrier()
         each = []
         t0 = time.perf_counter()
@@ -702,8 +764,8 @@ def allgather_compare(comms: dict, world: int, rank: int, dev, st, count: int, i
             torch.cuda.synchronize(dev)
             each.append((time.perf_counter() - t1) * 1e3)
         t = (time.perf_counter() - t0) / iters
-        res[name] = {"bit_exact": ok, "ms": round(t * 1e3, 3), "ms_each": [round(x, 3) for x in each],
-                     "busbw_gb_s": round((world - 1) * per * 4 / t / 1e9, 1)}
+        res[name] = {"bit_exact": ok, "wrong_slices_all_ranks": int(nwrong[0]), "ms": round(t * 1e3, 3),
+                     "ms_each": [round(x, 3) for x in each], "busbw_gb_s": round((world - 1) * per * 4 / t / 1e9, 1)}
         if wrong:
             res[name]["wrong_slices"] = wrong
     if dist.get_backend() == "nccl":
@@ -954,15 +1016,21 @@ def allreduce_summary(ar) -> dict:
     for name in ("ring", "direct"):
         if isinstance(ar.get(name), dict):
             out[name] = {k: ar[name][k] for k in ("int32_sum_bit_exact_vs_rccl", "fp32_within_bound", "ms",
-                                                  "busbw_gb_s", "broadcast_bit_exact", "broadcast_ms",
-                                                  "reduce_bit_exact", "reduce_ms") if k in ar[name]}
+                                                  "busbw_gb_s", "registered_ms", "registered_busbw_gb_s",
+                                                  "registered_fp32_bit_exact_vs_scratch", "broadcast_bit_exact",
+                                                  "broadcast_ms", "reduce_bit_exact", "reduce_ms") if k in ar[name]}
     if isinstance(ar.get("rccl_allreduce"), dict):
         out["rccl"] = {k: ar["rccl_allreduce"][k] for k in ("ms", "busbw_gb_s")}
     for key in ("dccl_allgather", "c5_allgather"):
         ag = ar.get(key)
         if isinstance(ag, dict):
-            out[key] = {name: {k: v[k] for k in ("bit_exact", "ms", "busbw_gb_s", "wrong_slices") if k in v}
+            out[key] = {name: {k: v[k] for k in ("bit_exact", "wrong_slices_all_ranks", "ms", "busbw_gb_s",
+                                                 "wrong_slices") if k in v}
                         for name, v in ag.items() if isinstance(v, dict)}
+    if isinstance(ar.get("ipc_stats"), dict):
+        out["ipc_stats"] = {k: ar["ipc_stats"][k] for k in (
+            "alias_errors", "alias_evictions", "mappings_retired", "retire_log_overflows", "open_retries",
+            "size_mismatches", "scratch_copies", "registered_hits", "exports_made") if k in ar["ipc_stats"]}
     return out
 
 
@@ -1127,6 +1195,8 @@ def run_rank(a):
             res["c4"] = config_c4(dev, stream)
             progress("C3: ops x dtypes at 1 GiB")
             res["c3"] = config_c3(dev, stream)
+            progress("ring step: scratchpad + user chunk, 512 MiB - 8 MiB")
+            extra["ring_step"] = ring_step(dev, stream)
         if world == 1 and not a.no_host_staged:
             res["host_staged"] = host_staged_rate(nbytes, dt, op)
         if "allgather" in extra:
@@ -1142,7 +1212,7 @@ def run_rank(a):
         if world == 1 and not a.no_cpu:
             progress("CPU baseline")
             res["cpu_baseline"] = cpu_baseline(a.cpu_seconds, nbytes)
-        for key in ("other_layout", "c5"):
+        for key in ("other_layout", "ring_step", "c5"):
             if key in extra:
                 res[key] = extra[key]
         if "dccl_allreduce" in extra:

@@ -115,6 +115,9 @@ def _load():
         "dccl_rccl_available": (c_int, []),
         "dccl_bootstrap_unique_id": (c_int, [ctypes.c_uint32, ctypes.c_uint32, c_void_p]),
         "dccl_bootstrap_done": (c_int, [ctypes.c_uint32, ctypes.c_uint32]),
+        "dccl_comm_register": (c_int, [c_void_p, c_void_p, c_size_t]),
+        "dccl_comm_deregister": (c_int, [c_void_p, c_void_p]),
+        "dccl_ipc_stats": (c_int, [ctypes.POINTER(ctypes.c_uint64), c_int]),
         "dccl_synth_fill": (c_int, [c_void_p, c_int, c_size_t, c_int, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),
         "dccl_synth_fill_range": (c_int, [c_void_p, c_int, c_size_t, c_int, ctypes.c_uint64, ctypes.c_uint64,
                                           c_size_t, c_void_p]),
@@ -137,8 +140,24 @@ EXPORTED_SYMBOLS = [
     "dccl_reduce_scatter", "dccl_all_gather", "dccl_rccl_available", "dccl_bootstrap_unique_id",
     "dccl_synth_fill", "dccl_synth_fill_range", "dccl_local_reduce_chain", "dccl_copy_multi",
     "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_local_reduce_chain_host", "dccl_comm_init_p2p",
-    "dccl_bootstrap_done",
+    "dccl_bootstrap_done", "dccl_comm_register", "dccl_comm_deregister", "dccl_ipc_stats",
 ]
+
+#: names of the dccl_ipc_stats counters, in order (include/dccl/dccl_comm.h)
+IPC_STAT_NAMES = [
+    "exports_made", "exports_retired", "registered_hits", "scratch_copies", "scratch_bytes", "scratch_grows",
+    "stale_registrations", "mappings_opened", "mappings_reused", "mappings_retired", "retire_log_overflows",
+    "mappings_trimmed", "alias_evictions", "alias_errors", "open_retries", "size_mismatches", "mappings_open",
+    "bytes_mapped",
+]
+
+
+def ipc_stats() -> dict:
+    """This process's IPC transport counters (dccl_ipc_stats) by name."""
+    buf = (ctypes.c_uint64 * len(IPC_STAT_NAMES))()
+    n = int(lib.dccl_ipc_stats(buf, len(IPC_STAT_NAMES)))
+    assert n == len(IPC_STAT_NAMES), (n, len(IPC_STAT_NAMES))
+    return dict(zip(IPC_STAT_NAMES, (int(v) for v in buf)))
 
 
 def result_string(code: int) -> str:
@@ -277,6 +296,14 @@ class Comm:
 
     def broadcast(self, send: int, recv: int, count: int, dtype: int, root: int, stream: int = 0) -> int:
         return int(lib.dccl_broadcast(send, recv, count, dtype, root, self.handle, stream or None))
+
+    def register(self, ptr: int, size: int) -> int:
+        """dcclRegisterCacheMemory: on an IPC communicator, peers then read device memory in
+        [ptr, ptr + size) in place until deregister(ptr); 64-byte aligned address and size."""
+        return int(lib.dccl_comm_register(self.handle, ptr, size))
+
+    def deregister(self, ptr: int) -> int:
+        return int(lib.dccl_comm_deregister(self.handle, ptr))
 
     def finalize(self) -> int:
         h, self.handle = self.handle, None

@@ -29,7 +29,8 @@ std::mutex g_mu;
 std::map<std::string, unsigned long long> g_published;  // path -> generations published by this process
 std::map<std::string, Stamp> g_consumed;                 // path#reader -> last stamp consumed
 
-// Start time of process `pid` in clock ticks since boot (/proc/<pid>/stat field 22), 0 if it is gone.
+}  // namespace
+
 unsigned long long proc_start_time(long pid) {
     std::ifstream f("/proc/" + std::to_string(pid) + "/stat");
     std::string line;
@@ -44,6 +45,8 @@ unsigned long long proc_start_time(long pid) {
     }
     return 0;
 }
+
+namespace {
 
 std::string to_hex(const std::string& s) {
     static const char* d = "0123456789abcdef";

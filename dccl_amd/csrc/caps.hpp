@@ -128,7 +128,7 @@ constexpr bool phased_loads_first(bool chain, int k) {
 
 // Pairwise launches: capped only when send and recv lie in two allocations of at least kSeparateCapBytes
 // each on the current device (DCCL's scratchpad + user chunk).  Paired A/B of the same pairs under every
-// cap (tools/separate_cap_paired.py, 6-8 separate pairs per run, profiles/r2_s61_separate_cap_*.json,
+// cap (separate_cap_paired.py@4f20423, 6-8 separate pairs per run, profiles/r2_s61_separate_cap_*.json,
 // r2_s66_separate_cap_shift*.json), median pair against uncapped: aligned at 22 resident waves +0.6 to
 // +1.0 points at 1 GiB (six runs, three boxes), -0.8 at 256 MiB; shifted at 26 +1.0 to +1.25 (four runs);
 // one-allocation pairs lose 0.4-1.1 under any cap and stay uncapped.  The LDS bytes are the values measured.

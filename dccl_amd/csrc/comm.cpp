@@ -24,7 +24,7 @@ Group::Group(uint32_t world)
 
 // Ranks of a collective arrive within microseconds of each other: poll the generation for up to 2 ms
 // (with the pause hint) before blocking on the condition variable, whose wake-up costs tens of
-// microseconds on the critical path of every direct collective (tools/ipc_latency.py).
+// microseconds on the critical path of every direct collective (ipc_latency.py@4f20423).
 bool Group::barrier(bool ok) {
     std::unique_lock<std::mutex> lk(bmu_);
     const uint64_t gen = barrier_gen_.load(std::memory_order_relaxed);

@@ -383,7 +383,7 @@ ncclResult_t dcclRegisterCacheMemory(ncclComm_t comm, void* buffer, size_t size)
     validate_comm(comm, __func__);
     if (buffer == nullptr || reinterpret_cast<uintptr_t>(buffer) % kCachelineSize || size % kCachelineSize)
         return ncclInvalidArgument;  // dccl.cpp:506-514
-    if (is_device_ptr(buffer)) return ncclSuccess;
+    if (is_device_ptr(buffer)) return comm->ipc != nullptr ? ipc_register(buffer, size) : ncclSuccess;
     if (hipHostRegister(buffer, size, hipHostRegisterDefault) != hipSuccess) {
         (void)hipGetLastError();  // already registered / pinned: nothing to do
     }
@@ -393,7 +393,8 @@ ncclResult_t dcclRegisterCacheMemory(ncclComm_t comm, void* buffer, size_t size)
 ncclResult_t dcclDeregisterCacheMemory(ncclComm_t comm, void* buffer, size_t) {
     validate_comm(comm, __func__);
     if (buffer == nullptr) return ncclInvalidArgument;
-    if (!is_device_ptr(buffer) && hipHostUnregister(buffer) != hipSuccess) (void)hipGetLastError();
+    if (is_device_ptr(buffer)) return comm->ipc != nullptr ? ipc_deregister(buffer) : ncclSuccess;
+    if (hipHostUnregister(buffer) != hipSuccess) (void)hipGetLastError();
     return ncclSuccess;
 }
 
@@ -693,6 +694,19 @@ extern "C" int dccl_broadcast(const void* send, void* recv, size_t count, int dt
 }
 
 extern "C" int dccl_rccl_available(void) { return rccl_available(); }
+
+extern "C" int dccl_comm_register(void* comm, void* buffer, size_t size) {
+    return guarded([&] { return dccl::dcclRegisterCacheMemory(static_cast<dccl::ncclComm_t>(comm), buffer, size); });
+}
+
+extern "C" int dccl_comm_deregister(void* comm, void* buffer) {
+    return guarded([&] { return dccl::dcclDeregisterCacheMemory(static_cast<dccl::ncclComm_t>(comm), buffer, 0); });
+}
+
+extern "C" int dccl_ipc_stats(uint64_t* out, int n) {
+    if (out == nullptr && n > 0) return -1;
+    return ipc_stats(out, n);
+}
 
 extern "C" int dccl_bootstrap_unique_id(uint32_t rank, uint32_t world, void* id128) {
     if (id128 == nullptr || world == 0 || rank >= world) return DCCL_INVALID_ARGUMENT;

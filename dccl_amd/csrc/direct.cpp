@@ -2,17 +2,18 @@
 #include "direct.hpp"
 
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <deque>
 #include <iterator>
 #include <map>
 #include <mutex>
@@ -24,29 +25,45 @@
 #include "bootstrap.hpp"
 #include "dccl/dccl_reduce.h"
 #include "dispatch.hpp"
+#include "ipc_cache.hpp"
 
 namespace dccl_amd {
 namespace {
 
 using dccl::dcclComm;
 
-constexpr uint64_t kMagic = 0x3143504943434344ull;  // "DCCIPC1"
+constexpr uint64_t kMagic = 0x3243504943434344ull;  // "DCCIPC2"
 constexpr uint32_t kMaxRanks = 64;
-constexpr size_t kHandleBytes = sizeof(hipIpcMemHandle_t);
-// Peer mappings are kept for later calls, in one cache per process (below); the oldest unused one is
-// closed beyond this many, or beyond this many bytes of peer memory: a mapping keeps the peer's allocation
-// alive after the peer freed it, so the cache must not hold more than a bounded amount of it.
+constexpr size_t kHandleBytes = ipc::kHandleBytes;
+static_assert(sizeof(hipIpcMemHandle_t) == kHandleBytes, "HIP IPC handle size");
+// Peer mappings kept for later calls (one cache per process, ipc_cache.hpp): the oldest unused one is
+// closed beyond this many, or beyond this many bytes of peer memory (a mapping keeps the peer's pages alive).
 constexpr size_t kMaxOpenMappings = 256;
 constexpr size_t kMaxOpenBytes = size_t(64) << 30;
+// Exports this rank ended and its peers have not necessarily seen yet (see ShmSlot::retired).
+constexpr uint32_t kRetireRing = 256;
+// The communicator's scratch (unregistered inputs are copied there for the peers to read): at least the
+// reference's initial scratchpad (SCRATCHPAD_INI_SIZE, /root/reference/src/core/dccl.cpp:57), in 2 MiB
+// pages, grown by at least half when it grows.
+constexpr size_t kScratchMin = size_t(64) << 20;
+constexpr size_t kScratchPage = size_t(2) << 20;
+
+// One published buffer: the export holding it (serial 0: nothing published) and the offset in it.
+struct Desc {
+    unsigned char handle[kHandleBytes];
+    uint64_t serial, off, size;  // size: of the exported allocation
+};
 
 struct ShmSlot {
-    unsigned char h_in[kHandleBytes];
-    unsigned char h_out[kHandleBytes];
-    uint64_t off_in, off_out;
-    uint64_t serial_in, serial_out;  // the exporter's serial of each handle (see Export)
-    uint64_t base_in, base_out;      // the exported allocations' base addresses in the exporter
-    uint64_t size_in, size_out;      // and their sizes
-    int64_t pid;                     // the exporter
+    Desc in, out;
+    int64_t pid;     // this rank's process and its start time (bootstrap.hpp), for the barrier's liveness check
+    uint64_t start;
+    // Exports this rank's process ended (deregistered, replaced scratch, freed allocations): serials in a
+    // ring, retired_n written last.  Every peer closes their mappings before it opens anything new.
+    std::atomic<uint64_t> retired_n;
+    uint64_t retired[kRetireRing];
+    // acked[p]: how many of rank p's retirements this rank has applied (its mappings of them are closed)
+    std::atomic<uint64_t> acked[kMaxRanks];
 };
 
 struct ShmCtl {
@@ -59,46 +76,80 @@ struct ShmCtl {
     ShmSlot slot[kMaxRanks];
 };
 
-// One export per allocation.  `serial` numbers this process's exports: the handle bytes of a new allocation
-// at a freed one's address and size repeat (observed on ROCm 7.2), so importers tell a new
-// allocation from the freed one by the serial, not by the bytes.
+// An allocation of this process that peers may map: a registered user allocation or a scratch buffer.
+// `serial` numbers this process's exports and is never reused, whatever the runtime's handle bytes do.
 struct Export {
     size_t size;
     uint64_t buffer_id;
     uint64_t serial;
-    hipIpcMemHandle_t handle;
+    ipc::Handle handle;
+    uint32_t regs;  // registered ranges on it (0 for a scratch buffer)
 };
 
-struct Mapping {
-    void* base;
-    uint64_t serial;
-    size_t bytes;
-    uint32_t users;      // collectives of this process between their import and their last phase point
-    uint64_t import_id;  // the runtime's buffer id of this import (0: unknown)
+// A range registered with dcclRegisterCacheMemory, and the allocation (export) holding it.
+struct Range {
+    size_t len;
+    uintptr_t base;
 };
 
-uint64_t buffer_id_of(void* p) {
+struct IpcXport {
+    ShmCtl* ctl = nullptr;
+    uint32_t rank = 0, world = 0;
+    double timeout_s = 60.0;
+    // scratch: inputs that are not registered are copied here (one allocation, exported once)
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    std::vector<void*> old_scratch;  // replaced buffers, freed at this rank's next collective
+    std::vector<uint64_t> seen;      // retirements of each peer already applied
+};
+
+uint64_t buffer_id_of(const void* p) {
     uint64_t id = 0;
-    if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, reinterpret_cast<hipDeviceptr_t>(p)) !=
-        hipSuccess) {
+    if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
+                               reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) != hipSuccess) {
         (void)hipGetLastError();
         return 0;
     }
     return id;
 }
 
-// Exports and peer mappings are per PROCESS, shared by every IPC communicator in it: the runtime hands out
-// one import per handle per process (opening handle bytes that are already open returns that mapping), so
-// a cache per communicator could not replace a stale mapping another communicator still holds.  Mappings
-// are keyed by the exporting process and the allocation's address there, for every peer of every communicator.
+struct HipOps final : ipc::Ops {
+    bool open(const ipc::Handle& h, void** mapped) override {
+        hipIpcMemHandle_t hh;
+        std::memcpy(&hh, h.b, kHandleBytes);
+        if (hipIpcOpenMemHandle(mapped, hh, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return true;
+    }
+    void close(void* mapped) override {
+        if (hipIpcCloseMemHandle(mapped) != hipSuccess) (void)hipGetLastError();
+    }
+    size_t size_of(void* mapped) override {
+        hipDeviceptr_t b = nullptr;
+        size_t s = 0;
+        if (hipMemGetAddressRange(&b, &s, mapped) != hipSuccess) {
+            (void)hipGetLastError();
+            return 0;
+        }
+        return s;
+    }
+};
+
+// Exports, registrations and peer mappings are per PROCESS, shared by its IPC communicators: the runtime
+// hands out one import per handle per process, so one communicator's stale mapping would shadow another's.
 struct ProcCache {
     std::mutex mu;
     uint64_t next_serial = 1;
-    std::map<uintptr_t, Export> exported;  // allocation base -> its export
-    std::map<std::string, Mapping> opened;  // (exporter pid, allocation base) -> mapping
-    std::deque<std::string> open_order;     // oldest first
-    size_t open_bytes = 0;
-    uint32_t comms = 0;                     // live IPC communicators of this process
+    std::map<uintptr_t, Export> exports;  // allocation base -> export
+    std::map<uintptr_t, Range> ranges;    // registered range start -> range
+    HipOps ops;
+    ipc::ImportCache imports{&ops, kMaxOpenMappings, kMaxOpenBytes};
+    std::vector<IpcXport*> xports;  // live IPC communicators of this process
+    // exporter-side counters (dccl_ipc_stats)
+    uint64_t exports_made = 0, retirements = 0, registered_hits = 0, scratch_copies = 0, scratch_bytes = 0,
+             scratch_grows = 0, stale_registrations = 0;
 };
 
 ProcCache& cache() {
@@ -106,15 +157,9 @@ ProcCache& cache() {
     return *c;
 }
 
-struct IpcXport {
-    ShmCtl* ctl = nullptr;
-    double timeout_s = 300.0;
-};
-
 IpcXport* xport(const dcclComm* c) { return static_cast<IpcXport*>(c->ipc); }
 
-// DCCL_IPC_DEBUG=1: one line on stderr per export made and per peer mapping opened, reused or replaced
-// (read once per process)
+// DCCL_IPC_DEBUG=1: one line on stderr per export made or retired (read once per process)
 bool ipc_debug() {
     static const bool on = [] {
         const char* v = std::getenv("DCCL_IPC_DEBUG");
@@ -123,11 +168,46 @@ bool ipc_debug() {
     return on;
 }
 
+// False once peer p's process is gone (or its pid names another process now).
+// DCCL_IPC_LIVENESS=0 turns the check off (ranks in different pid namespaces cannot see each other's pids).
+bool peer_alive(const ShmSlot& s) {
+    static const bool check = [] {
+        const char* v = std::getenv("DCCL_IPC_LIVENESS");
+        return v == nullptr || *v != '0';
+    }();
+    if (!check || s.pid <= 0) return true;  // not joined yet
+    if (::kill(static_cast<pid_t>(s.pid), 0) != 0 && errno == ESRCH) return false;
+    return proc_start_time(static_cast<long>(s.pid)) == s.start;
+}
+
+// Apply every retirement the peers of every IPC communicator of this process wrote since the last call.
+void apply_retirements(ProcCache& pc) {
+    for (IpcXport* x : pc.xports) {
+        for (uint32_t p = 0; p < x->world; ++p) {
+            if (p == x->rank) continue;
+            const ShmSlot& s = x->ctl->slot[p];
+            const uint64_t n = s.retired_n.load(std::memory_order_acquire);
+            uint64_t& seen = x->seen[p];
+            if (n == seen) continue;
+            if (n - seen > kRetireRing) {
+                pc.imports.retire_pid(s.pid);
+            } else {
+                for (uint64_t i = seen; i < n; ++i) pc.imports.retire(s.pid, s.retired[i % kRetireRing]);
+                // the writer may have lapped the ring while it was read
+                if (s.retired_n.load(std::memory_order_acquire) - seen > kRetireRing) pc.imports.retire_pid(s.pid);
+            }
+            seen = n;
+            x->ctl->slot[x->rank].acked[p].store(n, std::memory_order_release);
+        }
+    }
+}
+
 // Sense-reversing barrier on the shared counters that also agrees on success: a rank arriving with
 // ok == false raises the segment's abort flag, and every rank returns ncclRemoteError from a barrier that
 // completes with the flag up.  The flag is sticky (the transport is unusable after a failed collective,
-// like an aborted NCCL communicator).  Every waiter gives up (and tells the others) after timeout_s, so
-// a dead peer turns into an error instead of a hang.
+// like an aborted NCCL communicator).  A waiter checks every ~100 ms that its peers' processes still
+// exist, so a peer that died (a runtime abort, a kill) ends every other rank's wait with ncclRemoteError
+// at once; a live peer that never arrives ends it after timeout_s (DCCL_IPC_TIMEOUT_S, default 60 s).
 ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
     ShmCtl* s = x->ctl;
     if (!ok) s->abort.store(1, std::memory_order_relaxed);
@@ -139,10 +219,12 @@ ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
     }
     // Spin (with the pause hint) for up to kSpin before sleeping: peers arrive within microseconds of
     // each other in a collective, and a 20 us sleep costs 50-80 us once the kernel's timer slack is
-    // added, which set the latency of small collectives (tools/ipc_latency.py).
+    // added, which set the latency of small collectives.
     constexpr auto kSpin = std::chrono::milliseconds(2);
+    constexpr auto kLiveness = std::chrono::milliseconds(100);
     const auto start = std::chrono::steady_clock::now();
     const auto deadline = start + std::chrono::duration<double>(x->timeout_s);
+    auto next_check = start + kLiveness;
     for (uint64_t i = 0; s->gen.load(std::memory_order_acquire) == g; ++i) {
         if (s->abort.load(std::memory_order_relaxed)) return dccl::ncclRemoteError;
         if ((i & 1023) != 1023) {
@@ -154,192 +236,147 @@ ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
             s->abort.store(1, std::memory_order_relaxed);
             return dccl::ncclSystemError;
         }
+        if (now > next_check) {
+            next_check = now + kLiveness;
+            // close the mappings of exports the peers retired meanwhile: a peer may be waiting for that
+            // (ipc_deregister) before its process frees the memory
+            ProcCache& pc = cache();
+            if (pc.mu.try_lock()) {
+                apply_retirements(pc);
+                pc.mu.unlock();
+            }
+            for (uint32_t p = 0; p < s->world; ++p)
+                if (p != x->rank && !peer_alive(s->slot[p])) {
+                    if (ipc_debug()) std::fprintf(stderr, "[dccl ipc %d] rank %u's process is gone\n", ::getpid(), p);
+                    s->abort.store(1, std::memory_order_relaxed);
+                    return dccl::ncclRemoteError;
+                }
+        }
         if (now - start > kSpin) std::this_thread::sleep_for(std::chrono::microseconds(20));
         else std::this_thread::yield();  // a peer without a core of its own gets one
     }
     return s->abort.load(std::memory_order_relaxed) ? dccl::ncclRemoteError : dccl::ncclSuccess;
 }
 
-ncclResult_t export_ptr(const void* p, unsigned char* handle_out, uint64_t* off_out, uint64_t* serial_out,
-                        uint64_t* base_out, uint64_t* size_out) {
+// --- exporter side (caller holds pc.mu) ---------------------------------------------------------------
+
+// Tell every peer of every IPC communicator of this process that export `serial` ended.
+void write_retirement(ProcCache& pc, uint64_t serial) {
+    ++pc.retirements;
+    for (IpcXport* x : pc.xports) {
+        ShmSlot& s = x->ctl->slot[x->rank];
+        const uint64_t n = s.retired_n.load(std::memory_order_relaxed);
+        s.retired[n % kRetireRing] = serial;
+        s.retired_n.store(n + 1, std::memory_order_release);
+    }
+    if (ipc_debug()) std::fprintf(stderr, "[dccl ipc %d] retired serial %llu\n", ::getpid(), (unsigned long long)serial);
+}
+
+void drop_export(ProcCache& pc, std::map<uintptr_t, Export>::iterator it) {
+    write_retirement(pc, it->second.serial);
+    for (auto r = pc.ranges.begin(); r != pc.ranges.end();)
+        r = r->second.base == it->first ? pc.ranges.erase(r) : std::next(r);
+    pc.exports.erase(it);
+}
+
+// Export the allocation [base, base + size) with buffer id `id`; exports whose range it overlaps name
+// freed allocations and are retired.
+ncclResult_t make_export(ProcCache& pc, uintptr_t base, size_t size, uint64_t id, uint32_t regs) {
+    for (auto o = pc.exports.lower_bound(base); o != pc.exports.begin();) {
+        --o;
+        if (o->first + o->second.size <= base) break;
+        drop_export(pc, o);
+        o = pc.exports.lower_bound(base);
+    }
+    for (auto o = pc.exports.lower_bound(base); o != pc.exports.end() && o->first < base + size;
+         o = pc.exports.lower_bound(base))
+        drop_export(pc, o);
+    Export e{size, id, pc.next_serial++, {}, regs};
+    hipIpcMemHandle_t h;
+    // exporting an allocation at the address of a freed one that a peer still maps can fail for a moment
+    for (int attempt = 0, us = 100;; ++attempt, us = std::min(2 * us, 100000)) {
+        if (hipIpcGetMemHandle(&h, reinterpret_cast<void*>(base)) == hipSuccess) break;
+        (void)hipGetLastError();
+        if (attempt == 14) return dccl::ncclUnhandledCudaError;
+        std::this_thread::sleep_for(std::chrono::microseconds(us));
+    }
+    std::memcpy(e.handle.b, &h, kHandleBytes);
+    pc.exports.emplace(base, e);
+    ++pc.exports_made;
+    if (ipc_debug())
+        std::fprintf(stderr, "[dccl ipc %d] export base=%#zx size=%zu buffer_id=%llu serial=%llu\n", ::getpid(),
+                     size_t(base), size, (unsigned long long)id, (unsigned long long)e.serial);
+    return dccl::ncclSuccess;
+}
+
+// The registered export holding [p, p + bytes), or exports.end().  A registration whose allocation was
+// freed (its base now holds another buffer id) is dropped (retired) rather than trusted.
+std::map<uintptr_t, Export>::iterator find_registered(ProcCache& pc, const void* p, size_t bytes) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    auto r = pc.ranges.upper_bound(a);
+    if (r == pc.ranges.begin()) return pc.exports.end();
+    --r;
+    if (a + bytes > r->first + r->second.len) return pc.exports.end();
+    auto e = pc.exports.find(r->second.base);
+    if (e == pc.exports.end()) return e;
+    if (buffer_id_of(reinterpret_cast<void*>(e->first)) != e->second.buffer_id) {
+        ++pc.stale_registrations;
+        drop_export(pc, e);
+        return pc.exports.end();
+    }
+    ++pc.registered_hits;
+    return e;
+}
+
+void describe(const Export& e, uintptr_t base, const void* p, Desc* d) {
+    std::memcpy(d->handle, e.handle.b, kHandleBytes);
+    d->serial = e.serial;
+    d->off = reinterpret_cast<uintptr_t>(p) - base;
+    d->size = e.size;
+}
+
+// Make the communicator's scratch hold at least `bytes`.  A replaced buffer is retired now and freed at
+// this rank's next collective, after every peer passed this collective's exchange (and closed it).
+ncclResult_t ensure_ipc_scratch(ProcCache& pc, IpcXport* x, size_t bytes) {
+    if (bytes <= x->scratch_bytes) return dccl::ncclSuccess;
+    size_t want = std::max({bytes, x->scratch_bytes + x->scratch_bytes / 2, kScratchMin});
+    want = (want + kScratchPage - 1) / kScratchPage * kScratchPage;
+    void* p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        return dccl::ncclUnhandledCudaError;
+    }
     hipDeviceptr_t base = nullptr;
     size_t size = 0;
-    if (const hipError_t e = hipMemGetAddressRange(&base, &size, const_cast<void*>(p)); e != hipSuccess) {
+    if (hipMemGetAddressRange(&base, &size, p) != hipSuccess || base != p) {  // the export is keyed by its base
         (void)hipGetLastError();
-        if (ipc_debug()) std::fprintf(stderr, "[dccl ipc %d] hipMemGetAddressRange(%p) -> %d\n", ::getpid(), p, int(e));
-        return dccl::ncclInvalidArgument;  // not a device allocation of this process
+        (void)hipFree(p);
+        return dccl::ncclUnhandledCudaError;
     }
-    uint64_t id = 0;
-    const bool have_id = hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
-                                                reinterpret_cast<hipDeviceptr_t>(base)) == hipSuccess;
-    if (!have_id) {
-        (void)hipGetLastError();
-        if (ipc_debug()) std::fprintf(stderr, "[dccl ipc %d] no buffer id for %p: exported afresh\n", ::getpid(), base);
+    const ncclResult_t rc = make_export(pc, reinterpret_cast<uintptr_t>(base), size, buffer_id_of(base), 0);
+    if (rc != dccl::ncclSuccess) {
+        (void)hipFree(p);
+        return rc;
     }
-    const uintptr_t b = reinterpret_cast<uintptr_t>(base);
-    ProcCache& pc = cache();
-    std::lock_guard<std::mutex> lock(pc.mu);
-    auto it = pc.exported.find(b);
-    // without the allocation's buffer id the cached export cannot be told from a freed allocation's at the
-    // same address and size: export again (a new serial makes the peers re-map)
-    if (!have_id || it == pc.exported.end() || it->second.size != size || it->second.buffer_id != id) {
-        Export e{size, id, pc.next_serial++, {}};
-        // Exporting an allocation at the address of a freed one that a peer still maps can fail for a moment
-        // (hipErrorInvalidValue; seen about once in 600 re-allocations in tests/test_direct.py::
-        // test_ipc_reallocated_buffers); retry with backoff for ~0.5 s, like the re-open in import_ptr.
-        for (int attempt = 0, us = 100;; ++attempt, us = std::min(2 * us, 100000)) {
-            const hipError_t he = hipIpcGetMemHandle(&e.handle, base);
-            if (he == hipSuccess) break;
-            (void)hipGetLastError();
-            if (ipc_debug())
-                std::fprintf(stderr, "[dccl ipc %d] hipIpcGetMemHandle(base=%p size=%zu buffer_id=%llu) -> %d "
-                             "(attempt %d)\n", ::getpid(), base, size, static_cast<unsigned long long>(id), int(he),
-                             attempt);
-            if (attempt == 14) return dccl::ncclUnhandledCudaError;
-            std::this_thread::sleep_for(std::chrono::microseconds(us));
-        }
-        // entries whose range this allocation now covers name freed allocations: drop them, so the map
-        // holds one entry per address range in use rather than one per allocation ever exported
-        for (auto o = pc.exported.lower_bound(b); o != pc.exported.begin();) {
-            --o;
-            if (o->first + o->second.size <= b) break;
-            o = pc.exported.erase(o);
-        }
-        for (auto o = pc.exported.lower_bound(b); o != pc.exported.end() && o->first < b + size;)
-            o = pc.exported.erase(o);
-        it = pc.exported.emplace(b, e).first;
-        if (ipc_debug())
-            std::fprintf(stderr, "[dccl ipc %d] export base=%p size=%zu buffer_id=%llu serial=%llu\n", ::getpid(),
-                         base, size, static_cast<unsigned long long>(id), static_cast<unsigned long long>(e.serial));
+    if (x->scratch != nullptr) {
+        auto old = pc.exports.find(reinterpret_cast<uintptr_t>(x->scratch));
+        if (old != pc.exports.end()) drop_export(pc, old);
+        x->old_scratch.push_back(x->scratch);
     }
-    std::memcpy(handle_out, &it->second.handle, kHandleBytes);
-    *off_out = reinterpret_cast<uintptr_t>(p) - b;
-    *serial_out = it->second.serial;
-    *base_out = b;
-    *size_out = it->second.size;
+    x->scratch = p;
+    x->scratch_bytes = want;
+    ++pc.scratch_grows;
     return dccl::ncclSuccess;
 }
 
-void close_mapping(ProcCache& pc, std::map<std::string, Mapping>::iterator it) {
-    (void)hipIpcCloseMemHandle(it->second.base);
-    pc.open_bytes -= it->second.bytes;
-    const std::string key = it->first;
-    pc.opened.erase(it);
-    for (auto o = pc.open_order.begin(); o != pc.open_order.end(); ++o)
-        if (*o == key) {
-            pc.open_order.erase(o);
-            break;
-        }
-}
-
-// Close the oldest unused mappings so that this call's imports fit under kMaxOpenMappings and the
-// mappings kept from earlier calls under kMaxOpenBytes.  A mapping in use by a collective of this process
-// (another communicator, another thread) is never closed.  Caller holds pc.mu.
-void trim_mappings(ProcCache& pc, size_t incoming) {
-    for (size_t i = 0; i < pc.open_order.size() &&
-                       (pc.opened.size() + incoming > kMaxOpenMappings || pc.open_bytes > kMaxOpenBytes);) {
-        auto it = pc.opened.find(pc.open_order[i]);
-        if (it != pc.opened.end() && it->second.users == 0) {
-            if (ipc_debug())
-                std::fprintf(stderr, "[dccl ipc %d] trim: closing serial %llu at %p (%zu open, %zu bytes)\n", ::getpid(),
-                             static_cast<unsigned long long>(it->second.serial), it->second.base, pc.opened.size(),
-                             pc.open_bytes);
-            close_mapping(pc, it);
-        } else {
-            ++i;
-        }
-    }
-}
-
-// Map a peer's export (handle, serial) once and keep it; the caller holds a use of it (users) until its
-// last phase point.  The same exporter address with another serial names a new allocation that replaced a
-// freed one: the old mapping (which would still show the freed buffer's contents) is closed first, so the
-// open below imports the new allocation.  No collective of this process can still be using the old mapping:
-// the exporter freed that allocation, which it does only after every collective on it has completed on
-// every rank.  Caller holds pc.mu.
-ncclResult_t import_ptr(ProcCache& pc, uint32_t peer, int64_t pid, uint64_t base, uint64_t size,
-                        const unsigned char* handle, uint64_t serial, uint64_t off, unsigned char** out,
-                        std::vector<std::string>* held) {
-    // the key is the exporter's process and allocation address, not the handle bytes: a new allocation at a
-    // freed one's address is the same key with another serial whatever its handle bytes, so the freed
-    // allocation's mapping is closed before the new one is opened (the runtime may otherwise hand back its
-    // import of that address)
-    std::string key(reinterpret_cast<const char*>(&pid), sizeof(pid));
-    key.append(reinterpret_cast<const char*>(&base), sizeof(base));
-    uint64_t stale_id = 0;
-    auto it = pc.opened.find(key);
-    if (it != pc.opened.end() && it->second.serial != serial) {
-        if (ipc_debug())
-            std::fprintf(stderr, "[dccl ipc %d] peer %u: handle repeats with serial %llu (mapped: %llu, users %u), "
-                         "remapping\n", ::getpid(), peer, static_cast<unsigned long long>(serial),
-                         static_cast<unsigned long long>(it->second.serial), it->second.users);
-        if (it->second.users != 0) return dccl::ncclInternalError;  // see above: cannot happen
-        stale_id = it->second.import_id;
-        close_mapping(pc, it);
-        it = pc.opened.end();
-    }
-    if (it == pc.opened.end()) {
-        hipIpcMemHandle_t h;
-        std::memcpy(&h, handle, kHandleBytes);
-        void* mapped = nullptr;
-        // Re-opening an address whose previous mapping was closed just above races with the runtime's
-        // release of the old import: the open can fail for a moment (hipErrorInvalidDevicePointer, about
-        // one call in six in tests/test_direct.py::test_ipc_reallocated_buffers).  It is retried with
-        // backoff for ~0.5 s, and so is an open that hands back the closed import itself (the same runtime
-        // buffer id; never seen in tools/ipc_churn_stress.py runs, checked because it would be silent).
-        for (int attempt = 0, us = 100;; ++attempt, us = std::min(2 * us, 100000)) {
-            hipError_t e = hipIpcOpenMemHandle(&mapped, h, hipIpcMemLazyEnablePeerAccess);
-            if (e == hipSuccess && stale_id != 0 && buffer_id_of(mapped) == stale_id) {
-                (void)hipIpcCloseMemHandle(mapped);
-                e = hipErrorInvalidHandle;  // the old import again: not ours to use
-            }
-            if (e == hipSuccess) {  // an import of another size is another allocation: not ours either
-                hipDeviceptr_t mb = nullptr;
-                size_t got = 0;
-                if (hipMemGetAddressRange(&mb, &got, mapped) == hipSuccess && got != size) {
-                    if (ipc_debug())
-                        std::fprintf(stderr, "[dccl ipc %d] peer %u: import of serial %llu is %zu bytes, not %llu\n",
-                                     ::getpid(), peer, static_cast<unsigned long long>(serial), got,
-                                     static_cast<unsigned long long>(size));
-                    (void)hipIpcCloseMemHandle(mapped);
-                    e = hipErrorInvalidHandle;
-                }
-            }
-            if (e == hipSuccess) break;
-            (void)hipGetLastError();
-            if (ipc_debug())
-                std::fprintf(stderr, "[dccl ipc %d] peer %u: hipIpcOpenMemHandle(serial %llu) -> %d (attempt %d)\n",
-                             ::getpid(), peer, static_cast<unsigned long long>(serial), int(e), attempt);
-            if (attempt == 14) return dccl::ncclUnhandledCudaError;
-            std::this_thread::sleep_for(std::chrono::microseconds(us));
-        }
-        hipDeviceptr_t mb = nullptr;
-        size_t bytes = 0;
-        if (hipMemGetAddressRange(&mb, &bytes, mapped) != hipSuccess) {
-            (void)hipGetLastError();
-            bytes = 0;  // not counted against kMaxOpenBytes
-        }
-        pc.open_bytes += bytes;
-        it = pc.opened.emplace(key, Mapping{mapped, serial, bytes, 0, buffer_id_of(mapped)}).first;
-        pc.open_order.push_back(key);
-        if (ipc_debug())
-            std::fprintf(stderr, "[dccl ipc %d] peer %u: opened serial %llu at %p (%zu bytes, %zu mapped, import %llu, "
-                         "replaced %llu)\n", ::getpid(), peer, static_cast<unsigned long long>(serial), mapped, bytes,
-                         pc.open_bytes, static_cast<unsigned long long>(it->second.import_id),
-                         static_cast<unsigned long long>(stale_id));
-    }
-    ++it->second.users;
-    held->push_back(key);
-    *out = static_cast<unsigned char*>(it->second.base) + off;
-    return dccl::ncclSuccess;
-}
+// --- importer side (caller holds pc.mu) ---------------------------------------------------------------
 
 // Peer addresses of one collective's two buffers, own rank included.  On the IPC transport it holds a use
 // of every peer mapping it resolved, released when the collective returns (after its last phase point).
 struct Peers {
     std::vector<const unsigned char*> in;
     std::vector<unsigned char*> out;
-    std::vector<std::string> held;
+    std::vector<std::pair<int64_t, uint64_t>> held;
     Peers() = default;
     Peers(const Peers&) = delete;
     Peers& operator=(const Peers&) = delete;
@@ -347,12 +384,29 @@ struct Peers {
         if (held.empty()) return;
         ProcCache& pc = cache();
         std::lock_guard<std::mutex> lock(pc.mu);
-        for (const std::string& k : held) {
-            auto it = pc.opened.find(k);
-            if (it != pc.opened.end() && it->second.users > 0) --it->second.users;
-        }
+        for (const auto& k : held) pc.imports.release(k.first, k.second);
     }
 };
+
+ncclResult_t import_desc(ProcCache& pc, uint32_t peer, int64_t pid, const Desc& d, unsigned char** out, Peers* P) {
+    if (d.serial == 0) {
+        *out = nullptr;
+        return dccl::ncclSuccess;
+    }
+    ipc::Handle h;
+    std::memcpy(h.b, d.handle, kHandleBytes);
+    void* base = nullptr;
+    const ipc::Result r = pc.imports.acquire(pid, d.serial, h, d.size, &base);
+    if (r != ipc::kOk) {
+        if (ipc_debug())
+            std::fprintf(stderr, "[dccl ipc %d] peer %u serial %llu: import failed (%d)\n", ::getpid(), peer,
+                         (unsigned long long)d.serial, int(r));
+        return r == ipc::kOpenFailed ? dccl::ncclUnhandledCudaError : dccl::ncclInternalError;
+    }
+    P->held.emplace_back(pid, d.serial);
+    *out = static_cast<unsigned char*>(base) + d.off;
+    return dccl::ncclSuccess;
+}
 
 // A phase point of a direct collective: this rank's stream has drained (its inputs / outputs are
 // complete) and every rank got here.  It agrees on success: a rank whose step failed (rc) still comes
@@ -369,52 +423,99 @@ ncclResult_t arrive(dcclComm* c, hipStream_t st, ncclResult_t rc = dccl::ncclSuc
     return ok ? all : rc;
 }
 
-// Publish (in, out), meet every rank, then resolve every rank's (in, out) in this process.  *met is
-// false when the meeting itself failed (every rank sees that and returns); when it is true, a non-success
-// return is this rank's own failure to map a peer, which the caller carries into its next phase point.
-ncclResult_t exchange(dcclComm* c, const void* in, void* out, hipStream_t st, Peers* P, bool* met) {
+// What one rank publishes for a collective: `in` (peers read it; nullptr: nothing) of in_bytes, and
+// `out` (peers read the reduced chunks from it; nullptr: nothing) of out_bytes.  On the IPC transport a
+// buffer that is not registered is replaced by the communicator's scratch: `in` is copied there on `st`
+// (copy_in), and `out` becomes the scratch itself (the caller copies the result out).
+struct Publish {
+    const void* in = nullptr;
+    size_t in_bytes = 0;
+    void* out = nullptr;
+    size_t out_bytes = 0;
+    bool in_scratch = false, out_scratch = false;
+};
+
+// Decide and describe what this rank publishes (IPC): registered buffers as they are, the rest through
+// the scratch.  Fills this rank's slot.
+ncclResult_t plan_ipc(dcclComm* c, Publish* pub, hipStream_t st) {
+    IpcXport* x = xport(c);
+    ProcCache& pc = cache();
+    std::lock_guard<std::mutex> lock(pc.mu);
+    for (void* p : x->old_scratch) (void)hipFree(p);  // every peer closed them in the previous collective
+    x->old_scratch.clear();
+    auto in_e = pub->in ? find_registered(pc, pub->in, pub->in_bytes) : pc.exports.end();
+    auto out_e = pub->out ? find_registered(pc, pub->out, pub->out_bytes) : pc.exports.end();
+    pub->in_scratch = pub->in != nullptr && in_e == pc.exports.end();
+    pub->out_scratch = pub->out != nullptr && out_e == pc.exports.end();
+    // `out` in the scratch shares it with `in` (the all_reduce combines in place there)
+    const size_t need = std::max(pub->in_scratch ? pub->in_bytes : 0, pub->out_scratch ? pub->out_bytes : 0);
+    if (need > 0) {
+        const ncclResult_t rc = ensure_ipc_scratch(pc, x, need);
+        if (rc != dccl::ncclSuccess) return rc;
+    }
+    ShmSlot& s = x->ctl->slot[x->rank];
+    s.in.serial = s.out.serial = 0;
+    const uintptr_t sb = reinterpret_cast<uintptr_t>(x->scratch);
+    if (pub->in_scratch) {
+        if (hipMemcpyAsync(x->scratch, pub->in, pub->in_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess) {
+            (void)hipGetLastError();
+            return dccl::ncclUnhandledCudaError;
+        }
+        ++pc.scratch_copies;
+        pc.scratch_bytes += pub->in_bytes;
+        pub->in = x->scratch;
+    }
+    if (pub->out_scratch) pub->out = x->scratch;
+    if (pub->in) {
+        auto e = pub->in_scratch ? pc.exports.find(sb) : in_e;
+        describe(e->second, e->first, pub->in, &s.in);
+    }
+    if (pub->out) {
+        auto e = pub->out_scratch ? pc.exports.find(sb) : out_e;
+        describe(e->second, e->first, pub->out, &s.out);
+    }
+    return dccl::ncclSuccess;
+}
+
+// Publish, meet every rank, then resolve every rank's (in, out) in this process.  *met is false when the
+// meeting itself failed (every rank sees that and returns); when it is true, a non-success return is this
+// rank's own failure to map a peer, which the caller carries into its next phase point.
+ncclResult_t exchange(dcclComm* c, Publish* pub, hipStream_t st, Peers* P, bool* met) {
     const uint32_t W = c->world, r = c->rank;
     P->in.assign(W, nullptr);
     P->out.assign(W, nullptr);
     ncclResult_t rc = dccl::ncclSuccess;
     if (c->ipc) {
-        ShmSlot& s = xport(c)->ctl->slot[r];
-        s.pid = ::getpid();
-        rc = export_ptr(in, s.h_in, &s.off_in, &s.serial_in, &s.base_in, &s.size_in);
-        if (rc == dccl::ncclSuccess)
-            rc = export_ptr(out, s.h_out, &s.off_out, &s.serial_out, &s.base_out, &s.size_out);
+        rc = plan_ipc(c, pub, st);
     } else {
-        c->group->pub_in[r] = in;
-        c->group->pub_out[r] = out;
+        c->group->pub_in[r] = pub->in;
+        c->group->pub_out[r] = pub->out;
     }
     rc = arrive(c, st, rc);
     *met = rc == dccl::ncclSuccess;
     if (!*met) return rc;
-    ProcCache& pc = cache();
-    std::unique_lock<std::mutex> lock(pc.mu, std::defer_lock);
-    if (c->ipc) {
-        lock.lock();
-        trim_mappings(pc, 2 * size_t(W));
+    P->in[r] = static_cast<const unsigned char*>(pub->in);
+    P->out[r] = static_cast<unsigned char*>(pub->out);
+    if (!c->ipc) {
+        for (uint32_t p = 0; p < W; ++p)
+            if (p != r) {
+                P->in[p] = static_cast<const unsigned char*>(c->group->pub_in[p]);
+                P->out[p] = static_cast<unsigned char*>(c->group->pub_out[p]);
+            }
+        return dccl::ncclSuccess;
     }
+    ProcCache& pc = cache();
+    std::lock_guard<std::mutex> lock(pc.mu);
+    apply_retirements(pc);  // before any open: a retired export's handle bytes may come back
+    pc.imports.trim(2 * size_t(W));
+    const ShmCtl* ctl = xport(c)->ctl;
     for (uint32_t p = 0; p < W; ++p) {
-        if (p == r) {
-            P->in[p] = static_cast<const unsigned char*>(in);
-            P->out[p] = static_cast<unsigned char*>(out);
-        } else if (c->ipc) {
-            const ShmSlot& s = xport(c)->ctl->slot[p];
-            unsigned char* pi = nullptr;
-            unsigned char* po = nullptr;
-            rc = import_ptr(pc, p, s.pid, s.base_in, s.size_in, s.h_in, s.serial_in, s.off_in, &pi, &P->held);
-            if (rc == dccl::ncclSuccess)
-                rc = import_ptr(pc, p, s.pid, s.base_out, s.size_out, s.h_out, s.serial_out, s.off_out, &po,
-                                &P->held);
-            if (rc != dccl::ncclSuccess) return rc;
-            P->in[p] = pi;
-            P->out[p] = po;
-        } else {
-            P->in[p] = static_cast<const unsigned char*>(c->group->pub_in[p]);
-            P->out[p] = static_cast<unsigned char*>(c->group->pub_out[p]);
-        }
+        if (p == r) continue;
+        const ShmSlot& s = ctl->slot[p];
+        unsigned char* pi = nullptr;
+        if ((rc = import_desc(pc, p, s.pid, s.in, &pi, P)) != dccl::ncclSuccess) return rc;
+        if ((rc = import_desc(pc, p, s.pid, s.out, &P->out[p], P)) != dccl::ncclSuccess) return rc;
+        P->in[p] = pi;
     }
     return dccl::ncclSuccess;
 }
@@ -432,6 +533,7 @@ ncclResult_t chain(const Peers& P, uint32_t W, uint32_t first, size_t off, const
 
 ncclResult_t copy_pairs(const std::vector<const void*>& src, const std::vector<void*>& dst, size_t bytes,
                         hipStream_t st) {
+    if (src.empty()) return dccl::ncclSuccess;
     return static_cast<ncclResult_t>(dccl_copy_multi(src.data(), dst.data(), int(src.size()), bytes, st));
 }
 
@@ -500,17 +602,30 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
     }
     auto* x = new IpcXport;
     x->ctl = ctl;
-    if (const char* t = std::getenv("DCCL_IPC_TIMEOUT_S")) x->timeout_s = std::strtod(t, nullptr);
-    ctl->joined.fetch_add(1);
-    {
-        std::lock_guard<std::mutex> lock(cache().mu);
-        ++cache().comms;
+    x->rank = rank;
+    x->world = world;
+    x->seen.assign(world, 0);
+    if (const char* t = std::getenv("DCCL_IPC_TIMEOUT_S")) {
+        const double v = std::strtod(t, nullptr);
+        if (v > 0) x->timeout_s = v;
     }
+    ShmSlot& me = ctl->slot[rank];
+    me.start = proc_start_time(static_cast<long>(::getpid()));
+    me.pid = ::getpid();
+    ctl->joined.fetch_add(1);
     c->ipc = x;
     c->rank = rank;
     c->world = world;
     const ncclResult_t rc = shm_barrier(x);  // everyone mapped the segment
-    if (rc == dccl::ncclSuccess && rank == 0) {   // nothing left to find by name
+    {
+        // retirements written from here on reach this segment's peers (none can refer to an earlier export:
+        // nothing was published here before)
+        ProcCache& pc = cache();
+        std::lock_guard<std::mutex> lock(pc.mu);
+        for (uint32_t p = 0; p < world; ++p) x->seen[p] = ctl->slot[p].retired_n.load(std::memory_order_acquire);
+        pc.xports.push_back(x);
+    }
+    if (rc == dccl::ncclSuccess && rank == 0) {  // nothing left to find by name
         shm_unlink(name.c_str());
         rdv_remove(path);
     }
@@ -520,30 +635,148 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
 ncclResult_t ipc_leave(dcclComm* c) {
     IpcXport* x = xport(c);
     if (x == nullptr) return dccl::ncclInvalidArgument;
-    const ncclResult_t rc = shm_barrier(x);  // no peer still reads our buffers
+    ProcCache& pc = cache();
     {
-        // the last IPC communicator of the process releases the peer mappings (and with them the peers'
-        // freed allocations they kept alive)
-        ProcCache& pc = cache();
+        // the scratch ends with the communicator: retire it for every peer (of this and of every other
+        // communicator of this process) before the last meeting
         std::lock_guard<std::mutex> lock(pc.mu);
-        if (pc.comms > 0 && --pc.comms == 0) {
-            for (auto it = pc.opened.begin(); it != pc.opened.end();) {
-                auto next = std::next(it);
-                if (it->second.users == 0) close_mapping(pc, it);
-                it = next;
-            }
+        if (x->scratch != nullptr) {
+            auto e = pc.exports.find(reinterpret_cast<uintptr_t>(x->scratch));
+            if (e != pc.exports.end()) drop_export(pc, e);
         }
     }
+    ncclResult_t rc = shm_barrier(x);  // no peer still reads our buffers; every retirement is written
+    {
+        std::lock_guard<std::mutex> lock(pc.mu);
+        apply_retirements(pc);  // close the peers' scratch mappings
+        pc.xports.erase(std::remove(pc.xports.begin(), pc.xports.end(), x), pc.xports.end());
+        // the last IPC communicator of the process releases every peer mapping (and with them the peers'
+        // freed allocations they kept alive)
+        if (pc.xports.empty()) pc.imports.close_unused();
+    }
+    const ncclResult_t rc2 = shm_barrier(x);  // every peer closed our scratch
+    if (rc == dccl::ncclSuccess) rc = rc2;
+    for (void* p : x->old_scratch) (void)hipFree(p);
+    if (x->scratch) (void)hipFree(x->scratch);
     munmap(x->ctl, sizeof(ShmCtl));
     delete x;
     c->ipc = nullptr;
     return rc;
 }
 
+ncclResult_t ipc_register(void* buffer, size_t size) {
+    hipDeviceptr_t base = nullptr;
+    size_t asize = 0;
+    if (hipMemGetAddressRange(&base, &asize, buffer) != hipSuccess) {
+        (void)hipGetLastError();
+        return dccl::ncclInvalidArgument;  // not a device allocation of this process
+    }
+    const uintptr_t b = reinterpret_cast<uintptr_t>(base), a = reinterpret_cast<uintptr_t>(buffer);
+    if (a + size > b + asize) return dccl::ncclInvalidArgument;  // past its allocation
+    const uint64_t id = buffer_id_of(base);
+    ProcCache& pc = cache();
+    std::lock_guard<std::mutex> lock(pc.mu);
+    auto e = pc.exports.find(b);
+    if (e != pc.exports.end() && (e->second.size != asize || e->second.buffer_id != id)) {
+        ++pc.stale_registrations;  // a freed allocation's export at this address
+        drop_export(pc, e);
+        e = pc.exports.end();
+    }
+    if (e != pc.exports.end() && e->second.regs == 0) return dccl::ncclInvalidUsage;  // a communicator's scratch
+    auto old = pc.ranges.find(a);
+    if (old != pc.ranges.end()) {  // registering a range again replaces it
+        auto oe = pc.exports.find(old->second.base);
+        pc.ranges.erase(old);
+        if (oe != pc.exports.end() && --oe->second.regs == 0) drop_export(pc, oe);
+        e = pc.exports.find(b);
+    }
+    if (e == pc.exports.end()) {
+        const ncclResult_t rc = make_export(pc, b, asize, id, 0);
+        if (rc != dccl::ncclSuccess) return rc;
+        e = pc.exports.find(b);
+    }
+    ++e->second.regs;
+    pc.ranges[a] = Range{size, b};
+    return dccl::ncclSuccess;
+}
+
+namespace {
+
+// Wait until every live peer of every IPC communicator of this process has applied this process's
+// retirements written so far (ShmSlot::acked): then no peer maps a retired export any more, and the caller
+// may free the memory behind it.  The peers' own retirements are applied meanwhile (peers deregistering
+// at the same time wait for this process); a peer in a barrier applies them within ~0.1 s.  Called with
+// pc.mu held through `lock`, which it releases while it sleeps.  DCCL_IPC_DEREG_WAIT=0 skips it (A/B only).
+ncclResult_t wait_acked(ProcCache& pc, std::unique_lock<std::mutex>& lock) {
+    static const bool on = [] {
+        const char* v = std::getenv("DCCL_IPC_DEREG_WAIT");
+        return v == nullptr || *v != '0';
+    }();
+    if (!on) return dccl::ncclSuccess;
+    double timeout_s = 0;
+    for (IpcXport* x : pc.xports) timeout_s = std::max(timeout_s, x->timeout_s);
+    const auto start = std::chrono::steady_clock::now();
+    auto next_liveness = start + std::chrono::milliseconds(100);
+    std::vector<char> dead;
+    for (;;) {
+        apply_retirements(pc);
+        const auto now = std::chrono::steady_clock::now();
+        const bool check_live = now > next_liveness;
+        if (check_live) next_liveness = now + std::chrono::milliseconds(100);
+        bool done = true;
+        for (IpcXport* x : pc.xports) {
+            const uint64_t mine = x->ctl->slot[x->rank].retired_n.load(std::memory_order_acquire);
+            for (uint32_t p = 0; p < x->world; ++p) {
+                const ShmSlot& s = x->ctl->slot[p];
+                if (p == x->rank || s.acked[x->rank].load(std::memory_order_acquire) >= mine) continue;
+                if (check_live && !peer_alive(s)) continue;  // gone: its mappings went with it
+                done = false;
+            }
+        }
+        if (done) return dccl::ncclSuccess;
+        if (std::chrono::duration<double>(now - start).count() > timeout_s) return dccl::ncclSystemError;
+        lock.unlock();
+        if (now - start < std::chrono::milliseconds(2)) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+        lock.lock();
+    }
+}
+
+}  // namespace
+
+// dcclDeregisterCacheMemory: the export ends now (every peer is told through the segments), and the call
+// returns once every peer has closed its mapping of it, so the caller may free the buffer right away: a
+// peer still mapping a freed allocation is what made the runtime hand out stale memory for a new one at
+// the same address.
+ncclResult_t ipc_deregister(void* buffer) {
+    ProcCache& pc = cache();
+    std::unique_lock<std::mutex> lock(pc.mu);
+    auto r = pc.ranges.find(reinterpret_cast<uintptr_t>(buffer));
+    if (r == pc.ranges.end()) return dccl::ncclInvalidArgument;
+    auto e = pc.exports.find(r->second.base);
+    pc.ranges.erase(r);
+    if (e == pc.exports.end() || --e->second.regs != 0) return dccl::ncclSuccess;
+    drop_export(pc, e);
+    return wait_acked(pc, lock);
+}
+
+int ipc_stats(uint64_t* out, int n) {
+    ProcCache& pc = cache();
+    std::lock_guard<std::mutex> lock(pc.mu);
+    const ipc::ImportStats& s = pc.imports.stats;
+    const uint64_t v[] = {pc.exports_made, pc.retirements, pc.registered_hits, pc.scratch_copies, pc.scratch_bytes,
+                          pc.scratch_grows, pc.stale_registrations, s.opened, s.reused, s.retired, s.retired_pid,
+                          s.trimmed, s.alias_evicted, s.alias_errors, s.open_retries, s.size_mismatch,
+                          uint64_t(pc.imports.size()), uint64_t(pc.imports.bytes())};
+    const int m = std::min<int>(n, int(sizeof(v) / sizeof(v[0])));
+    for (int i = 0; i < m; ++i) out[i] = v[i];
+    return int(sizeof(v) / sizeof(v[0]));
+}
+
 // In-process groups take the direct collectives for device buffers unless DCCL_ALLREDUCE_ALGORITHM names
 // another algorithm: "direct", "auto" and unset select them.  They are faster than the ring at every
-// size measured (4 ranks, 1024 floats 199 -> 66 us; 8 ranks 992 -> 108 us) and give
-// the ring's results bit for bit.  Host buffers, the RCCL transport and groups above 8 ranks keep the ring.
+// size measured and give the ring's results bit for bit.  Host buffers, the RCCL
+// transport and groups above 8 ranks keep the ring.
 bool direct_selected(const dcclComm* c) {
     if (c->ipc != nullptr) return true;
     if (c->p2p != nullptr || c->world > kDirectMaxWorld) return false;
@@ -555,15 +788,22 @@ bool direct_selected(const dcclComm* c) {
 
 // ncclAllReduce: the ring all-reduce (all_reduce_ring.cpp:8-79) leaves chunk r+1 reduced on rank r;
 // here rank r reduces that chunk from every rank's input in the ring's order, then pulls every other
-// chunk from the rank that reduced it.
+// chunk from the rank that reduced it.  On the IPC transport an unregistered `send` is read from the
+// scratch copy, and an unregistered `recv` is replaced by the scratch for the reduced chunk (reduced in
+// place there: no other rank reads that chunk of anyone's input), which this rank then copies out.
 ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t count, int dtype, int op,
                                hipStream_t st) {
     const uint32_t W = c->world, r = c->rank;
     if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
-    const size_t esz = size_of_dtype(dtype), slot_elems = count / W, slot = slot_elems * esz;
+    const size_t esz = size_of_dtype(dtype), slot_elems = count / W, slot = slot_elems * esz, total = count * esz;
+    Publish pub;
+    pub.in = send;
+    pub.in_bytes = total;
+    pub.out = recv;
+    pub.out_bytes = total;
     Peers P;
     bool met = false;
-    ncclResult_t rc = exchange(c, send, recv, st, &P, &met);
+    ncclResult_t rc = exchange(c, &pub, st, &P, &met);
     if (!met) return rc;
     const uint32_t mine = (r + 1) % W;
     if (rc == dccl::ncclSuccess)
@@ -572,9 +812,9 @@ ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t
     std::vector<const void*> src;
     std::vector<void*> dst;
     for (uint32_t k = 0; k < W; ++k) {
-        if (k == mine) continue;
+        if (k == mine && !pub.out_scratch) continue;  // reduced in place
         src.push_back(P.out[(k + W - 1) % W] + k * slot);  // chunk k lives on rank k-1
-        dst.push_back(P.out[r] + k * slot);
+        dst.push_back(static_cast<unsigned char*>(recv) + k * slot);
     }
     return arrive(c, st, copy_pairs(src, dst, slot, st));  // peers are done reading our buffers
 }
@@ -648,9 +888,12 @@ ncclResult_t direct_reduce_scatter(dcclComm* c, const void* send, void* recv, si
     const uint32_t W = c->world, r = c->rank;
     if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
     const size_t slot = recvcount * size_of_dtype(dtype);
+    Publish pub;
+    pub.in = send;
+    pub.in_bytes = slot * W;
     Peers P;
     bool met = false;
-    ncclResult_t rc = exchange(c, send, recv, st, &P, &met);
+    ncclResult_t rc = exchange(c, &pub, st, &P, &met);
     if (!met) return rc;
     if (rc == dccl::ncclSuccess) rc = chain(P, W, (r + 1) % W, r * slot, P.in[r] + r * slot, recv, recvcount, dtype, op, st, r);
     return arrive(c, st, rc);
@@ -663,14 +906,17 @@ ncclResult_t direct_reduce(dcclComm* c, const void* send, void* recv, size_t cou
     const uint32_t W = c->world, r = c->rank;
     if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
     const size_t slot_elems = count / W, slot = slot_elems * size_of_dtype(dtype);
+    Publish pub;
+    pub.in = send;
+    pub.in_bytes = slot * W;
     Peers P;
     bool met = false;
-    ncclResult_t rc = exchange(c, send, r == root ? recv : const_cast<void*>(send), st, &P, &met);
+    ncclResult_t rc = exchange(c, &pub, st, &P, &met);
     if (!met) return rc;
     if (r == root)
         for (uint32_t o = 0; o < W && rc == dccl::ncclSuccess; ++o)
-            rc = chain(P, W, (o + 1) % W, o * slot, P.in[o] + o * slot, P.out[r] + o * slot, slot_elems, dtype, op,
-                       st, r);
+            rc = chain(P, W, (o + 1) % W, o * slot, P.in[o] + o * slot, static_cast<unsigned char*>(recv) + o * slot,
+                       slot_elems, dtype, op, st, r);
     return arrive(c, st, rc);
 }
 
@@ -679,17 +925,22 @@ ncclResult_t direct_all_gather(dcclComm* c, const void* send, void* recv, size_t
     const uint32_t W = c->world, r = c->rank;
     if (W > kDirectMaxWorld) return dccl::ncclInvalidUsage;
     const size_t slot = sendcount * size_of_dtype(dtype);
+    unsigned char* const out = static_cast<unsigned char*>(recv);
+    Publish pub;
+    pub.in = send;
+    pub.in_bytes = slot;
     Peers P;
     bool met = false;
-    ncclResult_t rc = exchange(c, send, recv, st, &P, &met);
+    ncclResult_t rc = exchange(c, &pub, st, &P, &met);
     if (!met) return rc;
     if (rc == dccl::ncclSuccess) {
         std::vector<const void*> src;
         std::vector<void*> dst;
         for (uint32_t p = 0; p < W; ++p) {
-            if (p == r && P.in[r] == P.out[r] + r * slot) continue;  // already in place
-            src.push_back(P.in[p]);
-            dst.push_back(P.out[r] + p * slot);
+            const void* from = p == r ? send : static_cast<const void*>(P.in[p]);  // own slice: the user's copy
+            if (p == r && from == out + r * slot) continue;  // already in place
+            src.push_back(from);
+            dst.push_back(out + p * slot);
         }
         rc = copy_pairs(src, dst, slot, st);
     }
@@ -700,13 +951,19 @@ ncclResult_t direct_broadcast(dcclComm* c, const void* send, void* recv, size_t 
                               hipStream_t st) {
     const uint32_t r = c->rank;
     const size_t bytes = count * size_of_dtype(dtype);
+    Publish pub;
+    if (r == root) {
+        pub.in = send;
+        pub.in_bytes = bytes;
+    }
     Peers P;
     bool met = false;
-    ncclResult_t rc = exchange(c, r == root ? send : recv, recv, st, &P, &met);
+    ncclResult_t rc = exchange(c, &pub, st, &P, &met);
     if (!met) return rc;
-    if (rc == dccl::ncclSuccess && P.in[root] != P.out[r]) {
-        std::vector<const void*> src{P.in[root]};
-        std::vector<void*> dst{P.out[r]};
+    const void* from = r == root ? send : static_cast<const void*>(P.in[root]);
+    if (rc == dccl::ncclSuccess && from != recv) {
+        std::vector<const void*> src{from};
+        std::vector<void*> dst{recv};
         rc = copy_pairs(src, dst, bytes, st);
     }
     return arrive(c, st, rc);

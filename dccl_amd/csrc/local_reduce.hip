@@ -7,7 +7,7 @@
 // scalar element per thread per iteration through a runtime op switch on a grid of
 // num_SMs x 256 threads; this one is an HBM stream:
 //   * 16-byte (global_load_dwordx4 / global_store_dwordx4) accesses of both operands;
-//   * the shipped shape (DefaultCfg, chosen by tools/tune_reduce.py on MI355X): one-wave
+//   * the shipped shape (DefaultCfg, chosen by tune_reduce.py@4f20423 on MI355X): one-wave
 //     (64-thread) blocks, one 16-B vector per lane and operand, i.e. one 1 KiB tile of each
 //     operand per block and ~1M blocks for 1 GiB; every load and the store non-temporal;
 //   * dtype and op are template parameters (no per-element switch);
@@ -33,11 +33,11 @@ namespace dccl_amd {
 namespace {
 
 // Default configuration of the shipped kernel.  One-wave blocks, one 16-B vector per lane and operand, every access non-temporal: the
-// fastest shape measured on MI355X at 1 GiB (tools/tune_reduce.py, profiles/r1_tune.json).
+// fastest shape measured on MI355X at 1 GiB (tune_reduce.py@4f20423, profiles/r1_tune.json).
 using DefaultCfg = VecCfg<64, 1, kNtSend | kNtRecv | kNtStore, false>;
 // When send's 128-B phase differs from recv's, every 1 KiB send tile straddles 9 lines, one of them
 // shared with the next tile (a wave on another XCD): send is then loaded through the caches, so the
-// shared line is fetched from HBM once (tools/phase_probe.py on MI355X, 1 GiB fp32 Sum: 81.0 % with
+// shared line is fetched from HBM once (phase_probe.py@4f20423 on MI355X, 1 GiB fp32 Sum: 81.0 % with
 // non-temporal send loads, 84.1 % cached; with equal phases non-temporal is 1 % faster).
 using StraddleCfg = VecCfg<64, 1, kNtRecv | kNtStore, false>;
 // The shifted kernel (operands with different 16-B phases) by the same rule; lane 63's extra send
@@ -46,7 +46,7 @@ constexpr int ShiftPolicy = kNtSend | kNtRecv | kNtStore;
 constexpr int ShiftStraddlePolicy = kNtRecv | kNtStore;
 // ... in the group-interleaved tile order (run_tile<8>): the vector lane 63 reads past its tile and the next
 // tile's first line then meet in one L2 in 7 of 8 cases while the chip sweeps one front.  1 GiB fp32 Sum,
-// pooled layout, two boxes (tools/pair_runs_probe.py, profiles/r3_s16_*, r3_s17_*): send + 4 B 83.8 -> 85.2-85.4 %,
+// pooled layout, two boxes (pair_runs_probe.py@4f20423, profiles/r3_s16_*, r3_s17_*): send + 4 B 83.8 -> 85.2-85.4 %,
 // send + 1 B 83.7-83.9 -> 85.3-85.4 %, send + 20 B (cached send loads) 84.1 -> 84.7 %: the aligned kernel's rate.
 constexpr int kShiftRun = 8;
 // recv is aligned to this many bytes by the head scalars (DCCL_REDUCE_ALIGN, a power of two from 16 to
@@ -146,7 +146,7 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
 // k-way combine: every resident wave keeps k+1 16-B loads per lane in flight, so the resident waves
 // per CU are capped (through unused dynamic LDS, 160 KiB per CU) to keep roughly 50-80 KiB of reads
 // outstanding per CU.  Measured optimum per k at 1 GiB per operand on MI355X, fp32 Sum
-// (tools/tune_multi.py, profiles/r1_tune_multi_waves.json): 4-7 % faster than 32 waves for k >= 2.
+// (tune_multi.py@4f20423, profiles/r1_tune_multi_waves.json): 4-7 % faster than 32 waves for k >= 2.
 // In-phase sources off recv's 128-B line grid (recv is line-aligned past the head): their loads go
 // through the caches, so the line two neighbouring tiles share is fetched once (StraddleCfg's rule).
 // 1 GiB-class A/B on one MI355X (profiles/r1_s5_kway_straddle_ab.json): k = 1 76.7 -> 85.6 %,

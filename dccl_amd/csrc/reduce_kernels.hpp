@@ -169,7 +169,7 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, unsigned b) {
 }
 
 // Cross-lane moves by one lane with DPP wave shifts (a VALU modifier, no LDS round trip), lane mapping
-// verified on gfx950 by tools/dpp_probe.hip: wave_rol:1 (0x134) gives lane l lane (l+1) % 64's value,
+// verified on gfx950 by dpp_probe.hip@4f20423: wave_rol:1 (0x134) gives lane l lane (l+1) % 64's value,
 // wave_shl:1 (0x130) the same except that lane 63 keeps `old`; wave_ror:1 (0x13C) gives lane l lane
 // (l+63) % 64's value, wave_shr:1 (0x138) the same except that lane 0 keeps `old`.
 template <int CTRL>
@@ -182,7 +182,7 @@ __device__ __forceinline__ u32x4 dpp16(u32x4 x, u32x4 old) {
     return o;
 }
 // lane l < 63 receives lane l+1's x, lane 63 keeps its own `last` (the tuning code's other shifts:
-// tools/tune/misaligned_2pass.hpp)
+// misaligned_2pass.hpp@4f20423)
 __device__ __forceinline__ u32x4 from_next_lane_or(u32x4 x, u32x4 last) { return dpp16<0x130>(x, last); }
 
 template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true, int RUN = 1>
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(64) void reduce_shift_kernel(const unsigned char* _
 // ---------------------------------------------------------------------------------
 // A recv that is not element-aligned (e.g. fp32 at an odd byte address; the reference's host loop takes
 // it with a warning, internal_common.hpp:504-512, its CUDA kernel not at all).  gfx950 executes
-// global_store_dwordx4 at any byte address (tools/unaligned_probe.hip checks every element), so lane i owns
+// global_store_dwordx4 at any byte address (unaligned_probe.hip@4f20423 checks every element), so lane i owns
 // the 16 bytes of elements [V i, V i + V) at their displaced address (V = 16 / sizeof(T)): adjacent lanes'
 // windows are disjoint and hold whole elements, so no byte is written twice.  Both operands' windows are
 // read the shifted kernel's way (aligned loads, lane exchange, funnel shift by the operand's own phase);
@@ -369,7 +369,7 @@ __device__ __forceinline__ u32x4 ld_phased_finish(const PhasedLoad& x, unsigned 
 
 // XCD: consecutive tiles on one XCD (xcd_remap), so the vector lane 63 reads past its tile and the
 // next tile's first line meet in one L2.  It pays while few operands share the L2.  1 GiB fp32 Sum,
-// sources 4 B off phase, on two boxes (tools/phased_probe.py, profiles/r2_phased_xcd_*.json), points of
+// sources 4 B off phase, on two boxes (phased_probe.py@4f20423, profiles/r2_phased_xcd_*.json), points of
 // HBM peak gained: k-way k = 2 +2.1..+4.0, k = 3 +2.1..+2.5, k = 4 +0.6..+1.7, k = 5 -0.2..+0.8,
 // k = 7 -2.2..-5.1; the chain kernel (in place) within 0.5 points of the same at every k.
 inline constexpr int kPhasedXcdMaxK = 4;
@@ -629,7 +629,7 @@ struct Split {
 
 // head scalars bring recv to an `align`-byte boundary (16 or more, a power of two).  Aligning recv to
 // its 128-B lines keeps every tile's recv loads and stores whole-line: a recv that straddles lines
-// costs 10-15 % (tools/phase_probe.py, profiles/r1_s3_phase_probe.json).  head < align / sizeof(T).
+// costs 10-15 % (phase_probe.py@4f20423, profiles/r1_s3_phase_probe.json).  head < align / sizeof(T).
 template <typename T>
 inline Split split_for_vectors(uintptr_t recv, size_t count, size_t align = 16) {
     constexpr size_t V = Pack<T>::N;

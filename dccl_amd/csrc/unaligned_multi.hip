@@ -19,7 +19,7 @@ size_t unaligned_grid(size_t nvec) {
 // Tile order: with every source at 16-B phase 0 (plain vector loads) one front for the chip wins, the
 // group-interleaved order up to k = 2 and block order above; sources at other phases keep consecutive tiles
 // on one XCD, where the vector lane 63 reads past its tile meets the next tile's first line in one L2.
-// 1 GiB fp32 Sum, destination + 2 B, one box (tools/unaligned_forms_probe.py, profiles/r3_s4_*): aligned sources
+// 1 GiB fp32 Sum, destination + 2 B, one box (unaligned_forms_probe.py@4f20423, profiles/r3_s4_*): aligned sources
 // k = 2 80.0 -> 83.4 % (group), k = 4 74.6 -> 78.0 %, k = 8 71.7 -> 76.4 % (block); the chain the same.
 int unaligned_order(const PhaseList& ph, int nsend) {
     for (int k = 0; k < nsend; ++k)

@@ -22,6 +22,25 @@
  *                         collective returns ncclRemoteError (6) until dccl_comm_finalize, which still
  *                         returns and releases the shared segment and the peers' mappings.  (The
  *                         in-process transport agrees per collective and stays usable after a failure.)
+ *                         Peers read device memory registered with dccl_comm_register in place; any other
+ *                         input is first copied (on the collective's stream) into the communicator's
+ *                         scratch, one library-owned allocation exported once.  A peer whose process dies
+ *                         ends every other rank's wait with ncclRemoteError within ~0.1 s; a live peer that
+ *                         never arrives, after DCCL_IPC_TIMEOUT_S (default 60 s).  Communicators of one
+ *                         process share one mapping cache under one mutex: collectives driven from several
+ *                         threads at once serialise while they map peer buffers.
+ *   dccl_comm_register /  dcclRegisterCacheMemory / dcclDeregisterCacheMemory (/root/reference/src/core/
+ *   dccl_comm_deregister  dccl.cpp:503-549): 64-byte aligned address and size.  Host memory is page-locked.
+ *                         Device memory on an IPC communicator becomes an export peers map in place until
+ *                         it is deregistered (the registration belongs to the process: every IPC
+ *                         communicator of it reads the range in place); the caller keeps the allocation
+ *                         alive until then.  Other communicators: accepted, nothing to do.
+ *   dccl_ipc_stats        the process's IPC transport counters, in this order: exports made, exports
+ *                         retired, registered-buffer hits, scratch copies, scratch bytes copied, scratch
+ *                         grows, stale registrations dropped, mappings opened, mappings reused, mappings
+ *                         closed on retirement, retirement-log overflows, mappings trimmed, alias
+ *                         evictions, alias errors, open retries, size mismatches, mappings open, bytes
+ *                         mapped.  Fills min(n, count) values; returns count.
  *   dccl_bootstrap_unique_id  single-node exchange of the RCCL id through DCCL_BOOTSTRAP_DIR: rank 0
  *                         creates and publishes it, the others wait (DCCL_BOOTSTRAP_TIMEOUT_S, default
  *                         120 s) for a file published by a LIVE rank 0 of the same world size, so a
@@ -64,6 +83,9 @@ int dccl_reduce(const void* send, void* recv, size_t count, int dtype, int op, i
                 void* stream);
 int dccl_broadcast(const void* send, void* recv, size_t count, int dtype, int root, void* comm, void* stream);
 int dccl_rccl_available(void);
+int dccl_comm_register(void* comm, void* buffer, size_t size);
+int dccl_comm_deregister(void* comm, void* buffer);
+int dccl_ipc_stats(uint64_t* out, int n);
 #ifdef __cplusplus
 }
 #endif

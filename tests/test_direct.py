@@ -374,13 +374,15 @@ def test_ipc_transport_processes(gpu, W, n, dt, op):
     assert all(results[r]["finalize"] == 0 for r in range(W))
 
 
-def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=False):
+def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=False, register=False):
     """All-gathers over fresh allocations: before each round every buffer of the previous round is freed back to
     the driver (torch.cuda.empty_cache), so the next allocation may reuse its address; every round carries new
     data.  `grow`: odd rounds send W times as much, so a round's input lands where the previous round's output
     was (bench.py's all_gather at 256 MiB followed by C5's).  `two_comms`: every round runs on two IPC
     communicators of the same ranks, which share the process's peer mappings.  `hold`: nothing is freed, so
-    every round's buffers are new allocations and the peer mappings pile up past the cache's bound."""
+    every round's buffers are new allocations and the peer mappings pile up past the cache's bound.
+    `register`: every round registers its buffers (dcclRegisterCacheMemory) and deregisters them before the
+    free, so peers read them in place and the exports churn; otherwise inputs go through the scratch."""
     os.environ["DCCL_BOOTSTRAP_TAG"] = tag
     os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")
     try:
@@ -393,6 +395,7 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=
             comms.append(dccl_amd.Comm.ipc(W, r))
         bad = []  # (round, peer, what it held) of every slice that is wrong
         kept = []
+        ptrs = []  # this rank's input address per round (a peer's report is read against it)
         try:
             st = torch.cuda.Stream()
             for k in range(rounds):
@@ -401,6 +404,11 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=
                 mine = torch.randint(-2**31, 2**31 - 1, (n,), device="cuda", dtype=torch.int32, generator=g)
                 out = torch.zeros(W * n, device="cuda", dtype=torch.int32)
                 torch.cuda.synchronize()
+                ptrs.append(mine.data_ptr())
+                if register:
+                    for cm in comms:
+                        assert cm.register(mine.data_ptr(), n * 4) == 0
+                        assert cm.register(out.data_ptr(), W * n * 4) == 0
                 want = [torch.randint(-2**31, 2**31 - 1, (n,), device="cuda", dtype=torch.int32,
                                       generator=torch.Generator(device="cuda").manual_seed(1000 * k + p))
                         for p in range(W)]
@@ -423,6 +431,10 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=
                             bad.append((k, p, f"comm {ci}: round {stale} data" if stale else f"comm {ci}: other, {frac}"))
                 if bad and bad[-1][1] == -1:
                     break
+                if register:
+                    for cm in comms:
+                        assert cm.deregister(mine.data_ptr()) == 0
+                        assert cm.deregister(out.data_ptr()) == 0
                 if hold:
                     kept.append((mine, out))
                 del mine, out, want
@@ -431,27 +443,36 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=
                     torch.cuda.empty_cache()
         finally:
             fin = max(cm.finalize() for cm in comms)
-        q.put((r, (bad, fin), None))
+        q.put((r, (bad, fin, dccl_amd.ipc_stats(), ptrs), None))
     except Exception as e:  # pragma: no cover - reported by the parent
         q.put((r, None, repr(e)))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,nbytes,rounds,grow,two,hold", [
-    (2, 64 << 20, 4, False, False, False), (4, 256 << 20, 4, False, False, False), (4, 64 << 20, 4, True, False, False),
-    (4, 64 << 20, 4, True, True, False), (2, 64 << 20, 6, False, True, False), (2, 16 << 20, 140, False, False, True)])
-def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold):
+@pytest.mark.parametrize("W,nbytes,rounds,grow,two,hold,reg", [
+    # VERDICT r3's churn cases: 1 MiB buffers freed and re-allocated every round
+    (2, 1 << 20, 140, False, False, False, False), (4, 1 << 20, 100, False, False, False, False),
+    (2, 1 << 20, 140, False, False, False, True), (4, 1 << 20, 100, False, False, False, True),
+    (4, 1 << 20, 40, True, True, False, True),
+    (2, 64 << 20, 4, False, False, False, False), (4, 256 << 20, 4, False, False, False, False),
+    (4, 64 << 20, 4, True, False, False, True), (4, 64 << 20, 4, True, True, False, False),
+    (2, 64 << 20, 6, False, True, False, True), (2, 16 << 20, 140, False, False, True, True)])
+def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold, reg):
     """A peer's buffer freed and a new one of the same size allocated must be mapped afresh: a cache of peer
     mappings keyed by the IPC handle alone can hand back the freed buffer's mapping (the handle bytes of a
     dmabuf export can repeat once the old export is closed), and the collective then reads stale data.
     140 rounds at W = 2 with every buffer kept (16 MiB inputs, 32 MiB outputs: one allocation each) import 280
     peer allocations, past the 256 mappings a process keeps open (trim_mappings closes the oldest unused ones).
     `two`: two communicators of the same ranks share the process's mappings (a stale mapping one of them still
-    held used to shadow the other's re-import)."""
+    held used to shadow the other's re-import).  `reg`: the buffers are registered every round (peers map
+    them in place, and every deregistration retires an export); otherwise inputs reach the peers through
+    each communicator's scratch, which is exported once.  Either way no mapping may alias another
+    (alias_errors == 0 in every process)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     tag = "test_" + uuid.uuid4().hex[:12]
-    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q, two, hold)) for r in range(W)]
+    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q, two, hold, reg))
+          for r in range(W)]
     for p in ps:
         p.start()
     results = {}
@@ -466,5 +487,57 @@ def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold):
             if p.is_alive():
                 p.kill()
     for r in range(W):
-        bad, fin = results[r]
-        assert not bad and fin == 0, (r, bad[:8], len(bad), fin)
+        bad, fin, stats, _ = results[r]
+        assert not bad and fin == 0, (r, bad[:8], len(bad), fin, stats)
+        assert stats["alias_errors"] == 0, (r, stats)
+        if reg:  # peers read the registered inputs in place: no scratch copy
+            assert stats["scratch_copies"] == 0 and stats["registered_hits"] >= rounds, (r, stats)
+        else:
+            assert stats["scratch_copies"] >= rounds, (r, stats)
+
+
+def _ipc_dying_rank(r, tag, q):
+    os.environ["DCCL_BOOTSTRAP_TAG"] = tag
+    os.environ["DCCL_IPC_TIMEOUT_S"] = "100"  # far above the wait the liveness check allows
+    try:
+        import time
+        import torch
+        import dccl_amd
+        torch.cuda.set_device(0)
+        comm = dccl_amd.Comm.ipc(2, r)
+        if r == 1:
+            q.put((r, None, None))
+            os._exit(0)  # gone without finalize, as after a runtime abort
+        x = torch.ones(1 << 20, device="cuda", dtype=torch.float32)
+        t0 = time.monotonic()
+        rc = comm.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), 7, 0, torch.cuda.current_stream().cuda_stream)
+        dt = time.monotonic() - t0
+        q.put((r, (rc, dt, comm.finalize()), None))
+    except Exception as e:  # pragma: no cover - reported by the parent
+        q.put((r, None, repr(e)))
+
+
+@pytest.mark.gpu
+def test_ipc_dead_peer_ends_wait(gpu):
+    """A rank whose process dies (a runtime abort in round 3's 64 MiB churn run left its peers in the
+    barrier for the whole timeout) ends the others' collective with an error within seconds."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    tag = "test_" + uuid.uuid4().hex[:12]
+    ps = [ctx.Process(target=_ipc_dying_rank, args=(r, tag, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    results = {}
+    try:
+        for _ in range(2):
+            r, res, err = q.get(timeout=120)
+            assert err is None, (r, err)
+            results[r] = res
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    rc, dt, fin = results[0]
+    assert rc in (2, 6), rc  # ncclRemoteError (or ncclSystemError)
+    assert dt < 10.0, dt

@@ -4,7 +4,11 @@ re-allocation rank body (all-gathers over buffers freed back to the driver and r
 round's data checked) run `--runs` times at W ranks on the box's one GPU.  One JSON line on stdout: runs, runs
 with a wrong slice or an error, and the first few reports.
 
-    python tools/ipc_churn_stress.py [--runs 20] [--world 2] [--mib 1] [--rounds 140] [--grow] [--two]
+    python tools/ipc_churn_stress.py [--runs 20] [--world 2] [--mib 1] [--rounds 140] [--grow] [--two] [--register]
+
+With --register every round registers its buffers (peers map them in place) and deregisters them before
+the free; a wrong slice is reported with whether its exporter's input sat at the same address as the round
+before (`va_reused`).
 """
 import argparse
 import json
@@ -26,6 +30,7 @@ def main():
     p.add_argument("--rounds", type=int, default=140)
     p.add_argument("--grow", action="store_true")
     p.add_argument("--two", action="store_true")
+    p.add_argument("--register", action="store_true")
     a = p.parse_args()
     # a rank that fails leaves its peers at a barrier: let them give up well before a pool's silence limit
     os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")
@@ -35,17 +40,25 @@ def main():
         q = ctx.Queue()
         tag = "stress_" + uuid.uuid4().hex[:10]
         ps = [ctx.Process(target=_ipc_realloc_rank,
-                          args=(r, a.world, a.mib << 20, a.rounds, a.grow, tag, q, a.two, False))
+                          args=(r, a.world, a.mib << 20, a.rounds, a.grow, tag, q, a.two, False, a.register))
               for r in range(a.world)]
         for x in ps:
             x.start()
-        bad = []
+        bad, results = [], {}
         for _ in range(a.world):
             r, res, err = q.get(timeout=150)
             if err is not None:
                 bad.append((r, err))
-            elif res[0] or res[1] != 0:
-                bad.append((r, res[0][:4], res[1]))
+            else:
+                results[r] = res
+        for r, res in results.items():
+            if res[0] or res[1] != 0:
+                rep = []
+                for k, peer, what in res[0][:4]:
+                    pp = results.get(peer, (None, None, None, []))[3] if peer >= 0 else []
+                    reused = bool(k > 0 and len(pp) > k and pp[k] == pp[k - 1])
+                    rep.append((k, peer, what, {"va_reused": reused}))
+                bad.append((r, rep, res[1], {k: v for k, v in res[2].items() if v}))
         for x in ps:
             x.join(60)
             if x.is_alive():
@@ -55,7 +68,8 @@ def main():
             reports.append({"run": run, "bad": bad})
         print(f"run {run}: {'FAILED ' + repr(bad) if bad else 'ok'}", file=sys.stderr, flush=True)
     print(json.dumps({"runs": a.runs, "world": a.world, "mib": a.mib, "rounds": a.rounds, "grow": a.grow,
-                      "two": a.two, "failed_runs": failed, "reports": reports[:5]}, default=str), flush=True)
+                      "two": a.two, "register": a.register,
+                      "dereg_wait": os.environ.get("DCCL_IPC_DEREG_WAIT", "1"), "failed_runs": failed, "reports": reports[:5]}, default=str), flush=True)
 
 
 if __name__ == "__main__":
