@@ -27,8 +27,9 @@ set, per-launch duration eager from Python and from a C++ loop, and graph-replay
 rank 0, N=1), allgather (RCCL all-gather of the shards over xGMI, N>1, reported separately),
 c5 (BASELINE config C5 on every run: --c5-gib GiB per operand sharded over the N GPUs, strong scaling,
 combine time and, N>1, the RCCL all-gather of the reduced shards),
-dccl_allreduce (N>1: the namespace-dccl ncclAllReduce over the RCCL p2p ring and over the direct
-IPC peer-read transport, checked against each other and RCCL's own all_reduce, timed beside it, plus
+dccl_allreduce (N>1: the namespace-dccl ncclAllReduce over RCCL (the ring step loop, and the grouped form:
+one RCCL group per phase and one chain combine) and over the direct IPC peer-read transport (inputs through
+the scratch, and registered), checked against each other and RCCL's own all_reduce, timed beside it, plus
 the namespace-dccl all_gather of each transport against RCCL's all_gather (`dccl_allgather`), and the
 direct all_gather at C5's size beside RCCL's (`c5_allgather`);
 in a child process per rank, so a fault or hang there cannot take the bench line with it).
@@ -601,9 +602,13 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
     dist.broadcast_object_list(obj, src=0)
     comms = {}
     if obj[0] is not None:
+        # one RCCL communicator, two algorithms: the reference's ring step loop, and the grouped form (one RCCL
+        # group per phase, one chain combine; the default on this transport, algorithms.hpp)
         comms["ring"] = dccl_amd.Comm.rccl(world, rank, obj[0])
+        comms["grouped"] = comms["ring"]
     if "direct" in transports:
         comms["direct"] = dccl_amd.Comm.ipc(world, rank)
+    algo_env = {"ring": "ring", "grouped": "auto", "direct": "auto"}
     out = {"count": count, "world": world, "bytes": count * 4}
     try:
         st = torch.cuda.current_stream(dev)
@@ -615,6 +620,7 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
         dist.all_reduce(rf)
         yf_by = {}
         for name, comm in comms.items():
+            os.environ["DCCL_ALLREDUCE_ALGORITHM"] = algo_env[name]
             yi = xi.clone()
             yf = xf.clone()
             torch.cuda.synchronize(dev)
@@ -655,17 +661,26 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
                 for buf in (yf, yr):
                     dccl_amd.check(comm.deregister(buf.data_ptr()), "deregister")
                 del yr, zr
-            res.update(root_ops(comm, world, rank, dev, st, xi, ri, iters))
+            if name != "grouped":  # broadcast / reduce do not depend on the all-reduce algorithm
+                res.update(root_ops(comm, world, rank, dev, st, xi, ri, iters))
             out[name] = res
             yf_by[name] = yf
-        if "ring" in yf_by and "direct" in yf_by:
-            # same association order: the first all_reduce of each path must agree bit for bit
-            a_, b_ = xf.clone(), xf.clone()
-            torch.cuda.synchronize(dev)
-            dccl_amd.check(comms["ring"].all_reduce(a_.data_ptr(), a_.data_ptr(), count, 7, 0, st.cuda_stream), "r")
-            dccl_amd.check(comms["direct"].all_reduce(b_.data_ptr(), b_.data_ptr(), count, 7, 0, st.cuda_stream), "d")
-            torch.cuda.synchronize(dev)
-            out["fp32_direct_bit_exact_vs_ring"] = bool(torch.equal(a_.view(torch.int32), b_.view(torch.int32)))
+        # same association order: the first all_reduce of every path must agree with the ring's bit for bit
+        if "ring" in yf_by:
+            first = {}
+            for name in ("ring", "grouped", "direct"):
+                if name in comms:
+                    os.environ["DCCL_ALLREDUCE_ALGORITHM"] = algo_env[name]
+                    first[name] = xf.clone()
+                    torch.cuda.synchronize(dev)
+                    dccl_amd.check(comms[name].all_reduce(first[name].data_ptr(), first[name].data_ptr(), count, 7,
+                                                          0, st.cuda_stream), name)
+                    torch.cuda.synchronize(dev)
+            for name in ("grouped", "direct"):
+                if name in first:
+                    out[f"fp32_{name}_bit_exact_vs_ring"] = bool(torch.equal(first["ring"].view(torch.int32),
+                                                                             first[name].view(torch.int32)))
+        os.environ["DCCL_ALLREDUCE_ALGORITHM"] = "auto"
         dist.barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
@@ -677,7 +692,8 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
                                  "backend": dist.get_backend(),
                                  "note": "the torch.distributed backend's own all_reduce (RCCL when the backend is "
                                          "nccl), informational: its combine is the backend's"}
-        out["dccl_allgather"] = allgather_compare(comms, world, rank, dev, st, count, iters)
+        out["dccl_allgather"] = allgather_compare({k: v for k, v in comms.items() if k != "grouped"}, world, rank,
+                                                  dev, st, count, iters)
         # BASELINE C5's exchange step at its own size (the reduced shards of DCCL_BENCH_C5_GIB GiB of fp32,
         # moved as int32): the direct IPC all-gather beside RCCL's (the single-link ring is left out here)
         c5_gib = float(os.environ.get("DCCL_BENCH_C5_GIB", "0") or 0)
@@ -686,7 +702,7 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
             torch.cuda.empty_cache()
             out["c5_allgather"] = allgather_compare({"direct": comms["direct"]}, world, rank, dev, st, c5_count, 3)
     finally:
-        for comm in comms.values():
+        for comm in {id(c): c for c in comms.values()}.values():
             comm.finalize()
     if "direct" in comms:  # the IPC transport's counters, summed over the ranks (alias_errors must be 0)
         every = [None] * world
@@ -1012,8 +1028,8 @@ def allreduce_summary(ar) -> dict:
     """The bit-exactness flags and rates of dccl_allreduce (N > 1), small enough for the line's tail."""
     if not isinstance(ar, dict):
         return {"error": repr(ar)}
-    out = {k: ar[k] for k in ("error", "fp32_direct_bit_exact_vs_ring") if k in ar}
-    for name in ("ring", "direct"):
+    out = {k: ar[k] for k in ("error", "fp32_direct_bit_exact_vs_ring", "fp32_grouped_bit_exact_vs_ring") if k in ar}
+    for name in ("ring", "grouped", "direct"):
         if isinstance(ar.get(name), dict):
             out[name] = {k: ar[name][k] for k in ("int32_sum_bit_exact_vs_rccl", "fp32_within_bound", "ms",
                                                   "busbw_gb_s", "registered_ms", "registered_busbw_gb_s",

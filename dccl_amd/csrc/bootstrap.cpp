@@ -119,6 +119,29 @@ dccl::ncclResult_t rdv_publish(const std::string& path, uint32_t world, const st
     return dccl::ncclSuccess;
 }
 
+namespace {
+
+std::string took_marker(const std::string& path, const Stamp& st, uint32_t reader) {
+    return path + ".took." + std::to_string(st.pid) + "." + std::to_string(st.start) + "." + std::to_string(st.gen) +
+           "." + std::to_string(reader);
+}
+
+// Reader `reader` took publication `st`: leave a marker, and the reader that completes the set (every rank
+// but the publisher, rank 0) removes the publication and the markers.  A process that starts afterwards finds
+// no file and waits for the next publication, so it can never join a group that already formed, whether or
+// not rank 0 ever calls dccl_bootstrap_done.
+void mark_taken(const std::string& path, const Stamp& st, uint32_t world, uint32_t reader) {
+    { std::ofstream(took_marker(path, st, reader)) << '\n'; }
+    for (uint32_t r = 1; r < world; ++r)
+        if (!std::ifstream(took_marker(path, st, r)).good()) return;
+    std::string payload;
+    Stamp now;
+    if (try_read(path, world, &payload, &now) && now == st) std::remove(path.c_str());
+    for (uint32_t r = 1; r < world; ++r) std::remove(took_marker(path, st, r).c_str());
+}
+
+}  // namespace
+
 dccl::ncclResult_t rdv_read(const std::string& path, uint32_t world, uint32_t reader, double timeout_s,
                             std::string* payload) {
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
@@ -126,10 +149,15 @@ dccl::ncclResult_t rdv_read(const std::string& path, uint32_t world, uint32_t re
     for (;;) {
         Stamp st;
         if (try_read(path, world, payload, &st)) {
-            std::lock_guard<std::mutex> lk(g_mu);
-            auto it = g_consumed.find(key);
-            if (it == g_consumed.end() || !(it->second == st)) {  // not the publication this reader already took
-                g_consumed[key] = st;
+            bool fresh = false;
+            {
+                std::lock_guard<std::mutex> lk(g_mu);
+                auto it = g_consumed.find(key);
+                fresh = it == g_consumed.end() || !(it->second == st);  // not the publication this reader took
+                if (fresh) g_consumed[key] = st;
+            }
+            if (fresh) {
+                mark_taken(path, st, world, reader);
                 return dccl::ncclSuccess;
             }
         }

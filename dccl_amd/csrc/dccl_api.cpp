@@ -272,6 +272,17 @@ Algorithm allreduce_algorithm() {
     return Algorithm::kUnknown;
 }
 
+// The grouped forms of algorithms.hpp on the RCCL transport's device buffers: unless
+// DCCL_ALLREDUCE_ALGORITHM names ring or rabenseifner ("auto", "direct" and unset select them, as for the
+// direct collectives of direct.hpp).  Results are the ring's bit for bit.
+bool grouped_selected(const dcclComm* c, bool device) {
+    if (!device || c->rccl == nullptr || c->world < 2) return false;
+    const char* a = std::getenv(DCCL_ALLREDUCE_ALGORITHM_CONFSTR);
+    if (a == nullptr || *a == 0) return true;
+    const std::string s(a);
+    return s == "auto" || s == "direct";
+}
+
 uint32_t floor_log2_u32(uint32_t n) {
     uint32_t k = 0;
     while ((n >> (k + 1)) != 0) ++k;
@@ -420,6 +431,8 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
         return direct_all_reduce(comm, sendbuff, recvbuff, count, datatype, op, stream);
     if (W > 1 && !dev && host_direct_selected(comm, total / W))
         return direct_all_reduce_host(comm, sendbuff, recvbuff, count, datatype, op);
+    if (W > 1 && algo != Algorithm::kRabenseifner && grouped_selected(comm, dev))
+        return all_reduce_grouped(comm, sendbuff, recvbuff, count, datatype, op, stream);
     if ((rc = copy_bytes(recvbuff, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:393-408
     if (W == 1) return ncclSuccess;
     void* scratch = nullptr;
@@ -447,6 +460,8 @@ ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recv
         return direct_reduce_scatter(comm, sendbuff, recvbuff, recvcount, datatype, op, stream);
     if (W > 1 && !dev && host_direct_selected(comm, slot))
         return direct_reduce_scatter_host(comm, sendbuff, recvbuff, recvcount, datatype, op);
+    if (W > 1 && grouped_selected(comm, dev))  // slot r, reduced straight from sendbuff: no work copy
+        return reduce_scatter_grouped(comm, sendbuff, recvbuff, recvcount * W, datatype, op, stream, 0);
     if ((rc = ensure_work(comm, total, dev)) != ncclSuccess) return rc;
     void* work = dev ? comm->dev_work : comm->host_work;
     if ((rc = copy_bytes(work, sendbuff, total, dev, stream)) != ncclSuccess) return rc;  // dccl.cpp:585-609

@@ -62,8 +62,6 @@ struct ShmSlot {
     // ring, retired_n written last.  Every peer closes their mappings before it opens anything new.
     std::atomic<uint64_t> retired_n;
     uint64_t retired[kRetireRing];
-    // acked[p]: how many of rank p's retirements this rank has applied (its mappings of them are closed)
-    std::atomic<uint64_t> acked[kMaxRanks];
 };
 
 struct ShmCtl {
@@ -84,6 +82,7 @@ struct Export {
     uint64_t serial;
     ipc::Handle handle;
     uint32_t regs;  // registered ranges on it (0 for a scratch buffer)
+    bool fresh;     // its handle bytes never named another allocation of this process (see make_export)
 };
 
 // A range registered with dcclRegisterCacheMemory, and the allocation (export) holding it.
@@ -147,13 +146,18 @@ struct ProcCache {
     HipOps ops;
     ipc::ImportCache imports{&ops, kMaxOpenMappings, kMaxOpenBytes};
     std::vector<IpcXport*> xports;  // live IPC communicators of this process
+    // handle bytes of every export this process made -> the buffer id of the allocation they named
+    std::map<std::string, uint64_t> handle_owner;
     // exporter-side counters (dccl_ipc_stats)
     uint64_t exports_made = 0, retirements = 0, registered_hits = 0, scratch_copies = 0, scratch_bytes = 0,
-             scratch_grows = 0, stale_registrations = 0;
+             scratch_grows = 0, stale_registrations = 0, recycled_handles = 0, registered_fallbacks = 0;
 };
 
 ProcCache& cache() {
-    static ProcCache* c = new ProcCache;  // never destroyed: communicators may outlive static destructors
+    static ProcCache* c = [] {
+        auto* p = new ProcCache;  // never destroyed: communicators may outlive static destructors
+        return p;
+    }();
     return *c;
 }
 
@@ -197,7 +201,6 @@ void apply_retirements(ProcCache& pc) {
                 if (s.retired_n.load(std::memory_order_acquire) - seen > kRetireRing) pc.imports.retire_pid(s.pid);
             }
             seen = n;
-            x->ctl->slot[x->rank].acked[p].store(n, std::memory_order_release);
         }
     }
 }
@@ -238,13 +241,6 @@ ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
         }
         if (now > next_check) {
             next_check = now + kLiveness;
-            // close the mappings of exports the peers retired meanwhile: a peer may be waiting for that
-            // (ipc_deregister) before its process frees the memory
-            ProcCache& pc = cache();
-            if (pc.mu.try_lock()) {
-                apply_retirements(pc);
-                pc.mu.unlock();
-            }
             for (uint32_t p = 0; p < s->world; ++p)
                 if (p != x->rank && !peer_alive(s->slot[p])) {
                     if (ipc_debug()) std::fprintf(stderr, "[dccl ipc %d] rank %u's process is gone\n", ::getpid(), p);
@@ -291,7 +287,7 @@ ncclResult_t make_export(ProcCache& pc, uintptr_t base, size_t size, uint64_t id
     for (auto o = pc.exports.lower_bound(base); o != pc.exports.end() && o->first < base + size;
          o = pc.exports.lower_bound(base))
         drop_export(pc, o);
-    Export e{size, id, pc.next_serial++, {}, regs};
+    Export e{size, id, pc.next_serial++, {}, regs, true};
     hipIpcMemHandle_t h;
     // exporting an allocation at the address of a freed one that a peer still maps can fail for a moment
     for (int attempt = 0, us = 100;; ++attempt, us = std::min(2 * us, 100000)) {
@@ -301,11 +297,30 @@ ncclResult_t make_export(ProcCache& pc, uintptr_t base, size_t size, uint64_t id
         std::this_thread::sleep_for(std::chrono::microseconds(us));
     }
     std::memcpy(e.handle.b, &h, kHandleBytes);
+    // Handle bytes that already named another (freed) allocation of this process are never published: a peer
+    // that mapped them once and opens them again can be handed the earlier import's pages by the runtime,
+    // even after it closed that mapping (registered-buffer churn read stale data in 6 of 6
+    // runs at W = 2 although every mapping was closed before the new open).  Such an export stays unused
+    // (`fresh` false): a registered buffer then goes through the scratch, a scratch is allocated again.
+    // Without a buffer id, or past a bound on the table, nothing counts as fresh.
+    const std::string key(reinterpret_cast<const char*>(e.handle.b), kHandleBytes);
+    auto owner = pc.handle_owner.find(key);
+    if (owner != pc.handle_owner.end()) {
+        e.fresh = id != 0 && owner->second == id;
+        owner->second = id;
+    } else if (pc.handle_owner.size() < (size_t(1) << 20)) {
+        pc.handle_owner.emplace(key, id);
+        e.fresh = id != 0;
+    } else {
+        e.fresh = false;
+    }
+    if (!e.fresh) ++pc.recycled_handles;
     pc.exports.emplace(base, e);
     ++pc.exports_made;
     if (ipc_debug())
-        std::fprintf(stderr, "[dccl ipc %d] export base=%#zx size=%zu buffer_id=%llu serial=%llu\n", ::getpid(),
-                     size_t(base), size, (unsigned long long)id, (unsigned long long)e.serial);
+        std::fprintf(stderr, "[dccl ipc %d] export base=%#zx size=%zu buffer_id=%llu serial=%llu%s\n", ::getpid(),
+                     size_t(base), size, (unsigned long long)id, (unsigned long long)e.serial,
+                     e.fresh ? "" : " (recycled handle: not published)");
     return dccl::ncclSuccess;
 }
 
@@ -341,23 +356,42 @@ ncclResult_t ensure_ipc_scratch(ProcCache& pc, IpcXport* x, size_t bytes) {
     if (bytes <= x->scratch_bytes) return dccl::ncclSuccess;
     size_t want = std::max({bytes, x->scratch_bytes + x->scratch_bytes / 2, kScratchMin});
     want = (want + kScratchPage - 1) / kScratchPage * kScratchPage;
+    // an allocation whose handle bytes are recycled (make_export) is kept until a fresh one is found, so the
+    // next allocation cannot be handed the same bytes, then freed
+    std::vector<void*> recycled;
     void* p = nullptr;
-    if (hipMalloc(&p, want) != hipSuccess) {
-        (void)hipGetLastError();
-        return dccl::ncclUnhandledCudaError;
+    ncclResult_t rc = dccl::ncclSuccess;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        if (hipMalloc(&p, want) != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+            rc = dccl::ncclUnhandledCudaError;
+            break;
+        }
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&base, &size, p) != hipSuccess || base != p) {  // the export is keyed by its base
+            (void)hipGetLastError();
+            recycled.push_back(p);
+            p = nullptr;
+            rc = dccl::ncclUnhandledCudaError;
+            break;
+        }
+        rc = make_export(pc, reinterpret_cast<uintptr_t>(base), size, buffer_id_of(base), 0);
+        if (rc != dccl::ncclSuccess) {
+            recycled.push_back(p);
+            p = nullptr;
+            break;
+        }
+        auto e = pc.exports.find(reinterpret_cast<uintptr_t>(base));
+        if (e->second.fresh) break;
+        pc.exports.erase(e);  // never published: nothing to retire
+        recycled.push_back(p);
+        p = nullptr;
+        rc = dccl::ncclInternalError;
     }
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    if (hipMemGetAddressRange(&base, &size, p) != hipSuccess || base != p) {  // the export is keyed by its base
-        (void)hipGetLastError();
-        (void)hipFree(p);
-        return dccl::ncclUnhandledCudaError;
-    }
-    const ncclResult_t rc = make_export(pc, reinterpret_cast<uintptr_t>(base), size, buffer_id_of(base), 0);
-    if (rc != dccl::ncclSuccess) {
-        (void)hipFree(p);
-        return rc;
-    }
+    for (void* q : recycled) (void)hipFree(q);
+    if (p == nullptr) return rc == dccl::ncclSuccess ? dccl::ncclInternalError : rc;
     if (x->scratch != nullptr) {
         auto old = pc.exports.find(reinterpret_cast<uintptr_t>(x->scratch));
         if (old != pc.exports.end()) drop_export(pc, old);
@@ -445,6 +479,15 @@ ncclResult_t plan_ipc(dcclComm* c, Publish* pub, hipStream_t st) {
     x->old_scratch.clear();
     auto in_e = pub->in ? find_registered(pc, pub->in, pub->in_bytes) : pc.exports.end();
     auto out_e = pub->out ? find_registered(pc, pub->out, pub->out_bytes) : pc.exports.end();
+    // a registration whose handle bytes are recycled is never published: through the scratch instead
+    if (in_e != pc.exports.end() && !in_e->second.fresh) {
+        ++pc.registered_fallbacks;
+        in_e = pc.exports.end();
+    }
+    if (out_e != pc.exports.end() && !out_e->second.fresh) {
+        ++pc.registered_fallbacks;
+        out_e = pc.exports.end();
+    }
     pub->in_scratch = pub->in != nullptr && in_e == pc.exports.end();
     pub->out_scratch = pub->out != nullptr && out_e == pc.exports.end();
     // `out` in the scratch shares it with `in` (the all_reduce combines in place there)
@@ -700,64 +743,16 @@ ncclResult_t ipc_register(void* buffer, size_t size) {
     return dccl::ncclSuccess;
 }
 
-namespace {
-
-// Wait until every live peer of every IPC communicator of this process has applied this process's
-// retirements written so far (ShmSlot::acked): then no peer maps a retired export any more, and the caller
-// may free the memory behind it.  The peers' own retirements are applied meanwhile (peers deregistering
-// at the same time wait for this process); a peer in a barrier applies them within ~0.1 s.  Called with
-// pc.mu held through `lock`, which it releases while it sleeps.  DCCL_IPC_DEREG_WAIT=0 skips it (A/B only).
-ncclResult_t wait_acked(ProcCache& pc, std::unique_lock<std::mutex>& lock) {
-    static const bool on = [] {
-        const char* v = std::getenv("DCCL_IPC_DEREG_WAIT");
-        return v == nullptr || *v != '0';
-    }();
-    if (!on) return dccl::ncclSuccess;
-    double timeout_s = 0;
-    for (IpcXport* x : pc.xports) timeout_s = std::max(timeout_s, x->timeout_s);
-    const auto start = std::chrono::steady_clock::now();
-    auto next_liveness = start + std::chrono::milliseconds(100);
-    std::vector<char> dead;
-    for (;;) {
-        apply_retirements(pc);
-        const auto now = std::chrono::steady_clock::now();
-        const bool check_live = now > next_liveness;
-        if (check_live) next_liveness = now + std::chrono::milliseconds(100);
-        bool done = true;
-        for (IpcXport* x : pc.xports) {
-            const uint64_t mine = x->ctl->slot[x->rank].retired_n.load(std::memory_order_acquire);
-            for (uint32_t p = 0; p < x->world; ++p) {
-                const ShmSlot& s = x->ctl->slot[p];
-                if (p == x->rank || s.acked[x->rank].load(std::memory_order_acquire) >= mine) continue;
-                if (check_live && !peer_alive(s)) continue;  // gone: its mappings went with it
-                done = false;
-            }
-        }
-        if (done) return dccl::ncclSuccess;
-        if (std::chrono::duration<double>(now - start).count() > timeout_s) return dccl::ncclSystemError;
-        lock.unlock();
-        if (now - start < std::chrono::milliseconds(2)) std::this_thread::yield();
-        else std::this_thread::sleep_for(std::chrono::microseconds(50));
-        lock.lock();
-    }
-}
-
-}  // namespace
-
-// dcclDeregisterCacheMemory: the export ends now (every peer is told through the segments), and the call
-// returns once every peer has closed its mapping of it, so the caller may free the buffer right away: a
-// peer still mapping a freed allocation is what made the runtime hand out stale memory for a new one at
-// the same address.
+// dcclDeregisterCacheMemory: the export ends now; every peer closes its mapping before it maps anything new.
 ncclResult_t ipc_deregister(void* buffer) {
     ProcCache& pc = cache();
-    std::unique_lock<std::mutex> lock(pc.mu);
+    std::lock_guard<std::mutex> lock(pc.mu);
     auto r = pc.ranges.find(reinterpret_cast<uintptr_t>(buffer));
     if (r == pc.ranges.end()) return dccl::ncclInvalidArgument;
     auto e = pc.exports.find(r->second.base);
     pc.ranges.erase(r);
-    if (e == pc.exports.end() || --e->second.regs != 0) return dccl::ncclSuccess;
-    drop_export(pc, e);
-    return wait_acked(pc, lock);
+    if (e != pc.exports.end() && --e->second.regs == 0) drop_export(pc, e);
+    return dccl::ncclSuccess;
 }
 
 int ipc_stats(uint64_t* out, int n) {
@@ -767,7 +762,8 @@ int ipc_stats(uint64_t* out, int n) {
     const uint64_t v[] = {pc.exports_made, pc.retirements, pc.registered_hits, pc.scratch_copies, pc.scratch_bytes,
                           pc.scratch_grows, pc.stale_registrations, s.opened, s.reused, s.retired, s.retired_pid,
                           s.trimmed, s.alias_evicted, s.alias_errors, s.open_retries, s.size_mismatch,
-                          uint64_t(pc.imports.size()), uint64_t(pc.imports.bytes())};
+                          uint64_t(pc.imports.size()), uint64_t(pc.imports.bytes()), pc.recycled_handles,
+                          pc.registered_fallbacks};
     const int m = std::min<int>(n, int(sizeof(v) / sizeof(v[0])));
     for (int i = 0; i < m; ++i) out[i] = v[i];
     return int(sizeof(v) / sizeof(v[0]));

@@ -162,7 +162,7 @@ public:
     // The exporter ended export (pid, serial): close its mapping now, or with its last use.
     void retire(int64_t pid, uint64_t serial) {
         auto it = map_.find(Key{pid, serial});
-        if (it == map_.end()) return;
+        if (it == map_.end() || it->second.retired) return;
         ++stats.retired;
         if (it->second.users == 0) close_entry(it);
         else it->second.retired = true;
@@ -173,7 +173,7 @@ public:
         ++stats.retired_pid;
         for (auto it = map_.begin(); it != map_.end();) {
             auto next = std::next(it);
-            if (it->first.pid == pid) {
+            if (it->first.pid == pid && !it->second.retired) {
                 if (it->second.users == 0) close_entry(it);
                 else it->second.retired = true;
             }

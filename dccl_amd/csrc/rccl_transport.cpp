@@ -102,4 +102,20 @@ int rccl_fan(void* rcomm, bool send, void* const* bufs, size_t bytes, uint32_t w
     return r != 0 ? r : re;
 }
 
+int rccl_exchange_all(void* rcomm, const void* const* sendbufs, void* const* recvbufs, size_t bytes, uint32_t world,
+                      uint32_t self, hipStream_t stream) {
+    const RcclApi& a = api();
+    if (!a.ok) return kSystem;
+    auto c = static_cast<ncclComm_t>(rcomm);
+    int r = rc(a.group_start());
+    if (r != 0) return r;
+    for (uint32_t p = 0; p < world && r == 0 && bytes; ++p) {
+        if (p == self) continue;
+        if (sendbufs[p] != nullptr) r = rc(a.send(sendbufs[p], bytes, ncclUint8, int(p), c, stream));
+        if (r == 0 && recvbufs[p] != nullptr) r = rc(a.recv(recvbufs[p], bytes, ncclUint8, int(p), c, stream));
+    }
+    const int re = rc(a.group_end());  // always close the group
+    return r != 0 ? r : re;
+}
+
 }  // namespace dccl_amd

@@ -32,5 +32,11 @@ int rccl_exchange(void* rcomm, const void* sendbuf, size_t send_bytes, uint32_t 
 // (broadcast; the gather to the root of ncclReduce, dccl.cpp:803-840) instead of one after another.
 int rccl_fan(void* rcomm, bool send, void* const* bufs, size_t bytes, uint32_t world, uint32_t self,
              hipStream_t stream);
+// Every pairwise transfer of one step in ONE group: `bytes` from sendbufs[p] to rank p and from rank p into
+// recvbufs[p], for every p != self (a null buffer skips that side), enqueued on `stream`: on the fully
+// connected xGMI mesh the W - 1 peers' transfers use W - 1 links at once (the grouped collectives of
+// algorithms.hpp).
+int rccl_exchange_all(void* rcomm, const void* const* sendbufs, void* const* recvbufs, size_t bytes, uint32_t world,
+                      uint32_t self, hipStream_t stream);
 
 }  // namespace dccl_amd

@@ -514,82 +514,87 @@ __global__ __launch_bounds__(64) void reduce_chain_phased_kernel(SendList sends,
 // ---------------------------------------------------------------------------------
 // k-way and chain combines into a destination that is not element-aligned (reduce_unaligned_kernel's
 // scheme for K operands): lane i's window is the 16 bytes of elements [V i, V i + V) at the destination's
-// own address (one unaligned 16-B load and store, gfx950), every operand read through ld_phased at its
-// own byte phase.  Consecutive tiles on one XCD, grid a multiple of 8.  A window and the bytes lane i
-// reads for it through ld_phased belong to lane i alone, so own may alias dst.  The tail (< V elements)
-// is block 0's, element by element.
+// own address (one unaligned 16-B store, gfx950); every operand -- the sources, then `own` (chain) or the
+// destination's own window (k-way) -- is read at its own byte phase through aligned loads, the lane
+// exchange and the funnel shift, one operand at a time.  A window and the bytes lane i reads for it belong
+// to lane i alone, so own may alias dst.  Round 4: the host passes every operand's 16-B
+// aligned base and phase (WindowArgs), the tile order is a template parameter, and tiles whose every vector
+// (and lane 63's extra one) lies inside the body take a path without bounds checks; the tail (< V
+// elements) is block 0's, element by element.  Grid: a multiple of 8 (the XCD / group orders).
 // ---------------------------------------------------------------------------------
-template <typename T, int OP, int K, bool FIRST = false>
-__global__ __launch_bounds__(64) void reduce_multi_unaligned_kernel(SendList sends, PhaseList ph,
-                                                                    unsigned char* __restrict__ recv, size_t nvec,
-                                                                    size_t count, int order) {
-    const size_t g = gridDim.x;
-    const unsigned pr = unsigned(reinterpret_cast<uintptr_t>(recv) & 15);
-    for (size_t t = tile_order(order, blockIdx.x, g); t * 64 < nvec; t += g) {
-        const size_t i = t * 64 + threadIdx.x;
-        const PhasedLoad xr = ld_phased_issue(recv, pr, i, nvec);  // recv's window, as reduce_unaligned_kernel
-        u32x4 acc;
-        if constexpr (FIRST) {  // every source's loads, then the shifts
-            PhasedLoad x[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) x[k] = ld_phased_issue(sends.p[k], ph.p[k], i, nvec);
-            acc = ld_phased_finish(xr, pr);
-#pragma unroll
-            for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, ld_phased_finish(x[k], ph.p[k]));
-        } else {  // one source at a time
-            u32x4 s[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k], ph.p[k], i, nvec);
-            acc = ld_phased_finish(xr, pr);
-#pragma unroll
-            for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, s[k]);
-        }
-        if (i < nvec) __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_u*>(recv + 16 * i));
-    }
-    if (blockIdx.x == 0)
-        for (size_t j = nvec * Pack<T>::N + threadIdx.x; j < count; j += 64) {
-            T acc = ld_elem<T, false>(recv, j);
-#pragma unroll
-            for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, false>(sends.p[k], j));
-            st_elem<T, false>(recv, j, acc);
-        }
+struct WindowArgs {
+    const u32x4* a[9];  // 16-B aligned base of each operand's window stream: sources, then own / the destination
+    unsigned p[9];      // its byte phase, 0..15
+    const unsigned char* src[8];  // the sources' bytes (tail elements)
+    const unsigned char* own;     // chain: own's bytes; k-way: the destination's
+    unsigned char* dst;
+    size_t nvec, count;
+};
+
+template <int ORDER>
+__device__ __forceinline__ size_t first_tile(size_t b, size_t g) {
+    if constexpr (ORDER == kOrderXcd) return (b % 8) * (g / 8) + b / 8;
+    else if constexpr (ORDER == kOrderBlock) return b;
+    else return xcd_group_tile(b, g);
 }
 
-// Chain order as reduce_chain_vec_kernel; ph.p[K] is own's phase.
-template <typename T, int OP, int K, bool FIRST = false>
-__global__ __launch_bounds__(64) void reduce_chain_unaligned_kernel(SendList sends, PhaseList ph,
-                                                                    const unsigned char* own, unsigned char* dst,
-                                                                    size_t nvec, size_t count, int order) {
+// One operand's window for vector v (the 16 bytes at byte phase p past aligned vector a[v]); all 64 lanes
+// call it (p is uniform).  FULL: v and lane 63's extra vector v + 1 lie inside the body (no bounds checks).
+template <bool FULL>
+__device__ __forceinline__ u32x4 ld_window(const u32x4* a, unsigned p, size_t v, size_t nvec) {
+    u32x4 lo = {0u, 0u, 0u, 0u}, ex = {0u, 0u, 0u, 0u};
+    if (FULL || (p != 0 ? v <= nvec : v < nvec)) lo = __builtin_nontemporal_load(a + v);
+    if (p == 0) return lo;
+    if ((threadIdx.x & 63) == 63 && (FULL || v < nvec)) ex = a[v + 1];
+    const u32x4 hi = from_next_lane_or(lo, ex);
+    const unsigned b = p & 3;
+    switch (p >> 2) {  // uniform
+    case 0: return funnel16<0>(lo, hi, b);
+    case 1: return funnel16<1>(lo, hi, b);
+    case 2: return funnel16<2>(lo, hi, b);
+    default: return funnel16<3>(lo, hi, b);
+    }
+}
+
+template <typename T, int OP, int K, bool CHAIN, bool FULL>
+__device__ __forceinline__ void window_tile(const WindowArgs& A, size_t t) {
+    const size_t v = t * 64 + threadIdx.x;
+    u32x4 acc;
+    if constexpr (CHAIN) {  // dst = op(own, op(s{K-1}, ... op(s1, s0)))
+        acc = ld_window<FULL>(A.a[0], A.p[0], v, A.nvec);
+#pragma unroll
+        for (int k = 1; k < K; ++k) acc = combine16<T, OP>(ld_window<FULL>(A.a[k], A.p[k], v, A.nvec), acc);
+        acc = combine16<T, OP>(ld_window<FULL>(A.a[K], A.p[K], v, A.nvec), acc);
+    } else {  // recv = op(...op(op(recv, s0), s1)..., s{K-1})
+        acc = ld_window<FULL>(A.a[K], A.p[K], v, A.nvec);
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, ld_window<FULL>(A.a[k], A.p[k], v, A.nvec));
+    }
+    if (FULL || v < A.nvec) __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_u*>(A.dst + 16 * v));
+}
+
+template <typename T, int OP, int K, bool CHAIN, int ORDER>
+__global__ __launch_bounds__(64) void reduce_windows_kernel(WindowArgs A) {
     const size_t g = gridDim.x;
-    for (size_t t = tile_order(order, blockIdx.x, g); t * 64 < nvec; t += g) {
-        const size_t i = t * 64 + threadIdx.x;
-        u32x4 acc, o;
-        if constexpr (FIRST) {  // every operand's loads, then the shifts
-            PhasedLoad x[K + 1];
-#pragma unroll
-            for (int k = 0; k < K; ++k) x[k] = ld_phased_issue(sends.p[k], ph.p[k], i, nvec);
-            x[K] = ld_phased_issue(own, ph.p[K], i, nvec);
-            acc = ld_phased_finish(x[0], ph.p[0]);
-#pragma unroll
-            for (int k = 1; k < K; ++k) acc = combine16<T, OP>(ld_phased_finish(x[k], ph.p[k]), acc);
-            o = ld_phased_finish(x[K], ph.p[K]);
-        } else {
-            u32x4 s[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k], ph.p[k], i, nvec);
-            o = ld_phased(own, ph.p[K], i, nvec);
-            acc = s[0];
-#pragma unroll
-            for (int k = 1; k < K; ++k) acc = combine16<T, OP>(s[k], acc);
-        }
-        if (i < nvec) __builtin_nontemporal_store(combine16<T, OP>(o, acc), reinterpret_cast<u32x4_u*>(dst + 16 * i));
+    const size_t ntiles = (A.nvec + 63) / 64;
+    for (size_t t = first_tile<ORDER>(blockIdx.x, g); t < ntiles; t += g) {
+        if ((t + 1) * 64 < A.nvec) window_tile<T, OP, K, CHAIN, true>(A, t);  // lane 63's extra vector inside too
+        else window_tile<T, OP, K, CHAIN, false>(A, t);
     }
     if (blockIdx.x == 0)
-        for (size_t j = nvec * Pack<T>::N + threadIdx.x; j < count; j += 64) {
-            T acc = ld_elem<T, false>(sends.p[0], j);
+        for (size_t j = A.nvec * Pack<T>::N + threadIdx.x; j < A.count; j += 64) {
+            T acc;
+            if constexpr (CHAIN) {
+                acc = ld_elem<T, false>(A.src[0], j);
 #pragma unroll
-            for (int k = 1; k < K; ++k) acc = Combine<T, OP>::apply(ld_elem<T, false>(sends.p[k], j), acc);
-            st_elem<T, false>(dst, j, Combine<T, OP>::apply(ld_elem<T, false>(own, j), acc));
+                for (int k = 1; k < K; ++k) acc = Combine<T, OP>::apply(ld_elem<T, false>(A.src[k], j), acc);
+                acc = Combine<T, OP>::apply(ld_elem<T, false>(A.own, j), acc);
+            } else {
+                acc = ld_elem<T, false>(A.own, j);
+#pragma unroll
+                for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, false>(A.src[k], j));
+            }
+            st_elem<T, false>(A.dst, j, acc);
         }
 }
 

@@ -1,5 +1,5 @@
 // dccl_amd/csrc/unaligned_multi.hip — the k-way and chain combines into a destination that is not
-// element-aligned (reduce_multi_unaligned_kernel / reduce_chain_unaligned_kernel in reduce_kernels.hpp).
+// element-aligned (reduce_windows_kernel in reduce_kernels.hpp).
 // Instantiated for every (T, OP) with sizeof(T) > 1 (a one-byte element is always aligned), in a
 // translation unit of its own, so the build compiles it beside local_reduce.hip.
 #include <hip/hip_runtime.h>
@@ -10,53 +10,69 @@
 namespace dccl_amd {
 namespace {
 
-// A grid that is a multiple of 8 (the kernels' XCD tile map); kMaxGrid is one.
+// A grid that is a multiple of 8 (the kernels' XCD / group tile maps); kMaxGrid is one.
 size_t unaligned_grid(size_t nvec) {
     const size_t g = ceil_div(ceil_div(nvec, size_t(64)), size_t(8)) * 8;
     return g == 0 ? 8 : g;
 }
 
-// Tile order: with every source at 16-B phase 0 (plain vector loads) one front for the chip wins, the
-// group-interleaved order up to k = 2 and block order above; sources at other phases keep consecutive tiles
-// on one XCD, where the vector lane 63 reads past its tile meets the next tile's first line in one L2.
-// 1 GiB fp32 Sum, destination + 2 B, one box (unaligned_forms_probe.py@4f20423, profiles/r3_s4_*): aligned sources
-// k = 2 80.0 -> 83.4 % (group), k = 4 74.6 -> 78.0 %, k = 8 71.7 -> 76.4 % (block); the chain the same.
+// Tile order (1 GiB fp32 Sum, destination + 2 B, tools/ab_unaligned.py, profiles/r4_s3_ab_unaligned.json):
+// with every source at 16-B phase 0 one front for the chip wins, the group-interleaved order up to k = 2
+// and block order above (k = 4 78.9 %, k = 8 79.8 %); sources at other phases want consecutive tiles in one
+// L2 (the lane-63 extra vector is the next tile's first): XCD ranges up to k = 4 (76.2 %), the
+// group-interleaved order above (k = 8 75.2 % against 72.0 % with XCD ranges).
 int unaligned_order(const PhaseList& ph, int nsend) {
     for (int k = 0; k < nsend; ++k)
-        if (ph.p[k] != 0) return kOrderXcd;
+        if (ph.p[k] != 0) return nsend <= 4 ? kOrderXcd : kOrderGroup;
     return nsend <= 2 ? kOrderGroup : kOrderBlock;
 }
 
-template <typename T, int OP, int K>
-int launch_multi(SendList sl, PhaseList ph, unsigned char* r, size_t count, hipStream_t stream) {
-    size_t nvec = count / Pack<T>::N;
-    int order = unaligned_order(ph, K);
-    void* args[] = {&sl, &ph, &r, &nvec, &count, &order};
-    return launch(reinterpret_cast<const void*>(&reduce_multi_unaligned_kernel<T, OP, K>), unaligned_grid(nvec), args,
-                  stream, 64);
-}
-
-template <typename T, int OP, int K>
-int launch_chain(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, size_t count,
-                 hipStream_t stream) {
-    size_t nvec = count / Pack<T>::N;
-    int order = unaligned_order(ph, K);  // the sources' phases decide; own is the destination's window
-    void* args[] = {&sl, &ph, &own, &d, &nvec, &count, &order};
-    return launch(reinterpret_cast<const void*>(&reduce_chain_unaligned_kernel<T, OP, K>), unaligned_grid(nvec), args,
-                  stream, 64);
+template <typename T, int OP, int K, bool CHAIN>
+int launch_windows(const SendList& sl, const PhaseList& ph, const unsigned char* own, unsigned char* d, size_t count,
+                   hipStream_t stream) {
+    WindowArgs A{};
+    for (int k = 0; k < K; ++k) {
+        A.p[k] = ph.p[k];
+        A.a[k] = reinterpret_cast<const u32x4*>(sl.p[k] - ph.p[k]);
+        A.src[k] = sl.p[k];
+    }
+    const unsigned char* w = CHAIN ? own : d;  // the last window: own (chain) or the destination's own (k-way)
+    A.p[K] = phase_word(w, 0);
+    A.a[K] = reinterpret_cast<const u32x4*>(w - A.p[K]);
+    A.own = w;
+    A.dst = d;
+    A.nvec = count / Pack<T>::N;
+    A.count = count;
+    void* args[] = {&A};
+    const size_t grid = unaligned_grid(A.nvec);
+    switch (unaligned_order(ph, K)) {
+    case kOrderXcd:
+        return launch(reinterpret_cast<const void*>(&reduce_windows_kernel<T, OP, K, CHAIN, kOrderXcd>), grid, args,
+                      stream, 64);
+    case kOrderBlock:
+        return launch(reinterpret_cast<const void*>(&reduce_windows_kernel<T, OP, K, CHAIN, kOrderBlock>), grid, args,
+                      stream, 64);
+    default:
+        return launch(reinterpret_cast<const void*>(&reduce_windows_kernel<T, OP, K, CHAIN, kOrderGroup>), grid, args,
+                      stream, 64);
+    }
 }
 
 }  // namespace
 
 template <typename T, int OP>
 int multi_unaligned_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, size_t count, hipStream_t stream) {
-    return with_k<2, 8>(nsend, [&](auto K) { return launch_multi<T, OP, K.value>(sl, ph, r, count, stream); });
+    return with_k<2, 8>(nsend, [&](auto K) {
+        return launch_windows<T, OP, K.value, false>(sl, ph, nullptr, r, count, stream);
+    });
 }
 
 template <typename T, int OP>
 int chain_unaligned_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d,
                           size_t count, hipStream_t stream) {
-    return with_k<1, 8>(nsend, [&](auto K) { return launch_chain<T, OP, K.value>(sl, ph, own, d, count, stream); });
+    return with_k<1, 8>(nsend, [&](auto K) {
+        return launch_windows<T, OP, K.value, true>(sl, ph, own, d, count, stream);
+    });
 }
 
 #define DCCL_UNALIGNED_INST_OP(T, OP)                                                                             \

@@ -40,13 +40,17 @@
  *                         grows, stale registrations dropped, mappings opened, mappings reused, mappings
  *                         closed on retirement, retirement-log overflows, mappings trimmed, alias
  *                         evictions, alias errors, open retries, size mismatches, mappings open, bytes
- *                         mapped.  Fills min(n, count) values; returns count.
+ *                         mapped, exports with recycled handle bytes (never published), registered buffers
+ *                         sent through the scratch for that reason.  Fills min(n, count) values; returns
+ *                         count.
  *   dccl_bootstrap_unique_id  single-node exchange of the RCCL id through DCCL_BOOTSTRAP_DIR: rank 0
  *                         creates and publishes it, the others wait (DCCL_BOOTSTRAP_TIMEOUT_S, default
  *                         120 s) for a file published by a LIVE rank 0 of the same world size, so a
  *                         file an earlier job left behind is never taken (what ncclCommInit does
  *                         with DCCL_TRANSPORT=rccl).  A second call under the same tag waits for a new
- *                         publication: a rank never takes the id it already took
+ *                         publication: a rank never takes the id it already took, and the file is removed
+ *                         as soon as every reader rank took it, so a process started later never takes a
+ *                         formed group's id (even without dccl_bootstrap_done)
  *   dccl_bootstrap_done   rank 0 removes the published id once dccl_comm_init_rccl returned (every rank
  *                         has read it then), as ncclCommInit does; other ranks: no-op
  *   dccl_all_reduce       ncclAllReduce       (/root/reference/include/dccl/dccl.hpp:206-207)

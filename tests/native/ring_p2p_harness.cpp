@@ -10,7 +10,10 @@
 //
 //   ring_p2p_harness <algo> <world> <count> <dtype> <op> <outdir>
 //     algo: rs (reduce_scatter_ring, identity maps) | rs_api (ncclReduceScatter's maps) |
-//           ag (all_gather_ring) | ar (all_reduce_ring) | rab (all_reduce_rabenseifner)
+//           ag (all_gather_ring) | ar (all_reduce_ring) | rab (all_reduce_rabenseifner) |
+//           grs / grs_api / gar (reduce_scatter_grouped shift 1 / 0, all_reduce_grouped: grouped.cpp, with the
+//           grouped RCCL exchange faked on the same mailboxes and the chain combine done by the oracle)
+//   grs / grs_api leave the owned slot's result in place ((r + 1) % W, resp. r), as the ring does.
 //   rank r's buffer starts as oracle_synth_fill(seed 0xDCC1, buffer_id r); <outdir>/rank<r>.bin gets the
 //   final buffer; stdout gets one JSON line: {"rc": [...], "log": [[[to, from, send_off, recv_off,
 //   send_bytes, recv_bytes], ...] per rank]} with offsets relative to the rank's buffer (-1: the
@@ -46,18 +49,39 @@ ncclResult_t xport_recv_combine(dccl::dcclComm*, uint32_t, void*, size_t, int, i
     return dccl::ncclInternalError;
 }
 ncclResult_t ensure_scratch(dccl::dcclComm* c, size_t bytes, bool device) {
-    if (device) return dccl::ncclInternalError;
-    if (c->host_scratch_bytes >= bytes) return dccl::ncclSuccess;
-    std::free(c->host_scratch);
-    c->host_scratch = std::aligned_alloc(64, (bytes + 63) / 64 * 64);
-    c->host_scratch_bytes = bytes;
-    return c->host_scratch ? dccl::ncclSuccess : dccl::ncclSystemError;
+    void*& pad = device ? c->dev_scratch : c->host_scratch;  // "device" memory is host memory here
+    size_t& have = device ? c->dev_scratch_bytes : c->host_scratch_bytes;
+    if (have >= bytes) return dccl::ncclSuccess;
+    std::free(pad);
+    pad = std::aligned_alloc(64, (bytes + 63) / 64 * 64);
+    have = bytes;
+    return pad ? dccl::ncclSuccess : dccl::ncclSystemError;
 }
 ncclResult_t combine(const void* send, void* recv, int dtype, size_t count, int op, bool device, hipStream_t) {
     if (device) return dccl::ncclInternalError;
     return static_cast<ncclResult_t>(oracle_expected_reduce(send, recv, count, dtype, op));
 }
+int rccl_exchange_all(void* rcomm, const void* const* sendbufs, void* const* recvbufs, size_t bytes, uint32_t world,
+                      uint32_t self, hipStream_t stream);  // below: the fake exchange's grouped form
 }  // namespace dccl_amd
+
+// dccl_local_reduce_chain on host memory: dst = op(own, op(s{k-1}, ... op(s1, s0))), every application
+// op(recv = the next part, send = the partial so far), as reduce_scatter_ring.cpp:84-94 applies it.
+extern "C" int dccl_local_reduce_chain(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
+                                       size_t count, int op, void*) {
+    const size_t bytes = count * dccl_amd::size_of_dtype(dtype);
+    std::vector<unsigned char> acc(static_cast<const unsigned char*>(sends[0]),
+                                   static_cast<const unsigned char*>(sends[0]) + bytes);
+    for (int k = 1; k <= nsend; ++k) {
+        const auto* part = static_cast<const unsigned char*>(k < nsend ? sends[k] : own);
+        std::vector<unsigned char> next(part, part + bytes);
+        const int rc = oracle_expected_reduce(acc.data(), next.data(), count, dtype, op);
+        if (rc != 0) return rc;
+        acc.swap(next);
+    }
+    std::memcpy(dst, acc.data(), bytes);
+    return 0;
+}
 
 namespace {
 
@@ -110,6 +134,23 @@ int fake_exchange(void* ctx, const void* sendbuf, size_t send_bytes, uint32_t to
 
 }  // namespace
 
+// The grouped exchange on the same mailboxes: every send first, then every receive (one log entry per peer).
+int dccl_amd::rccl_exchange_all(void* rcomm, const void* const* sendbufs, void* const* recvbufs, size_t bytes,
+                                uint32_t world, uint32_t self, hipStream_t) {
+    auto* e = static_cast<Endpoint*>(rcomm);
+    for (uint32_t p = 0; p < world; ++p)
+        if (p != self) {
+            const int rc = fake_exchange(e, sendbufs[p], sendbufs[p] ? bytes : 0, p, nullptr, 0, 0, nullptr);
+            if (rc != 0) return rc;
+        }
+    for (uint32_t p = 0; p < world; ++p)
+        if (p != self) {
+            const int rc = fake_exchange(e, nullptr, 0, 0, recvbufs[p], recvbufs[p] ? bytes : 0, p, nullptr);
+            if (rc != 0) return rc;
+        }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc != 7) {
         std::fprintf(stderr, "usage: %s algo world count dtype op outdir\n", argv[0]);
@@ -134,6 +175,7 @@ int main(int argc, char** argv) {
         comms[r].p2p = &fake_exchange;
         comms[r].p2p_ctx = &eps[r];
         comms[r].p2p_host = true;
+        comms[r].rccl = &eps[r];  // read by grouped.cpp only, as the fake rccl_exchange_all's context
         eps[r] = Endpoint{&net, &comms[r], r, bufs[r].data(), count * esz, {}};
     }
     const dccl_amd::RankMap id = [](uint32_t x) { return x; };
@@ -155,6 +197,12 @@ int main(int argc, char** argv) {
                 rc = dccl_amd::all_reduce_ring(c, b, nullptr, count, dtype, op, false, nullptr);
             } else if (algo == "rab") {
                 rc = dccl_amd::all_reduce_rabenseifner(c, b, nullptr, count, dtype, op, false, nullptr);
+            } else if (algo == "grs" || algo == "grs_api") {  // the owned slot's result in place, like the ring
+                const uint32_t shift = algo == "grs" ? 1 : 0;
+                unsigned char* mine = static_cast<unsigned char*>(b) + ((r + shift) % W) * (count / W) * esz;
+                rc = dccl_amd::reduce_scatter_grouped(c, b, mine, count, dtype, op, nullptr, shift);
+            } else if (algo == "gar") {
+                rc = dccl_amd::all_reduce_grouped(c, b, b, count, dtype, op, nullptr);
             }
             rcs[r] = static_cast<int>(rc);
         });
@@ -168,6 +216,8 @@ int main(int argc, char** argv) {
         std::fclose(f);
         std::free(comms[r].host_scratch);
         comms[r].host_scratch = nullptr;
+        std::free(comms[r].dev_scratch);
+        comms[r].dev_scratch = nullptr;
     }
     std::printf("{\"rc\": [");
     for (uint32_t r = 0; r < W; ++r) std::printf("%s%d", r ? ", " : "", rcs[r]);

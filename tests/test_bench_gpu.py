@@ -133,6 +133,11 @@ def test_bench_rccl_two_ranks_one_gpu():
         assert s["dccl_allgather"][name]["bit_exact"], s
     assert s["fp32_direct_bit_exact_vs_ring"] and s["rccl"]["ms"] > 0, s
     assert s["c5_allgather"]["direct"]["bit_exact"], s
+    # round 4: the grouped RCCL all-reduce, the registered IPC path and the transport's counters
+    assert s["fp32_grouped_bit_exact_vs_ring"] and s["grouped"]["int32_sum_bit_exact_vs_rccl"], s
+    assert s["direct"]["registered_fp32_bit_exact_vs_scratch"] and s["direct"]["registered_ms"] > 0, s
+    assert s["ipc_stats"]["alias_errors"] == 0 and s["ipc_stats"]["scratch_copies"] > 0, s
+    assert s["dccl_allgather"]["direct"]["wrong_slices_all_ranks"] == 0, s
 
 
 def test_bench_single_gpu_line():

@@ -163,7 +163,7 @@ def test_chain_mixed_phases(gpu, dt):
 @pytest.mark.parametrize("dt", [2, 4, 6, 7, 8, 9])
 def test_chain_byte_offsets(gpu, dt):
     """Sends and own at any byte address (phased chain kernel with byte phases) into a dst that is
-    element-aligned or not (reduce_chain_unaligned_kernel), separate and in place (own == dst at a byte
+    element-aligned or not (reduce_windows_kernel), separate and in place (own == dst at a byte
     offset), against the ring-order oracle; nothing outside dst written."""
     import dccl_amd
     from tests.test_gpu_parity import rand_inputs, dev_bytes, host_of
@@ -466,8 +466,11 @@ def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold, reg):
     `two`: two communicators of the same ranks share the process's mappings (a stale mapping one of them still
     held used to shadow the other's re-import).  `reg`: the buffers are registered every round (peers map
     them in place, and every deregistration retires an export); otherwise inputs reach the peers through
-    each communicator's scratch, which is exported once.  Either way no mapping may alias another
-    (alias_errors == 0 in every process)."""
+    each communicator's scratch, which is exported once.  A registration whose handle bytes once named another
+    (freed) allocation of its process is never published (it goes through the scratch): a peer that opens
+    such bytes again can be handed the freed allocation's pages even though it closed that mapping (round 4:
+    6 of 6 runs of the registered W = 2 case read stale data before this rule).  Either way no mapping may
+    alias another (alias_errors == 0 in every process)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     tag = "test_" + uuid.uuid4().hex[:12]
@@ -490,10 +493,11 @@ def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold, reg):
         bad, fin, stats, _ = results[r]
         assert not bad and fin == 0, (r, bad[:8], len(bad), fin, stats)
         assert stats["alias_errors"] == 0, (r, stats)
-        if reg:  # peers read the registered inputs in place: no scratch copy
-            assert stats["scratch_copies"] == 0 and stats["registered_hits"] >= rounds, (r, stats)
+        if reg:  # registered inputs: read in place, or through the scratch when their handle bytes are recycled
+            assert stats["registered_hits"] >= rounds, (r, stats)
+            assert stats["scratch_copies"] == stats["registered_fallbacks"], (r, stats)
         else:
-            assert stats["scratch_copies"] >= rounds, (r, stats)
+            assert stats["scratch_copies"] >= rounds and stats["registered_hits"] == 0, (r, stats)
 
 
 def _ipc_dying_rank(r, tag, q):

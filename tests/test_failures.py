@@ -142,13 +142,52 @@ def test_bootstrap_two_groups_same_tag_cpu(rdv):
     assert second.raw != first.raw
     rc, got = _read_id()
     assert rc == 0 and got == second.raw
-    # another reader rank of the same process takes the current publication once, too
+    # every reader of the world took it: the file is gone, nobody can take it again
+    assert not rdv.exists() and not list(rdv.parent.glob(rdv.name + ".took.*"))
     rc, got = _read_id(rank=1, world=2)
     assert rc == 2
-    assert dccl_amd.lib.dccl_bootstrap_done(1, 2) == 0 and rdv.exists()  # not rank 0: nothing removed
-    assert dccl_amd.lib.dccl_bootstrap_done(0, 2) == 0 and not rdv.exists()
+    # with more readers the file stays until the last one took it; dccl_bootstrap_done on rank 0 removes it
+    third = ctypes.create_string_buffer(128)
+    assert dccl_amd.lib.dccl_bootstrap_unique_id(0, 3, third) == 0
+    assert _read_id(world=3, rank=1) == (0, third.raw) and rdv.exists()
+    assert dccl_amd.lib.dccl_bootstrap_done(1, 3) == 0 and rdv.exists()  # not rank 0: nothing removed
+    assert dccl_amd.lib.dccl_bootstrap_done(0, 3) == 0 and not rdv.exists()
     assert _read_id()[0] == 2
     assert dccl_amd.lib.dccl_bootstrap_done(2, 2) == 4 and dccl_amd.lib.dccl_bootstrap_done(0, 0) == 4
+
+
+_READER = r'''
+import ctypes, json, os, sys
+sys.path.insert(0, os.environ["ROOT"])
+import dccl_amd
+buf = ctypes.create_string_buffer(128)
+rc = dccl_amd.lib.dccl_bootstrap_unique_id(1, 2, buf)
+print(json.dumps({"rc": rc, "id": buf.raw.hex()}))
+'''
+
+
+def test_bootstrap_fresh_process_never_takes_old_id_cpu(rdv):
+    """ADVICE r3: readers in separate processes.  Rank 0 publishes without ever calling dccl_bootstrap_done;
+    once its group's readers took the id, a freshly started process polling the same tag must not get it
+    (it would join a group that already formed); it gets the next publication."""
+    import json as _json
+    import dccl_amd
+    env = {**os.environ, "ROOT": os.path.dirname(os.path.dirname(os.path.abspath(__file__)))}
+
+    def reader():
+        p = subprocess.run([sys.executable, "-c", _READER], env=env, capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, p.stderr[-2000:]
+        return _json.loads(p.stdout.strip().splitlines()[-1])
+
+    first = ctypes.create_string_buffer(128)
+    assert dccl_amd.lib.dccl_bootstrap_unique_id(0, 2, first) == 0
+    got = reader()
+    assert got["rc"] == 0 and bytes.fromhex(got["id"]) == first.raw
+    assert reader()["rc"] == 2  # a new process: the old id is gone, it times out
+    second = ctypes.create_string_buffer(128)
+    assert dccl_amd.lib.dccl_bootstrap_unique_id(0, 2, second) == 0
+    got = reader()
+    assert got["rc"] == 0 and bytes.fromhex(got["id"]) == second.raw != first.raw
 
 
 def test_bootstrap_argument_checks_cpu():

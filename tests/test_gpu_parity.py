@@ -306,7 +306,7 @@ def test_multi_mixed_phases(dccl, k):
 @pytest.mark.parametrize("k", [2, 3, 5, 8])
 def test_multi_byte_offsets(dccl, k):
     """Sources at any byte address (phased kernel with byte phases, sources' head / tail read bytewise) and
-    recv at any byte address (reduce_multi_unaligned_kernel when recv is not element-aligned): every dtype
+    recv at any byte address (reduce_windows_kernel when recv is not element-aligned): every dtype
     wider than a byte, sizes around a tile, against the sequential oracle; nothing outside recv written."""
     rng = np.random.default_rng(1300 + k)
     for dt in [2, 3, 4, 5, 6, 7, 8, 9]:

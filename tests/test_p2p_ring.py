@@ -26,13 +26,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "build", "tests")
 HARNESS = os.path.join(OUT, "ring_p2p_harness")
 SRCS = [os.path.join(ROOT, "tests", "native", "ring_p2p_harness.cpp"),
-        os.path.join(ROOT, "dccl_amd", "csrc", "algorithms.cpp"), os.path.join(ROOT, "oracle", "host_reduce.c")]
+        os.path.join(ROOT, "dccl_amd", "csrc", "algorithms.cpp"), os.path.join(ROOT, "oracle", "host_reduce.c"),
+        os.path.join(ROOT, "dccl_amd", "csrc", "grouped.cpp")]
 SEED = 0xDCC1
 
 
 @pytest.fixture(scope="module")
 def harness():
-    deps = SRCS + [os.path.join(ROOT, "dccl_amd", "csrc", f) for f in ("algorithms.hpp", "comm.hpp", "dispatch.hpp")]
+    deps = SRCS + [os.path.join(ROOT, "dccl_amd", "csrc", f) for f in ("algorithms.hpp", "comm.hpp", "dispatch.hpp",
+                                                                        "rccl_transport.hpp")]
     if not os.path.exists(HARNESS) or os.path.getmtime(HARNESS) < max(os.path.getmtime(p) for p in deps):
         # Per-process scratch directory and an atomic rename: pytest-xdist workers may build at once.
         tmp = os.path.join(OUT, f"tmp.{os.getpid()}")
@@ -41,10 +43,12 @@ def harness():
                f"-I{ROOT}/include", f"-I{ROOT}/dccl_amd/csrc"]
         subprocess.run(hip + ["-c", SRCS[0], "-o", f"{tmp}/harness.o"], check=True)
         subprocess.run(hip + ["-c", SRCS[1], "-o", f"{tmp}/algorithms.o"], check=True)
+        subprocess.run(hip + ["-c", SRCS[3], "-o", f"{tmp}/grouped.o"], check=True)
         subprocess.run(["gcc", "-std=c11", "-O2", "-fPIC", "-c", SRCS[2], "-o", f"{tmp}/oracle_host_reduce.o"],
                        check=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", f"{tmp}/harness.o", f"{tmp}/algorithms.o",
-                        f"{tmp}/oracle_host_reduce.o", "-o", f"{tmp}/ring_p2p_harness", "-pthread"], check=True)
+                        f"{tmp}/grouped.o", f"{tmp}/oracle_host_reduce.o", "-o", f"{tmp}/ring_p2p_harness",
+                        "-pthread"], check=True)
         os.replace(f"{tmp}/ring_p2p_harness", HARNESS)
         shutil.rmtree(tmp, ignore_errors=True)
     return HARNESS
@@ -156,6 +160,51 @@ def test_p2p_branch_schedule_and_result_cpu(harness, tmp_path, W, algo):
         for r in range(W):
             assert log[r] == logs[r], (algo, W, r, log[r][:4], logs[r][:4])
             assert got[r].tobytes() == want[r].tobytes(), (algo, W, dt, op, r)
+
+
+def grouped_log(W, r, slot_bytes, shift, gather):
+    """grouped.cpp's exchanges: to every peer p its part of the slot p owns, then from every peer into the
+    scratch (offset -3: inside the scratch), in peer order; then, for the all-reduce, the owned slot to every
+    peer and every peer's owned slot into place."""
+    peers = [p for p in range(W) if p != r]
+    out = [[p, -1, slot_bytes * ((p + shift) % W), -2, slot_bytes, 0] for p in peers]
+    out += [[-1, p, -2, -3, 0, slot_bytes] for p in peers]
+    if gather:
+        out += [[p, -1, slot_bytes * ((r + 1) % W), -2, slot_bytes, 0] for p in peers]
+        out += [[-1, p, -2, slot_bytes * ((p + 1) % W), 0, slot_bytes] for p in peers]
+    return out
+
+
+@pytest.mark.parametrize("W", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("algo", ["grs", "grs_api", "gar"])
+def test_grouped_schedule_and_result_cpu(harness, tmp_path, W, algo):
+    """The grouped RCCL forms (grouped.cpp): every exchange (peer, offset, bytes) and every owned slot (all of the
+    all-reduce's buffer) bit-exact against the ring simulation: the chain applies the ring's operations in the
+    ring's order."""
+    for dt, op in CASES:
+        count = 840 * (1 + (dt % 3))
+        esz = oracle.NP_DTYPES[dt]().itemsize
+        slot = count // W
+        rc, log, got = run(harness, tmp_path, algo, W, count, dt, op)
+        assert rc == [0] * W, (algo, W, dt, op, rc)
+        want = inputs(W, count, dt, op)
+        comb = combine_with(dt, op)
+        if algo == "gar":
+            ringsim.ring_allreduce(want, comb, copy)
+        elif algo == "grs":
+            ringsim.reduce_scatter_ring(want, comb)
+        else:
+            tn, to = ringsim.rs_maps()
+            ringsim.reduce_scatter_ring(want, comb, tn, to)
+        shift = 0 if algo == "grs_api" else 1
+        for r in range(W):
+            assert log[r] == grouped_log(W, r, slot * esz, shift, algo == "gar"), (algo, W, r, log[r][:4])
+            if algo == "gar":
+                assert got[r].tobytes() == want[r].tobytes(), (algo, W, dt, op, r)
+            else:
+                m = (r + shift) % W
+                assert got[r][m * slot:(m + 1) * slot].tobytes() == want[r][m * slot:(m + 1) * slot].tobytes(), \
+                    (algo, W, dt, op, r)
 
 
 def test_p2p_branch_rejects_bad_counts_cpu(harness, tmp_path):

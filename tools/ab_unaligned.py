@@ -39,7 +39,7 @@ def cases(ptrs):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="11,10,111,110,211,210,21,41,121,141,221,241")
+    ap.add_argument("--variants", default="10,11,20,21,40,110,111,120,210,211,220")
     ap.add_argument("--cases", default="")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=10)

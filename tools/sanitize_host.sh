@@ -12,7 +12,7 @@ mkdir -p "$out"
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 flags=(-std=c++17 -O1 -g -fPIC "-Xarch_host" "-fsanitize=$kind" -I"$root/include" -I"$root/dccl_amd/csrc" --offload-arch=gfx950)
 objs=()
-for f in comm algorithms bootstrap dccl_api direct host_staged rccl_transport; do
+for f in comm algorithms grouped bootstrap dccl_api direct host_staged rccl_transport; do
   "$HIPCC" "${flags[@]}" -c "$root/dccl_amd/csrc/$f.cpp" -o "$out/$f.o"
   objs+=("$out/$f.o")
 done

@@ -8,10 +8,10 @@
 // operand, and a uniform 4-way switch per operand for the funnel shift.  The variants remove these:
 //   * the host passes each operand's 16-B aligned base and phase (UArgs), the order is a template parameter;
 //   * tiles whose every vector (and lane 63's extra vector) is inside the body take a path without bounds
-//     checks, with every operand's lane-63 extra load under ONE branch;
-//   * SEL: the funnel shift picks its words with selects instead of a uniform switch (phase 0 goes through
-//     the same code: alignbyte by 0 returns the low word);
-//   * TPW tiles per wave (consecutive), amortising the wave's set-up.
+//     checks;
+//   * U vectors per lane per operand (U = 1, 2, 4), so every per-operand branch (phase 0 or not, the lane-63
+//     extra loads, the funnel's 4-way switch) is paid once per U vectors; one operand at a time, as the
+//     product kernels (loading every operand first needs twice the VGPRs and lost in round 2).
 //
 //   extern "C" int uv4_combine(int variant, const void* const* sends, int k, const void* own, void* dst,
 //                              size_t count, void* stream)       own == nullptr: k-way into dst; else chain
@@ -38,92 +38,99 @@ __device__ __forceinline__ size_t first_tile(size_t b, size_t g) {
     else return xcd_group_tile(b, g);
 }
 
-// 16 bytes at byte offset p of the 32 bytes (lo, hi), without a branch on p
-__device__ __forceinline__ u32x4 funnel_sel(u32x4 lo, u32x4 hi, unsigned p) {
-    const unsigned d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    const bool q1 = (p & 4) != 0, q2 = (p & 8) != 0;
-    unsigned y[7], z[5];
+// One operand's 16-B windows for U vectors per lane (vectors base + u*64 + lane), through aligned loads, the
+// lane exchange and the funnel shift at the operand's phase p (uniform): branches on p once per operand per
+// U vectors.  FULL: every vector and lane 63's extra vector lie inside the body (no bounds checks).
+template <int U, bool FULL>
+__device__ __forceinline__ void load_windows(const u32x4* a, unsigned p, size_t base, size_t nvec, u32x4 (&s)[U]) {
+    const unsigned lane = threadIdx.x;
+    u32x4 lo[U], ex[U];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) y[j] = q1 ? d[j + 1] : d[j];
+    for (int u = 0; u < U; ++u) {
+        lo[u] = u32x4{0u, 0u, 0u, 0u};
+        ex[u] = u32x4{0u, 0u, 0u, 0u};
+        const size_t v = base + size_t(u) * 64 + lane;
+        if (FULL || (p != 0 ? v <= nvec : v < nvec)) lo[u] = __builtin_nontemporal_load(a + v);
+    }
+    if (p == 0) {
 #pragma unroll
-    for (int j = 0; j < 5; ++j) z[j] = q2 ? y[j + 2] : y[j];
+        for (int u = 0; u < U; ++u) s[u] = lo[u];
+        return;
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t v = base + size_t(u) * 64 + 63;
+            if (FULL || v < nvec) ex[u] = a[v + 1];
+        }
+    }
+    u32x4 hi[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) hi[u] = from_next_lane_or(lo[u], ex[u]);
     const unsigned b = p & 3;
-    u32x4 o;
-    o.x = __builtin_amdgcn_alignbyte(z[1], z[0], b);
-    o.y = __builtin_amdgcn_alignbyte(z[2], z[1], b);
-    o.z = __builtin_amdgcn_alignbyte(z[3], z[2], b);
-    o.w = __builtin_amdgcn_alignbyte(z[4], z[3], b);
-    return o;
-}
-
-__device__ __forceinline__ u32x4 funnel_sw(u32x4 lo, u32x4 hi, unsigned p) {
-    const unsigned b = p & 3;
-    switch (p >> 2) {
-    case 0: return funnel16<0>(lo, hi, b);
-    case 1: return funnel16<1>(lo, hi, b);
-    case 2: return funnel16<2>(lo, hi, b);
-    default: return funnel16<3>(lo, hi, b);
+    switch (p >> 2) {  // uniform, once per operand
+    case 0:
+#pragma unroll
+        for (int u = 0; u < U; ++u) s[u] = funnel16<0>(lo[u], hi[u], b);
+        break;
+    case 1:
+#pragma unroll
+        for (int u = 0; u < U; ++u) s[u] = funnel16<1>(lo[u], hi[u], b);
+        break;
+    case 2:
+#pragma unroll
+        for (int u = 0; u < U; ++u) s[u] = funnel16<2>(lo[u], hi[u], b);
+        break;
+    default:
+#pragma unroll
+        for (int u = 0; u < U; ++u) s[u] = funnel16<3>(lo[u], hi[u], b);
+        break;
     }
 }
 
-template <bool SEL>
-__device__ __forceinline__ u32x4 shifted(u32x4 lo, u32x4 ex, unsigned p) {
-    const u32x4 hi = from_next_lane_or(lo, ex);
-    return SEL ? funnel_sel(lo, hi, p) : funnel_sw(lo, hi, p);
-}
-
-// one tile: N = K + 1 operands (sources, then own / the destination's window)
-template <int K, bool CHAIN, bool SEL, bool FULL>
+// one tile of U * 64 vectors: the destination's window (multi) or the sources then own (chain), one operand
+// at a time, in the product kernels' association order
+template <int K, bool CHAIN, int U, bool FULL, bool SB>
 __device__ __forceinline__ void tile(const UArgs& A, size_t t) {
-    constexpr int N = K + 1;
-    const size_t v = t * 64 + threadIdx.x;
-    u32x4 lo[N], ex[N];
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        lo[k] = u32x4{0u, 0u, 0u, 0u};
-        ex[k] = u32x4{0u, 0u, 0u, 0u};
-    }
-    if constexpr (FULL) {
-#pragma unroll
-        for (int k = 0; k < N; ++k) lo[k] = __builtin_nontemporal_load(A.a[k] + v);
-        if (threadIdx.x == 63) {
-#pragma unroll
-            for (int k = 0; k < N; ++k) ex[k] = A.a[k][v + 1];
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < N; ++k) {
-            if (A.p[k] != 0 ? v <= A.nvec : v < A.nvec) lo[k] = __builtin_nontemporal_load(A.a[k] + v);
-            if (A.p[k] != 0 && threadIdx.x == 63 && v < A.nvec) ex[k] = A.a[k][v + 1];
-        }
-    }
-    u32x4 acc;
+    const size_t base = t * U * 64;
+    u32x4 acc[U], s[U];
     if constexpr (CHAIN) {
-        acc = shifted<SEL>(lo[0], ex[0], A.p[0]);
+        load_windows<U, FULL>(A.a[0], A.p[0], base, A.nvec, acc);
 #pragma unroll
-        for (int k = 1; k < K; ++k) acc = combine16<float, kSum>(shifted<SEL>(lo[k], ex[k], A.p[k]), acc);
-        acc = combine16<float, kSum>(shifted<SEL>(lo[K], ex[K], A.p[K]), acc);
+        for (int k = 1; k < K; ++k) {
+            load_windows<U, FULL>(A.a[k], A.p[k], base, A.nvec, s);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] = combine16<float, kSum>(s[u], acc[u]);
+            if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+        }
+        load_windows<U, FULL>(A.a[K], A.p[K], base, A.nvec, s);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = combine16<float, kSum>(s[u], acc[u]);
     } else {
-        acc = shifted<SEL>(lo[K], ex[K], A.p[K]);
+        load_windows<U, FULL>(A.a[K], A.p[K], base, A.nvec, acc);
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc = combine16<float, kSum>(acc, shifted<SEL>(lo[k], ex[k], A.p[k]));
+        for (int k = 0; k < K; ++k) {
+            load_windows<U, FULL>(A.a[k], A.p[k], base, A.nvec, s);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] = combine16<float, kSum>(acc[u], s[u]);
+            if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+        }
     }
-    if (FULL || v < A.nvec) __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_u*>(A.dst + 16 * v));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t v = base + size_t(u) * 64 + threadIdx.x;
+        if (FULL || v < A.nvec) __builtin_nontemporal_store(acc[u], reinterpret_cast<u32x4_u*>(A.dst + 16 * v));
+    }
 }
 
-template <int K, bool CHAIN, int ORDER, int TPW, bool SEL>
+template <int K, bool CHAIN, int ORDER, int U, bool SB>
 __global__ __launch_bounds__(64) void uv4_kernel(UArgs A) {
     const size_t g = gridDim.x;
-    const size_t ntiles = (A.nvec + 63) / 64;
-    // a full tile: lane 63's extra vector v + 1 is inside the body too
-    const size_t nfull = A.nvec >= 65 ? (A.nvec - 1) / 64 : 0;
-    for (size_t t0 = first_tile<ORDER>(blockIdx.x, g) * TPW; t0 < ntiles; t0 += g * TPW) {
-#pragma unroll
-        for (int j = 0; j < TPW; ++j) {
-            const size_t t = t0 + j;
-            if (t < nfull) tile<K, CHAIN, SEL, true>(A, t);
-            else if (t < ntiles) tile<K, CHAIN, SEL, false>(A, t);
-        }
+    const size_t span = size_t(U) * 64;
+    const size_t ntiles = (A.nvec + span - 1) / span;
+    for (size_t t = first_tile<ORDER>(blockIdx.x, g); t < ntiles; t += g) {
+        if ((t + 1) * span < A.nvec) tile<K, CHAIN, U, true, SB>(A, t);  // lane 63's extra vector inside too
+        else tile<K, CHAIN, U, false, SB>(A, t);
     }
     if (blockIdx.x == 0)
         for (size_t j = A.nvec * 4 + threadIdx.x; j < A.count; j += 64) {
@@ -142,31 +149,32 @@ __global__ __launch_bounds__(64) void uv4_kernel(UArgs A) {
         }
 }
 
-template <int K, bool CHAIN, int ORDER, int TPW, bool SEL>
+template <int K, bool CHAIN, int ORDER, int U, bool SB>
 int launch_v(const UArgs& A, hipStream_t st) {
-    const size_t ntiles = (A.nvec + 63) / 64;
-    size_t g = ceil_div(ceil_div(ntiles, size_t(TPW)), size_t(8)) * 8;
+    const size_t ntiles = ceil_div(A.nvec, size_t(U) * 64);
+    size_t g = ceil_div(ntiles, size_t(8)) * 8;
     if (g == 0) g = 8;
     UArgs a = A;
     void* args[] = {&a};
-    return launch(reinterpret_cast<const void*>(&uv4_kernel<K, CHAIN, ORDER, TPW, SEL>), g, args, st, 64);
+    return launch(reinterpret_cast<const void*>(&uv4_kernel<K, CHAIN, ORDER, U, SB>), g, args, st, 64);
 }
 
-// variant = 100 * order + 10 * tpw + sel   (order 0 xcd, 1 block, 2 group; tpw 1, 2, 4; sel 0 switch, 1 select)
+// variant = 100 * order + 10 * U + sb   (order 0 xcd, 1 block, 2 group; U 1, 2, 4 vectors per lane; sb 1: a
+// scheduling barrier between operands, so the compiler cannot hoist every operand's loads to the top)
 template <int K, bool CHAIN>
 int dispatch(int variant, const UArgs& A, hipStream_t st) {
-    const int order = variant / 100, tpw = (variant / 10) % 10;
-    const bool sel = variant % 10 != 0;
-    auto by_tpw = [&](auto O) -> int {
+    const int order = variant / 100, u = (variant / 10) % 10;
+    const bool sb = variant % 10 != 0;
+    auto by_u = [&](auto O) -> int {
         constexpr int ORD = decltype(O)::value;
-        if (tpw == 1) return sel ? launch_v<K, CHAIN, ORD, 1, true>(A, st) : launch_v<K, CHAIN, ORD, 1, false>(A, st);
-        if (tpw == 2) return sel ? launch_v<K, CHAIN, ORD, 2, true>(A, st) : launch_v<K, CHAIN, ORD, 2, false>(A, st);
-        if (tpw == 4) return sel ? launch_v<K, CHAIN, ORD, 4, true>(A, st) : launch_v<K, CHAIN, ORD, 4, false>(A, st);
+        if (u == 1) return sb ? launch_v<K, CHAIN, ORD, 1, true>(A, st) : launch_v<K, CHAIN, ORD, 1, false>(A, st);
+        if (u == 2) return sb ? launch_v<K, CHAIN, ORD, 2, true>(A, st) : launch_v<K, CHAIN, ORD, 2, false>(A, st);
+        if (u == 4) return sb ? launch_v<K, CHAIN, ORD, 4, true>(A, st) : launch_v<K, CHAIN, ORD, 4, false>(A, st);
         return DCCL_INVALID_ARGUMENT;
     };
-    if (order == 0) return by_tpw(std::integral_constant<int, kOrderXcd>{});
-    if (order == 1) return by_tpw(std::integral_constant<int, kOrderBlock>{});
-    if (order == 2) return by_tpw(std::integral_constant<int, kOrderGroup>{});
+    if (order == 0) return by_u(std::integral_constant<int, kOrderXcd>{});
+    if (order == 1) return by_u(std::integral_constant<int, kOrderBlock>{});
+    if (order == 2) return by_u(std::integral_constant<int, kOrderGroup>{});
     return DCCL_INVALID_ARGUMENT;
 }
 
