@@ -639,8 +639,9 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
             t = (time.perf_counter() - t0) / iters
             res.update({"ms": round(t * 1e3, 3), "busbw_gb_s": round(2 * (world - 1) / world * count * 4 / t / 1e9, 1)})
             if name == "direct":
-                # the same all_reduce with the buffer registered (dcclRegisterCacheMemory): peers read it in
-                # place instead of through the communicator's scratch copy
+                # the same all_reduce with the buffer registered (dcclRegisterCacheMemory) and
+                # DCCL_IPC_ZERO_COPY=1: peers read it in place instead of through the scratch copy
+                os.environ["DCCL_IPC_ZERO_COPY"] = "1"
                 dccl_amd.check(comm.register(yf.data_ptr(), count * 4), "register")
                 yr, zr = xf.clone(), xf.clone()
                 dccl_amd.check(comm.register(yr.data_ptr(), count * 4), "register")
@@ -660,6 +661,7 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
                 res["registered_busbw_gb_s"] = round(2 * (world - 1) / world * count * 4 / t / 1e9, 1)
                 for buf in (yf, yr):
                     dccl_amd.check(comm.deregister(buf.data_ptr()), "deregister")
+                os.environ.pop("DCCL_IPC_ZERO_COPY", None)
                 del yr, zr
             if name != "grouped":  # broadcast / reduce do not depend on the all-reduce algorithm
                 res.update(root_ops(comm, world, rank, dev, st, xi, ri, iters))
@@ -1046,7 +1048,8 @@ def allreduce_summary(ar) -> dict:
     if isinstance(ar.get("ipc_stats"), dict):
         out["ipc_stats"] = {k: ar["ipc_stats"][k] for k in (
             "alias_errors", "alias_evictions", "mappings_retired", "retire_log_overflows", "open_retries",
-            "size_mismatches", "scratch_copies", "registered_hits", "exports_made") if k in ar["ipc_stats"]}
+            "size_mismatches", "scratch_copies", "registered_hits", "registered_fallbacks", "verify_failures",
+            "exports_made") if k in ar["ipc_stats"]}
     return out
 
 

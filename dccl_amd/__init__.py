@@ -148,7 +148,7 @@ IPC_STAT_NAMES = [
     "exports_made", "exports_retired", "registered_hits", "scratch_copies", "scratch_bytes", "scratch_grows",
     "stale_registrations", "mappings_opened", "mappings_reused", "mappings_retired", "retire_log_overflows",
     "mappings_trimmed", "alias_evictions", "alias_errors", "open_retries", "size_mismatches", "mappings_open",
-    "bytes_mapped", "recycled_handles", "registered_fallbacks",
+    "bytes_mapped", "recycled_handles", "registered_fallbacks", "verify_failures",
 ]
 
 

@@ -41,6 +41,7 @@ unsigned long long proc_start_time(long pid) {
     std::string tok;
     for (int field = 3; field <= 22; ++field) {  // fields after ')' start at 3 (state)
         if (!(rest >> tok)) return 0;
+        if (field == 3 && (tok == "Z" || tok == "X" || tok == "x")) return 0;  // exited, not yet reaped: gone
         if (field == 22) return std::strtoull(tok.c_str(), nullptr, 10);
     }
     return 0;

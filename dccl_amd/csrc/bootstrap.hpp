@@ -34,8 +34,9 @@ dccl::ncclResult_t rdv_publish(const std::string& path, uint32_t world, const st
 dccl::ncclResult_t rdv_read(const std::string& path, uint32_t world, uint32_t reader, double timeout_s,
                             std::string* payload);
 void rdv_remove(const std::string& path);
-// Start time of process `pid` in clock ticks since boot (/proc/<pid>/stat field 22), 0 if it is gone:
-// (pid, start time) names one process, also after the pid is reused.
+// Start time of process `pid` in clock ticks since boot (/proc/<pid>/stat field 22), 0 if it is gone (a
+// zombie that exited but was not reaped yet counts as gone): (pid, start time) names one process, also
+// after the pid is reused.
 unsigned long long proc_start_time(long pid);
 
 }  // namespace dccl_amd

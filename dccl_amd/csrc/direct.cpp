@@ -47,11 +47,15 @@ constexpr uint32_t kRetireRing = 256;
 // pages, grown by at least half when it grows.
 constexpr size_t kScratchMin = size_t(64) << 20;
 constexpr size_t kScratchPage = size_t(2) << 20;
+// The first bytes of every scratch hold a random 128-bit token that the exporter publishes with it; a peer
+// reads it through a new mapping before trusting the mapping (import_desc).  Data starts after the header.
+constexpr size_t kScratchHeader = 256;
 
 // One published buffer: the export holding it (serial 0: nothing published) and the offset in it.
 struct Desc {
     unsigned char handle[kHandleBytes];
     uint64_t serial, off, size;  // size: of the exported allocation
+    uint64_t token[2];           // a scratch's token at its first bytes (0, 0: none, a registered buffer)
 };
 
 struct ShmSlot {
@@ -89,6 +93,7 @@ struct Export {
 struct Range {
     size_t len;
     uintptr_t base;
+    uint32_t refs;  // registrations of this start address (e.g. one per communicator)
 };
 
 struct IpcXport {
@@ -96,8 +101,9 @@ struct IpcXport {
     uint32_t rank = 0, world = 0;
     double timeout_s = 60.0;
     // scratch: inputs that are not registered are copied here (one allocation, exported once)
-    void* scratch = nullptr;
+    void* scratch = nullptr;        // allocation base: header (token), then scratch_bytes of data
     size_t scratch_bytes = 0;
+    uint64_t token[2] = {0, 0};
     std::vector<void*> old_scratch;  // replaced buffers, freed at this rank's next collective
     std::vector<uint64_t> seen;      // retirements of each peer already applied
 };
@@ -181,7 +187,7 @@ bool peer_alive(const ShmSlot& s) {
     }();
     if (!check || s.pid <= 0) return true;  // not joined yet
     if (::kill(static_cast<pid_t>(s.pid), 0) != 0 && errno == ESRCH) return false;
-    return proc_start_time(static_cast<long>(s.pid)) == s.start;
+    return proc_start_time(static_cast<long>(s.pid)) == s.start;  // 0 for a zombie (exited, not reaped)
 }
 
 // Apply every retirement the peers of every IPC communicator of this process wrote since the last call.
@@ -343,18 +349,29 @@ std::map<uintptr_t, Export>::iterator find_registered(ProcCache& pc, const void*
     return e;
 }
 
-void describe(const Export& e, uintptr_t base, const void* p, Desc* d) {
+void describe(const Export& e, uintptr_t base, const void* p, const uint64_t* token, Desc* d) {
     std::memcpy(d->handle, e.handle.b, kHandleBytes);
     d->serial = e.serial;
     d->off = reinterpret_cast<uintptr_t>(p) - base;
     d->size = e.size;
+    d->token[0] = token ? token[0] : 0;
+    d->token[1] = token ? token[1] : 0;
+}
+
+// DCCL_IPC_ZERO_COPY=1 (read per call): peers read registered buffers in place.  Off by default: a peer's
+// first read through a NEW export of a user allocation returned another allocation's data in about one of
+// 1,000 first uses under registration churn on ROCm 7.2, and a user allocation cannot carry
+// the token that lets a scratch mapping be verified.  Registered buffers then go through the scratch too.
+bool zero_copy_enabled() {
+    const char* v = std::getenv("DCCL_IPC_ZERO_COPY");
+    return v != nullptr && *v == '1';
 }
 
 // Make the communicator's scratch hold at least `bytes`.  A replaced buffer is retired now and freed at
 // this rank's next collective, after every peer passed this collective's exchange (and closed it).
 ncclResult_t ensure_ipc_scratch(ProcCache& pc, IpcXport* x, size_t bytes) {
     if (bytes <= x->scratch_bytes) return dccl::ncclSuccess;
-    size_t want = std::max({bytes, x->scratch_bytes + x->scratch_bytes / 2, kScratchMin});
+    size_t want = std::max({bytes + kScratchHeader, x->scratch_bytes + x->scratch_bytes / 2, kScratchMin});
     want = (want + kScratchPage - 1) / kScratchPage * kScratchPage;
     // an allocation whose handle bytes are recycled (make_export) is kept until a fresh one is found, so the
     // next allocation cannot be handed the same bytes, then freed
@@ -392,13 +409,28 @@ ncclResult_t ensure_ipc_scratch(ProcCache& pc, IpcXport* x, size_t bytes) {
     }
     for (void* q : recycled) (void)hipFree(q);
     if (p == nullptr) return rc == dccl::ncclSuccess ? dccl::ncclInternalError : rc;
+    uint64_t token[2] = {0, 0};
+    {
+        std::random_device rd;
+        for (uint64_t& t : token) t = (uint64_t(rd()) << 32) ^ rd() ^ (uint64_t(pc.next_serial) << 48);
+        if (token[0] == 0 && token[1] == 0) token[1] = 1;
+    }
+    if (hipMemcpy(p, token, sizeof(token), hipMemcpyHostToDevice) != hipSuccess) {  // complete on return
+        (void)hipGetLastError();
+        auto e = pc.exports.find(reinterpret_cast<uintptr_t>(p));
+        if (e != pc.exports.end()) pc.exports.erase(e);  // never published
+        (void)hipFree(p);
+        return dccl::ncclUnhandledCudaError;
+    }
     if (x->scratch != nullptr) {
         auto old = pc.exports.find(reinterpret_cast<uintptr_t>(x->scratch));
         if (old != pc.exports.end()) drop_export(pc, old);
         x->old_scratch.push_back(x->scratch);
     }
     x->scratch = p;
-    x->scratch_bytes = want;
+    x->scratch_bytes = want - kScratchHeader;
+    x->token[0] = token[0];
+    x->token[1] = token[1];
     ++pc.scratch_grows;
     return dccl::ncclSuccess;
 }
@@ -430,7 +462,25 @@ ncclResult_t import_desc(ProcCache& pc, uint32_t peer, int64_t pid, const Desc& 
     ipc::Handle h;
     std::memcpy(h.b, d.handle, kHandleBytes);
     void* base = nullptr;
-    const ipc::Result r = pc.imports.acquire(pid, d.serial, h, d.size, &base);
+    ipc::Result r = ipc::kOk;
+    // A new mapping of a scratch is trusted only once its first bytes read back the token the exporter
+    // published: the mapping then provably shows the exporter's allocation.  One close and re-open on a
+    // mismatch, then an error (never data read through a wrong mapping).
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        bool opened = false;
+        r = pc.imports.acquire(pid, d.serial, h, d.size, &base, 15, &opened);
+        if (r != ipc::kOk || !opened || (d.token[0] == 0 && d.token[1] == 0)) break;
+        uint64_t got[2] = {0, 0};
+        if (hipMemcpy(got, base, sizeof(got), hipMemcpyDeviceToHost) != hipSuccess) (void)hipGetLastError();
+        if (got[0] == d.token[0] && got[1] == d.token[1]) break;
+        ++pc.imports.stats.verify_failures;
+        if (ipc_debug())
+            std::fprintf(stderr, "[dccl ipc %d] peer %u serial %llu: token mismatch at %p (attempt %d)\n", ::getpid(),
+                         peer, (unsigned long long)d.serial, base, attempt);
+        pc.imports.release(pid, d.serial);
+        pc.imports.retire(pid, d.serial);  // closes it: the next acquire opens afresh
+        r = ipc::kAliasOpened;
+    }
     if (r != ipc::kOk) {
         if (ipc_debug())
             std::fprintf(stderr, "[dccl ipc %d] peer %u serial %llu: import failed (%d)\n", ::getpid(), peer,
@@ -439,6 +489,9 @@ ncclResult_t import_desc(ProcCache& pc, uint32_t peer, int64_t pid, const Desc& 
     }
     P->held.emplace_back(pid, d.serial);
     *out = static_cast<unsigned char*>(base) + d.off;
+    if (ipc_debug())
+        std::fprintf(stderr, "[dccl ipc %d] peer %u (pid %lld) serial %llu -> %p + %llu\n", ::getpid(), peer,
+                     (long long)pid, (unsigned long long)d.serial, base, (unsigned long long)d.off);
     return dccl::ncclSuccess;
 }
 
@@ -477,8 +530,9 @@ ncclResult_t plan_ipc(dcclComm* c, Publish* pub, hipStream_t st) {
     std::lock_guard<std::mutex> lock(pc.mu);
     for (void* p : x->old_scratch) (void)hipFree(p);  // every peer closed them in the previous collective
     x->old_scratch.clear();
-    auto in_e = pub->in ? find_registered(pc, pub->in, pub->in_bytes) : pc.exports.end();
-    auto out_e = pub->out ? find_registered(pc, pub->out, pub->out_bytes) : pc.exports.end();
+    const bool zc = zero_copy_enabled();
+    auto in_e = zc && pub->in ? find_registered(pc, pub->in, pub->in_bytes) : pc.exports.end();
+    auto out_e = zc && pub->out ? find_registered(pc, pub->out, pub->out_bytes) : pc.exports.end();
     // a registration whose handle bytes are recycled is never published: through the scratch instead
     if (in_e != pc.exports.end() && !in_e->second.fresh) {
         ++pc.registered_fallbacks;
@@ -499,23 +553,24 @@ ncclResult_t plan_ipc(dcclComm* c, Publish* pub, hipStream_t st) {
     ShmSlot& s = x->ctl->slot[x->rank];
     s.in.serial = s.out.serial = 0;
     const uintptr_t sb = reinterpret_cast<uintptr_t>(x->scratch);
+    unsigned char* data = static_cast<unsigned char*>(x->scratch) + kScratchHeader;
     if (pub->in_scratch) {
-        if (hipMemcpyAsync(x->scratch, pub->in, pub->in_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess) {
+        if (hipMemcpyAsync(data, pub->in, pub->in_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess) {
             (void)hipGetLastError();
             return dccl::ncclUnhandledCudaError;
         }
         ++pc.scratch_copies;
         pc.scratch_bytes += pub->in_bytes;
-        pub->in = x->scratch;
+        pub->in = data;
     }
-    if (pub->out_scratch) pub->out = x->scratch;
+    if (pub->out_scratch) pub->out = data;
     if (pub->in) {
         auto e = pub->in_scratch ? pc.exports.find(sb) : in_e;
-        describe(e->second, e->first, pub->in, &s.in);
+        describe(e->second, e->first, pub->in, pub->in_scratch ? x->token : nullptr, &s.in);
     }
     if (pub->out) {
         auto e = pub->out_scratch ? pc.exports.find(sb) : out_e;
-        describe(e->second, e->first, pub->out, &s.out);
+        describe(e->second, e->first, pub->out, pub->out_scratch ? x->token : nullptr, &s.out);
     }
     return dccl::ncclSuccess;
 }
@@ -727,10 +782,21 @@ ncclResult_t ipc_register(void* buffer, size_t size) {
     }
     if (e != pc.exports.end() && e->second.regs == 0) return dccl::ncclInvalidUsage;  // a communicator's scratch
     auto old = pc.ranges.find(a);
-    if (old != pc.ranges.end()) {  // registering a range again replaces it
+    if (old != pc.ranges.end() && old->second.base == b && e != pc.exports.end()) {
+        // the same start registered again (another communicator, or the same one): counted, deregistered as often
+        old->second.len = std::max(old->second.len, size);
+        ++old->second.refs;
+        ++e->second.regs;
+        return dccl::ncclSuccess;
+    }
+    if (old != pc.ranges.end()) {  // a range of another allocation at this start: it was freed
         auto oe = pc.exports.find(old->second.base);
+        const uint32_t refs = old->second.refs;
         pc.ranges.erase(old);
-        if (oe != pc.exports.end() && --oe->second.regs == 0) drop_export(pc, oe);
+        if (oe != pc.exports.end()) {
+            oe->second.regs = oe->second.regs > refs ? oe->second.regs - refs : 0;
+            if (oe->second.regs == 0) drop_export(pc, oe);
+        }
         e = pc.exports.find(b);
     }
     if (e == pc.exports.end()) {
@@ -739,7 +805,7 @@ ncclResult_t ipc_register(void* buffer, size_t size) {
         e = pc.exports.find(b);
     }
     ++e->second.regs;
-    pc.ranges[a] = Range{size, b};
+    pc.ranges[a] = Range{size, b, 1};
     return dccl::ncclSuccess;
 }
 
@@ -750,7 +816,7 @@ ncclResult_t ipc_deregister(void* buffer) {
     auto r = pc.ranges.find(reinterpret_cast<uintptr_t>(buffer));
     if (r == pc.ranges.end()) return dccl::ncclInvalidArgument;
     auto e = pc.exports.find(r->second.base);
-    pc.ranges.erase(r);
+    if (--r->second.refs == 0) pc.ranges.erase(r);
     if (e != pc.exports.end() && --e->second.regs == 0) drop_export(pc, e);
     return dccl::ncclSuccess;
 }
@@ -763,7 +829,7 @@ int ipc_stats(uint64_t* out, int n) {
                           pc.scratch_grows, pc.stale_registrations, s.opened, s.reused, s.retired, s.retired_pid,
                           s.trimmed, s.alias_evicted, s.alias_errors, s.open_retries, s.size_mismatch,
                           uint64_t(pc.imports.size()), uint64_t(pc.imports.bytes()), pc.recycled_handles,
-                          pc.registered_fallbacks};
+                          pc.registered_fallbacks, s.verify_failures};
     const int m = std::min<int>(n, int(sizeof(v) / sizeof(v[0])));
     for (int i = 0; i < m; ++i) out[i] = v[i];
     return int(sizeof(v) / sizeof(v[0]));

@@ -68,6 +68,7 @@ struct ImportStats {
     uint64_t alias_errors = 0;   // opens refused: kAliasInUse or kAliasOpened
     uint64_t open_retries = 0;   // failed open attempts (retried)
     uint64_t size_mismatch = 0;  // opens whose allocation size differed from the published one (retried)
+    uint64_t verify_failures = 0;  // new mappings whose content token did not match the exporter's (direct.cpp)
 };
 
 enum Result { kOk = 0, kOpenFailed = 1, kAliasInUse = 2, kAliasOpened = 3 };
@@ -92,8 +93,11 @@ public:
         : ops_(ops), max_mappings_(max_mappings), max_bytes_(max_bytes) {}
 
     // Map export (pid, serial) with handle `h` of an allocation of `size` bytes and take a use of it.
-    Result acquire(int64_t pid, uint64_t serial, const Handle& h, uint64_t size, void** base, int max_attempts = 15) {
+    // *opened (optional): true when this call opened the mapping (the caller may verify it before trusting it).
+    Result acquire(int64_t pid, uint64_t serial, const Handle& h, uint64_t size, void** base, int max_attempts = 15,
+                   bool* opened = nullptr) {
         const Key k{pid, serial};
+        if (opened) *opened = false;
         auto it = map_.find(k);
         if (it != map_.end() && !it->second.retired) {
             ++it->second.users;
@@ -149,6 +153,7 @@ public:
         bytes_ += e.bytes;
         ++stats.opened;
         *base = mapped;
+        if (opened) *opened = true;
         return kOk;
     }
 

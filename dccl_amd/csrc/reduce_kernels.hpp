@@ -598,6 +598,61 @@ __global__ __launch_bounds__(64) void reduce_windows_kernel(WindowArgs A) {
         }
 }
 
+// The round-3 forms, kept for k <= 2: every operand through ld_phased with bounds checks and a
+// runtime tile order.  At k = 2 they run 2.5-4.3 points faster than reduce_windows_kernel (83.8 / 82.1 % against
+// 79.5 / 79.6 %, destination + 2 B, sources in phase; profiles/r4_s7_ab_windows.json), which wins from k = 3.
+template <typename T, int OP, int K>
+__global__ __launch_bounds__(64) void reduce_multi_unaligned_kernel(SendList sends, PhaseList ph,
+                                                                    unsigned char* __restrict__ recv, size_t nvec,
+                                                                    size_t count, int order) {
+    const size_t g = gridDim.x;
+    const unsigned pr = unsigned(reinterpret_cast<uintptr_t>(recv) & 15);
+    for (size_t t = tile_order(order, blockIdx.x, g); t * 64 < nvec; t += g) {
+        const size_t i = t * 64 + threadIdx.x;
+        const PhasedLoad xr = ld_phased_issue(recv, pr, i, nvec);  // recv's window, as reduce_unaligned_kernel
+        u32x4 s[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k], ph.p[k], i, nvec);
+        u32x4 acc = ld_phased_finish(xr, pr);
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, s[k]);
+        if (i < nvec) __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_u*>(recv + 16 * i));
+    }
+    if (blockIdx.x == 0)
+        for (size_t j = nvec * Pack<T>::N + threadIdx.x; j < count; j += 64) {
+            T acc = ld_elem<T, false>(recv, j);
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc = Combine<T, OP>::apply(acc, ld_elem<T, false>(sends.p[k], j));
+            st_elem<T, false>(recv, j, acc);
+        }
+}
+
+// Chain order as reduce_chain_vec_kernel; ph.p[K] is own's phase.
+template <typename T, int OP, int K>
+__global__ __launch_bounds__(64) void reduce_chain_unaligned_kernel(SendList sends, PhaseList ph,
+                                                                    const unsigned char* own, unsigned char* dst,
+                                                                    size_t nvec, size_t count, int order) {
+    const size_t g = gridDim.x;
+    for (size_t t = tile_order(order, blockIdx.x, g); t * 64 < nvec; t += g) {
+        const size_t i = t * 64 + threadIdx.x;
+        u32x4 s[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) s[k] = ld_phased(sends.p[k], ph.p[k], i, nvec);
+        const u32x4 o = ld_phased(own, ph.p[K], i, nvec);
+        u32x4 acc = s[0];
+#pragma unroll
+        for (int k = 1; k < K; ++k) acc = combine16<T, OP>(s[k], acc);
+        if (i < nvec) __builtin_nontemporal_store(combine16<T, OP>(o, acc), reinterpret_cast<u32x4_u*>(dst + 16 * i));
+    }
+    if (blockIdx.x == 0)
+        for (size_t j = nvec * Pack<T>::N + threadIdx.x; j < count; j += 64) {
+            T acc = ld_elem<T, false>(sends.p[0], j);
+#pragma unroll
+            for (int k = 1; k < K; ++k) acc = Combine<T, OP>::apply(ld_elem<T, false>(sends.p[k], j), acc);
+            st_elem<T, false>(dst, j, Combine<T, OP>::apply(ld_elem<T, false>(own, j), acc));
+        }
+}
+
 // ---------------------------------------------------------------------------------
 // Host-side launch helpers
 // ---------------------------------------------------------------------------------

@@ -1,5 +1,5 @@
 // dccl_amd/csrc/unaligned_multi.hip — the k-way and chain combines into a destination that is not
-// element-aligned (reduce_windows_kernel in reduce_kernels.hpp).
+// element-aligned (reduce_windows_kernel, and the round-3 forms for k <= 2, in reduce_kernels.hpp).
 // Instantiated for every (T, OP) with sizeof(T) > 1 (a one-byte element is always aligned), in a
 // translation unit of its own, so the build compiles it beside local_reduce.hip.
 #include <hip/hip_runtime.h>
@@ -25,6 +25,31 @@ int unaligned_order(const PhaseList& ph, int nsend) {
     for (int k = 0; k < nsend; ++k)
         if (ph.p[k] != 0) return nsend <= 4 ? kOrderXcd : kOrderGroup;
     return nsend <= 2 ? kOrderGroup : kOrderBlock;
+}
+
+// k <= 2 with every source at 16-B phase 0: the round-3 kernels (reduce_kernels.hpp), 2.5-4.3 points faster
+// there; everything else: reduce_windows_kernel.
+bool round3_form(const PhaseList& ph, int nsend) {
+    if (nsend > 2) return false;
+    for (int k = 0; k < nsend; ++k)
+        if (ph.p[k] != 0) return false;
+    return true;
+}
+
+template <typename T, int OP, int K, bool CHAIN>
+int launch_round3(SendList sl, PhaseList ph, const unsigned char* own, unsigned char* d, size_t count,
+                  hipStream_t stream) {
+    size_t nvec = count / Pack<T>::N;
+    int order = unaligned_order(ph, K);
+    if constexpr (CHAIN) {
+        void* args[] = {&sl, &ph, &own, &d, &nvec, &count, &order};
+        return launch(reinterpret_cast<const void*>(&reduce_chain_unaligned_kernel<T, OP, K>), unaligned_grid(nvec),
+                      args, stream, 64);
+    } else {
+        void* args[] = {&sl, &ph, &d, &nvec, &count, &order};
+        return launch(reinterpret_cast<const void*>(&reduce_multi_unaligned_kernel<T, OP, K>), unaligned_grid(nvec),
+                      args, stream, 64);
+    }
 }
 
 template <typename T, int OP, int K, bool CHAIN>
@@ -62,6 +87,10 @@ int launch_windows(const SendList& sl, const PhaseList& ph, const unsigned char*
 
 template <typename T, int OP>
 int multi_unaligned_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r, size_t count, hipStream_t stream) {
+    if (round3_form(ph, nsend))
+        return with_k<2, 2>(nsend, [&](auto K) {
+            return launch_round3<T, OP, K.value, false>(sl, ph, nullptr, r, count, stream);
+        });
     return with_k<2, 8>(nsend, [&](auto K) {
         return launch_windows<T, OP, K.value, false>(sl, ph, nullptr, r, count, stream);
     });
@@ -70,6 +99,10 @@ int multi_unaligned_typed(SendList sl, PhaseList ph, int nsend, unsigned char* r
 template <typename T, int OP>
 int chain_unaligned_typed(SendList sl, PhaseList ph, int nsend, const unsigned char* own, unsigned char* d,
                           size_t count, hipStream_t stream) {
+    if (round3_form(ph, nsend))
+        return with_k<1, 2>(nsend, [&](auto K) {
+            return launch_round3<T, OP, K.value, true>(sl, ph, own, d, count, stream);
+        });
     return with_k<1, 8>(nsend, [&](auto K) {
         return launch_windows<T, OP, K.value, true>(sl, ph, own, d, count, stream);
     });

@@ -22,9 +22,10 @@
  *                         collective returns ncclRemoteError (6) until dccl_comm_finalize, which still
  *                         returns and releases the shared segment and the peers' mappings.  (The
  *                         in-process transport agrees per collective and stays usable after a failure.)
- *                         Peers read device memory registered with dccl_comm_register in place; any other
- *                         input is first copied (on the collective's stream) into the communicator's
- *                         scratch, one library-owned allocation exported once.  A peer whose process dies
+ *                         Inputs are first copied (on the collective's stream) into the communicator's
+ *                         scratch, one library-owned allocation exported once, whose token every peer
+ *                         checks through its new mapping; with DCCL_IPC_ZERO_COPY=1 peers read device
+ *                         memory registered with dccl_comm_register in place instead (unverified).  A peer whose process dies
  *                         ends every other rank's wait with ncclRemoteError within ~0.1 s; a live peer that
  *                         never arrives, after DCCL_IPC_TIMEOUT_S (default 60 s).  Communicators of one
  *                         process share one mapping cache under one mutex: collectives driven from several
@@ -32,17 +33,18 @@
  *   dccl_comm_register /  dcclRegisterCacheMemory / dcclDeregisterCacheMemory (/root/reference/src/core/
  *   dccl_comm_deregister  dccl.cpp:503-549): 64-byte aligned address and size.  Host memory is page-locked.
  *                         Device memory on an IPC communicator becomes an export peers map in place until
- *                         it is deregistered (the registration belongs to the process: every IPC
- *                         communicator of it reads the range in place); the caller keeps the allocation
- *                         alive until then.  Other communicators: accepted, nothing to do.
+ *                         it is deregistered, with DCCL_IPC_ZERO_COPY=1 (the registration belongs to the
+ *                         process; registering a start address again counts, deregister as often); the
+ *                         caller keeps the allocation alive until then.  Other communicators: accepted,
+ *                         nothing to do.
  *   dccl_ipc_stats        the process's IPC transport counters, in this order: exports made, exports
  *                         retired, registered-buffer hits, scratch copies, scratch bytes copied, scratch
  *                         grows, stale registrations dropped, mappings opened, mappings reused, mappings
  *                         closed on retirement, retirement-log overflows, mappings trimmed, alias
  *                         evictions, alias errors, open retries, size mismatches, mappings open, bytes
  *                         mapped, exports with recycled handle bytes (never published), registered buffers
- *                         sent through the scratch for that reason.  Fills min(n, count) values; returns
- *                         count.
+ *                         sent through the scratch for that reason, new scratch mappings whose token did
+ *                         not read back.  Fills min(n, count) values; returns count.
  *   dccl_bootstrap_unique_id  single-node exchange of the RCCL id through DCCL_BOOTSTRAP_DIR: rank 0
  *                         creates and publishes it, the others wait (DCCL_BOOTSTRAP_TIMEOUT_S, default
  *                         120 s) for a file published by a LIVE rank 0 of the same world size, so a

@@ -82,8 +82,9 @@ void test_reuse_and_release() {
     FakeRuntime rt;
     ImportCache c(&rt, 16, 1 << 30);
     void *a = nullptr, *b = nullptr;
-    CHECK(c.acquire(100, 1, handle(1), 4096, &a) == kOk);
-    CHECK(c.acquire(100, 1, handle(1), 4096, &b) == kOk);
+    bool opened = false;
+    CHECK(c.acquire(100, 1, handle(1), 4096, &a, 15, &opened) == kOk && opened);
+    CHECK(c.acquire(100, 1, handle(1), 4096, &b, 15, &opened) == kOk && !opened);
     CHECK(a == b && rt.opens == 1);
     CHECK(c.find(100, 1)->users == 2);
     c.release(100, 1);

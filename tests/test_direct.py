@@ -7,6 +7,7 @@ sharing the box's GPU.  CPU: argument checks of the new entry points.
 """
 import multiprocessing as mp
 import os
+import sys
 import threading
 import uuid
 
@@ -374,7 +375,7 @@ def test_ipc_transport_processes(gpu, W, n, dt, op):
     assert all(results[r]["finalize"] == 0 for r in range(W))
 
 
-def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=False, register=False):
+def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=False, register=False, zc=False):
     """All-gathers over fresh allocations: before each round every buffer of the previous round is freed back to
     the driver (torch.cuda.empty_cache), so the next allocation may reuse its address; every round carries new
     data.  `grow`: odd rounds send W times as much, so a round's input lands where the previous round's output
@@ -385,6 +386,12 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=
     free, so peers read them in place and the exports churn; otherwise inputs go through the scratch."""
     os.environ["DCCL_BOOTSTRAP_TAG"] = tag
     os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")
+    if zc:
+        os.environ["DCCL_IPC_ZERO_COPY"] = "1"
+    log_dir = os.environ.get("DCCL_STRESS_LOG_DIR")  # tools/ipc_churn_stress.py --trace: this rank's stderr to a file
+    if log_dir:
+        fd = os.open(os.path.join(log_dir, f"rank{r}.log"), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        os.dup2(fd, 2)
     try:
         import torch
         import dccl_amd
@@ -405,6 +412,9 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=
                 out = torch.zeros(W * n, device="cuda", dtype=torch.int32)
                 torch.cuda.synchronize()
                 ptrs.append(mine.data_ptr())
+                if log_dir:
+                    print(f"[round {k}] rank {r} mine {mine.data_ptr():#x} out {out.data_ptr():#x}", file=sys.stderr,
+                          flush=True)
                 if register:
                     for cm in comms:
                         assert cm.register(mine.data_ptr(), n * 4) == 0
@@ -449,32 +459,33 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,nbytes,rounds,grow,two,hold,reg", [
+@pytest.mark.parametrize("W,nbytes,rounds,grow,two,hold,reg,zc", [
     # VERDICT r3's churn cases: 1 MiB buffers freed and re-allocated every round
-    (2, 1 << 20, 140, False, False, False, False), (4, 1 << 20, 100, False, False, False, False),
-    (2, 1 << 20, 140, False, False, False, True), (4, 1 << 20, 100, False, False, False, True),
-    (4, 1 << 20, 40, True, True, False, True),
-    (2, 64 << 20, 4, False, False, False, False), (4, 256 << 20, 4, False, False, False, False),
-    (4, 64 << 20, 4, True, False, False, True), (4, 64 << 20, 4, True, True, False, False),
-    (2, 64 << 20, 6, False, True, False, True), (2, 16 << 20, 140, False, False, True, True)])
-def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold, reg):
+    (2, 1 << 20, 140, False, False, False, False, False), (4, 1 << 20, 100, False, False, False, False, False),
+    (2, 1 << 20, 140, False, False, False, True, False), (4, 1 << 20, 100, False, False, False, True, False),
+    (4, 1 << 20, 40, True, True, False, True, False),
+    (2, 64 << 20, 4, False, False, False, False, False), (4, 256 << 20, 4, False, False, False, False, False),
+    (4, 64 << 20, 4, True, False, False, True, False), (4, 64 << 20, 4, True, True, False, False, False),
+    (2, 64 << 20, 6, False, True, False, True, False), (2, 16 << 20, 140, False, False, True, True, False),
+    # DCCL_IPC_ZERO_COPY=1: registered buffers read in place, kept allocated (each a new export once)
+    (2, 16 << 20, 4, False, False, True, True, True)])
+def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold, reg, zc):
     """A peer's buffer freed and a new one of the same size allocated must be mapped afresh: a cache of peer
     mappings keyed by the IPC handle alone can hand back the freed buffer's mapping (the handle bytes of a
     dmabuf export can repeat once the old export is closed), and the collective then reads stale data.
     140 rounds at W = 2 with every buffer kept (16 MiB inputs, 32 MiB outputs: one allocation each) import 280
     peer allocations, past the 256 mappings a process keeps open (trim_mappings closes the oldest unused ones).
     `two`: two communicators of the same ranks share the process's mappings (a stale mapping one of them still
-    held used to shadow the other's re-import).  `reg`: the buffers are registered every round (peers map
-    them in place, and every deregistration retires an export); otherwise inputs reach the peers through
-    each communicator's scratch, which is exported once.  A registration whose handle bytes once named another
-    (freed) allocation of its process is never published (it goes through the scratch): a peer that opens
-    such bytes again can be handed the freed allocation's pages even though it closed that mapping (round 4:
-    6 of 6 runs of the registered W = 2 case read stale data before this rule).  Either way no mapping may
-    alias another (alias_errors == 0 in every process)."""
+    held used to shadow the other's re-import).  `reg`: the buffers are registered every round (and registered
+    on both communicators with `two`: counted registrations); inputs reach the peers through each
+    communicator's scratch, exported once and verified by its token.  `zc` (DCCL_IPC_ZERO_COPY=1): peers read
+    registered buffers in place; a registration whose handle bytes once named another (freed) allocation of its
+    process is never published (it goes through the scratch).  No mapping may alias another and every new
+    scratch mapping must read back its token (alias_errors == verify_failures == 0 in every process)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     tag = "test_" + uuid.uuid4().hex[:12]
-    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q, two, hold, reg))
+    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q, two, hold, reg, zc))
           for r in range(W)]
     for p in ps:
         p.start()
@@ -492,17 +503,17 @@ def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold, reg):
     for r in range(W):
         bad, fin, stats, _ = results[r]
         assert not bad and fin == 0, (r, bad[:8], len(bad), fin, stats)
-        assert stats["alias_errors"] == 0, (r, stats)
-        if reg:  # registered inputs: read in place, or through the scratch when their handle bytes are recycled
+        assert stats["alias_errors"] == 0 and stats["verify_failures"] == 0, (r, stats)
+        if zc:  # registered inputs read in place, or through the scratch when their handle bytes are recycled
             assert stats["registered_hits"] >= rounds, (r, stats)
             assert stats["scratch_copies"] == stats["registered_fallbacks"], (r, stats)
-        else:
+        else:  # every input through the verified scratch, registered or not
             assert stats["scratch_copies"] >= rounds and stats["registered_hits"] == 0, (r, stats)
 
 
 def _ipc_dying_rank(r, tag, q):
     os.environ["DCCL_BOOTSTRAP_TAG"] = tag
-    os.environ["DCCL_IPC_TIMEOUT_S"] = "100"  # far above the wait the liveness check allows
+    os.environ["DCCL_IPC_TIMEOUT_S"] = "25"  # far above the wait the liveness check allows
     try:
         import time
         import torch
@@ -511,6 +522,8 @@ def _ipc_dying_rank(r, tag, q):
         comm = dccl_amd.Comm.ipc(2, r)
         if r == 1:
             q.put((r, None, None))
+            q.close()
+            q.join_thread()  # the message is in the pipe before the process vanishes
             os._exit(0)  # gone without finalize, as after a runtime abort
         x = torch.ones(1 << 20, device="cuda", dtype=torch.float32)
         t0 = time.monotonic()

@@ -31,16 +31,26 @@ def main():
     p.add_argument("--grow", action="store_true")
     p.add_argument("--two", action="store_true")
     p.add_argument("--register", action="store_true")
+    p.add_argument("--zero-copy", action="store_true", help="DCCL_IPC_ZERO_COPY=1: registered buffers read in place")
+    p.add_argument("--trace", default="", help="directory: DCCL_IPC_DEBUG=1, every rank's stderr kept per run "
+                                               "(runs without a wrong slice are deleted)")
     a = p.parse_args()
     # a rank that fails leaves its peers at a barrier: let them give up well before a pool's silence limit
     os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")
     ctx = mp.get_context("spawn")
     failed, reports = 0, []
+    import shutil
     for run in range(a.runs):
+        run_dir = ""
+        if a.trace:
+            run_dir = os.path.join(a.trace, f"run{run}")
+            os.makedirs(run_dir, exist_ok=True)
+            os.environ.update({"DCCL_IPC_DEBUG": "1", "DCCL_STRESS_LOG_DIR": run_dir})
         q = ctx.Queue()
         tag = "stress_" + uuid.uuid4().hex[:10]
         ps = [ctx.Process(target=_ipc_realloc_rank,
-                          args=(r, a.world, a.mib << 20, a.rounds, a.grow, tag, q, a.two, False, a.register))
+                          args=(r, a.world, a.mib << 20, a.rounds, a.grow, tag, q, a.two, False, a.register,
+                                a.zero_copy))
               for r in range(a.world)]
         for x in ps:
             x.start()
@@ -66,10 +76,11 @@ def main():
         if bad:
             failed += 1
             reports.append({"run": run, "bad": bad})
+        elif run_dir:
+            shutil.rmtree(run_dir, ignore_errors=True)
         print(f"run {run}: {'FAILED ' + repr(bad) if bad else 'ok'}", file=sys.stderr, flush=True)
     print(json.dumps({"runs": a.runs, "world": a.world, "mib": a.mib, "rounds": a.rounds, "grow": a.grow,
-                      "two": a.two, "register": a.register,
-                      "dereg_wait": os.environ.get("DCCL_IPC_DEREG_WAIT", "1"), "failed_runs": failed, "reports": reports[:5]}, default=str), flush=True)
+                      "two": a.two, "register": a.register, "zero_copy": a.zero_copy, "failed_runs": failed, "reports": reports[:5]}, default=str), flush=True)
 
 
 if __name__ == "__main__":
