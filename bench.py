@@ -602,13 +602,13 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
     dist.broadcast_object_list(obj, src=0)
     comms = {}
     if obj[0] is not None:
-        # one RCCL communicator, two algorithms: the reference's ring step loop, and the grouped form (one RCCL
-        # group per phase, one chain combine; the default on this transport, algorithms.hpp)
+        # one RCCL communicator, two algorithms: the reference's ring step loop (the default), and the grouped
+        # form (one RCCL group per phase, one chain combine, DCCL_ALLREDUCE_ALGORITHM=grouped, algorithms.hpp)
         comms["ring"] = dccl_amd.Comm.rccl(world, rank, obj[0])
         comms["grouped"] = comms["ring"]
     if "direct" in transports:
         comms["direct"] = dccl_amd.Comm.ipc(world, rank)
-    algo_env = {"ring": "ring", "grouped": "auto", "direct": "auto"}
+    algo_env = {"ring": "ring", "grouped": "grouped", "direct": "auto"}
     out = {"count": count, "world": world, "bytes": count * 4}
     try:
         st = torch.cuda.current_stream(dev)

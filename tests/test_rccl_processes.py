@@ -41,7 +41,7 @@ def _rccl_rank(r, W, n, dt, op, hostid, conn, algo):
         outs = {}
         try:
             st = torch.cuda.Stream()
-            for api in (APIS if algo in ("ring", "auto") else ["all_reduce"]):
+            for api in (APIS if algo in ("ring", "grouped") else ["all_reduce"]):
                 outs[api] = _run_direct_rank(comm, r, W, n, dt, op, api, st.cuda_stream, torch)
             # device memory only on this transport: a host buffer is ncclInvalidUsage
             outs["host_rejected"] = comm.all_reduce(np.zeros(4, np.float32).ctypes.data,
@@ -81,11 +81,11 @@ def _run(W, n, dt, op, algo):
     return results
 
 
-@pytest.mark.parametrize("algo", ["ring", "auto"])
+@pytest.mark.parametrize("algo", ["ring", "grouped"])
 @pytest.mark.parametrize("W,n,dt,op", [(2, 2 * 65536, 7, 0), (3, 3 * 4099, 2, 1), (4, 4 * 1000, 9, 3),
                                       (8, 8 * 777, 7, 2)])
 def test_rccl_transport_processes(gpu, W, n, dt, op, algo):
-    """`ring`: the reference's ring step loop over RCCL send/recv; `auto` (the default): all_reduce and
+    """`ring` (the default): the reference's ring step loop over RCCL send/recv; `grouped`: all_reduce and
     reduce_scatter take the grouped forms (one RCCL group per phase, one chain combine in the ring's order,
     algorithms.hpp).  Both bit-exact against the ring simulation."""
     import dccl_amd

@@ -62,7 +62,7 @@ def rank_main(r, W, n, calls, algo, hostid, conn, q):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("algo", choices=["ring", "auto"])
+    ap.add_argument("algo", choices=["ring", "grouped"])
     ap.add_argument("--world", type=int, default=4)
     ap.add_argument("--mib", type=int, default=64)
     ap.add_argument("--calls", type=int, default=10)
