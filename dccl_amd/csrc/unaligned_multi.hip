@@ -4,6 +4,8 @@
 // translation unit of its own, so the build compiles it beside local_reduce.hip.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "dispatch.hpp"
 #include "reduce_kernels.hpp"
 
@@ -70,16 +72,19 @@ int launch_windows(const SendList& sl, const PhaseList& ph, const unsigned char*
     A.count = count;
     void* args[] = {&A};
     const size_t grid = unaligned_grid(A.nvec);
+    // DCCL_WINDOWS_WAVES=<n> (tuning sweeps only, tools/windows_caps.py): cap resident waves per CU
+    const char* cap = std::getenv("DCCL_WINDOWS_WAVES");
+    const size_t lds = cap ? caps::lds_for_waves(std::atoi(cap)) : 0;
     switch (unaligned_order(ph, K)) {
     case kOrderXcd:
         return launch(reinterpret_cast<const void*>(&reduce_windows_kernel<T, OP, K, CHAIN, kOrderXcd>), grid, args,
-                      stream, 64);
+                      stream, 64, lds);
     case kOrderBlock:
         return launch(reinterpret_cast<const void*>(&reduce_windows_kernel<T, OP, K, CHAIN, kOrderBlock>), grid, args,
-                      stream, 64);
+                      stream, 64, lds);
     default:
         return launch(reinterpret_cast<const void*>(&reduce_windows_kernel<T, OP, K, CHAIN, kOrderGroup>), grid, args,
-                      stream, 64);
+                      stream, 64, lds);
     }
 }
 
