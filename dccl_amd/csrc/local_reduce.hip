@@ -189,6 +189,13 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
         }
     }
     if (!vec_ok) {  // an element-aligned recv and sources at other 16-B (or byte) phases: the phased kernel
+        if constexpr (sizeof(T) > 1) {
+            if (caps::phased_via_windows(false, nsend, count * sizeof(T))) {  // or the windows kernel (caps.hpp)
+                PhaseList ph{};
+                for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], 0);
+                return multi_unaligned_typed<T, OP>(sl, ph, nsend, r, count, stream);
+            }
+        }
         const Split sp = split_for_vectors<T>(ar, count, recv_align());
         PhaseList ph{};
         for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(T));
@@ -266,6 +273,14 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
         }
     }
     if (!vec_ok) {  // an element-aligned dst and operands at other 16-B (or byte) phases: the phased kernel
+        if constexpr (sizeof(T) > 1) {
+            if (caps::phased_via_windows(true, nsend, count * sizeof(T))) {  // or the windows kernel (caps.hpp)
+                PhaseList ph{};
+                for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], 0);
+                ph.p[nsend] = phase_word(o, 0);
+                return chain_unaligned_typed<T, OP>(sl, ph, nsend, o, d, count, stream);
+            }
+        }
         const Split sp = split_for_vectors<T>(ad, count, recv_align());
         PhaseList ph{};
         for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], sp.head * sizeof(T));

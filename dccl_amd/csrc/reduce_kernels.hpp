@@ -573,13 +573,70 @@ __device__ __forceinline__ void window_tile(const WindowArgs& A, size_t t) {
     if (FULL || v < A.nvec) __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_u*>(A.dst + 16 * v));
 }
 
-template <typename T, int OP, int K, bool CHAIN, int ORDER>
+// The loads-first tile: every operand's aligned load and lane 63's extra vectors are issued before any lane
+// exchange, so a wave waits once per tile.  (In window_tile the uniform phase branches keep the compiler
+// from hoisting the next operand's load above the previous one's exchange: K + 1 round trips per tile.)
+// Twice the VGPRs in flight, so it runs under a resident-wave cap (caps.hpp kWindowsFirst).
+template <typename T, int OP, int K, bool CHAIN, bool FULL>
+__device__ __forceinline__ void window_tile_first(const WindowArgs& A, size_t t) {
+    const size_t v = t * 64 + threadIdx.x;
+    u32x4 lo[K + 1], ex[K + 1];
+#pragma unroll
+    for (int k = 0; k <= K; ++k) {
+        lo[k] = u32x4{0u, 0u, 0u, 0u};
+        ex[k] = u32x4{0u, 0u, 0u, 0u};
+        if (FULL || (A.p[k] != 0 ? v <= A.nvec : v < A.nvec)) lo[k] = __builtin_nontemporal_load(A.a[k] + v);
+    }
+    if ((threadIdx.x & 63) == 63) {
+#pragma unroll
+        for (int k = 0; k <= K; ++k)
+            if (A.p[k] != 0 && (FULL || v < A.nvec)) ex[k] = A.a[k][v + 1];
+    }
+    u32x4 w[K + 1];
+#pragma unroll
+    for (int k = 0; k <= K; ++k) {
+        const unsigned p = A.p[k];
+        if (p == 0) {
+            w[k] = lo[k];
+            continue;
+        }
+        const u32x4 hi = from_next_lane_or(lo[k], ex[k]);
+        const unsigned b = p & 3;
+        switch (p >> 2) {  // uniform
+        case 0: w[k] = funnel16<0>(lo[k], hi, b); break;
+        case 1: w[k] = funnel16<1>(lo[k], hi, b); break;
+        case 2: w[k] = funnel16<2>(lo[k], hi, b); break;
+        default: w[k] = funnel16<3>(lo[k], hi, b); break;
+        }
+    }
+    u32x4 acc;
+    if constexpr (CHAIN) {
+        acc = w[0];
+#pragma unroll
+        for (int k = 1; k < K; ++k) acc = combine16<T, OP>(w[k], acc);
+        acc = combine16<T, OP>(w[K], acc);
+    } else {
+        acc = w[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = combine16<T, OP>(acc, w[k]);
+    }
+    if (FULL || v < A.nvec) __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_u*>(A.dst + 16 * v));
+}
+
+template <typename T, int OP, int K, bool CHAIN, int ORDER, bool FIRST = false>
 __global__ __launch_bounds__(64) void reduce_windows_kernel(WindowArgs A) {
     const size_t g = gridDim.x;
     const size_t ntiles = (A.nvec + 63) / 64;
     for (size_t t = first_tile<ORDER>(blockIdx.x, g); t < ntiles; t += g) {
-        if ((t + 1) * 64 < A.nvec) window_tile<T, OP, K, CHAIN, true>(A, t);  // lane 63's extra vector inside too
-        else window_tile<T, OP, K, CHAIN, false>(A, t);
+        const bool full = (t + 1) * 64 < A.nvec;  // lane 63's extra vector inside too
+        if constexpr (FIRST) {
+            if (full) window_tile_first<T, OP, K, CHAIN, true>(A, t);
+            else window_tile_first<T, OP, K, CHAIN, false>(A, t);
+        } else if (full) {
+            window_tile<T, OP, K, CHAIN, true>(A, t);
+        } else {
+            window_tile<T, OP, K, CHAIN, false>(A, t);
+        }
     }
     if (blockIdx.x == 0)
         for (size_t j = A.nvec * Pack<T>::N + threadIdx.x; j < A.count; j += 64) {

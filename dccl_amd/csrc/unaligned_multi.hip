@@ -1,10 +1,9 @@
 // dccl_amd/csrc/unaligned_multi.hip — the k-way and chain combines into a destination that is not
-// element-aligned (reduce_windows_kernel, and the round-3 forms for k <= 2, in reduce_kernels.hpp).
+// element-aligned (reduce_windows_kernel, and the round-3 forms for k <= 2, in reduce_kernels.hpp), and the
+// phased launches that caps::phased_via_windows routes here (element-aligned destination, k = 3..5).
 // Instantiated for every (T, OP) with sizeof(T) > 1 (a one-byte element is always aligned), in a
 // translation unit of its own, so the build compiles it beside local_reduce.hip.
 #include <hip/hip_runtime.h>
-
-#include <cstdlib>
 
 #include "dispatch.hpp"
 #include "reduce_kernels.hpp"
@@ -54,14 +53,30 @@ int launch_round3(SendList sl, PhaseList ph, const unsigned char* own, unsigned 
     }
 }
 
+template <typename T, int OP, int K, bool CHAIN, bool FIRST, int ORDER>
+int launch_form(WindowArgs A, hipStream_t stream, size_t lds) {
+    void* args[] = {&A};
+    return launch(reinterpret_cast<const void*>(&reduce_windows_kernel<T, OP, K, CHAIN, ORDER, FIRST>),
+                  unaligned_grid(A.nvec), args, stream, 64, lds);
+}
+
+// The tuned form of operand class C at K (caps.hpp kWindow): one kernel per (class, K).
+template <typename T, int OP, int K, bool CHAIN, int C>
+int launch_tuned(const WindowArgs& A, hipStream_t stream) {
+    constexpr caps::WindowForm f = caps::window_form(caps::WindowClass(C), K);
+    return launch_form<T, OP, K, CHAIN, f.first != 0, int(f.order)>(A, stream, caps::lds_for_waves(f.waves));
+}
+
 template <typename T, int OP, int K, bool CHAIN>
 int launch_windows(const SendList& sl, const PhaseList& ph, const unsigned char* own, unsigned char* d, size_t count,
                    hipStream_t stream) {
     WindowArgs A{};
+    bool off = false;
     for (int k = 0; k < K; ++k) {
         A.p[k] = ph.p[k];
         A.a[k] = reinterpret_cast<const u32x4*>(sl.p[k] - ph.p[k]);
         A.src[k] = sl.p[k];
+        off = off || ph.p[k] != 0;
     }
     const unsigned char* w = CHAIN ? own : d;  // the last window: own (chain) or the destination's own (k-way)
     A.p[K] = phase_word(w, 0);
@@ -70,21 +85,13 @@ int launch_windows(const SendList& sl, const PhaseList& ph, const unsigned char*
     A.dst = d;
     A.nvec = count / Pack<T>::N;
     A.count = count;
-    void* args[] = {&A};
-    const size_t grid = unaligned_grid(A.nvec);
-    // DCCL_WINDOWS_WAVES=<n> (tuning sweeps only, tools/windows_caps.py): cap resident waves per CU
-    const char* cap = std::getenv("DCCL_WINDOWS_WAVES");
-    const size_t lds = cap ? caps::lds_for_waves(std::atoi(cap)) : 0;
-    switch (unaligned_order(ph, K)) {
-    case kOrderXcd:
-        return launch(reinterpret_cast<const void*>(&reduce_windows_kernel<T, OP, K, CHAIN, kOrderXcd>), grid, args,
-                      stream, 64, lds);
-    case kOrderBlock:
-        return launch(reinterpret_cast<const void*>(&reduce_windows_kernel<T, OP, K, CHAIN, kOrderBlock>), grid, args,
-                      stream, 64, lds);
-    default:
-        return launch(reinterpret_cast<const void*>(&reduce_windows_kernel<T, OP, K, CHAIN, kOrderGroup>), grid, args,
-                      stream, 64, lds);
+    if (count * sizeof(T) >= caps::kWindowTunedBytes)
+        return off ? launch_tuned<T, OP, K, CHAIN, caps::kWinOffPhase>(A, stream)
+                   : launch_tuned<T, OP, K, CHAIN, caps::kWinInPhase>(A, stream);
+    switch (unaligned_order(ph, K)) {  // smaller launches: the per-operand form, uncapped
+    case kOrderXcd: return launch_form<T, OP, K, CHAIN, false, kOrderXcd>(A, stream, 0);
+    case kOrderBlock: return launch_form<T, OP, K, CHAIN, false, kOrderBlock>(A, stream, 0);
+    default: return launch_form<T, OP, K, CHAIN, false, kOrderGroup>(A, stream, 0);
     }
 }
 

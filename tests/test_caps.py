@@ -43,6 +43,18 @@ int main() {
     std::printf("], \"loads_first\": [");
     for (int ch = 0; ch < 2; ++ch)
         for (int k = 1; k <= 8; ++k) std::printf("%s%d", (ch || k > 1) ? ", " : "", int(phased_loads_first(ch, k)));
+    std::printf("], \"windows\": [");
+    for (int c = 0; c < kNumWindowClasses; ++c)
+        for (int k = 0; k <= 8; ++k) {
+            const WindowForm f = window_form(WindowClass(c), k);
+            std::printf("%s[%d, %d, %d, %d, %zu]", (c || k) ? ", " : "", c, k, f.first * 100 + f.order * 10, f.waves,
+                        lds_for_waves(f.waves));
+        }
+    std::printf("], \"phased_via_windows\": [");
+    for (int ch = 0; ch < 2; ++ch)
+        for (int k = 1; k <= 8; ++k)
+            std::printf("%s[%d, %d, %d, %d]", (ch || k > 1) ? ", " : "", ch, k,
+                        int(phased_via_windows(ch, k, kWindowTunedBytes - 1)), int(phased_via_windows(ch, k, kWindowTunedBytes)));
     std::printf("]}\n");
 }
 """
@@ -133,3 +145,16 @@ def test_separate_allocation_rule(table):
         else:
             assert lds == (6144 if sh else 7168), (sh, sep, b)
             assert (160 << 10) // lds == (26 if sh else 22)
+
+
+def test_window_forms(table):
+    """reduce_windows_kernel's tuned forms (caps.hpp kWindow): per-operand block order under 26
+    waves in phase from k = 3; off phase group order, per-operand at 26 except loads-first at k = 4 (14 waves)
+    and k = 5 (12); k <= 2 uncapped; the phased launches at k = 3..5 (chain 4..5) from 96 MiB per operand."""
+    want = {0: {k: (10, 26 if k >= 3 else 32) for k in range(9)},
+            1: {k: (0, 32) if k <= 2 else (120, 14) if k == 4 else (120, 12) if k == 5 else (20, 26) for k in range(9)}}
+    for c, k, form, w, lds in table["windows"]:
+        assert (form, w) == want[c][k], (c, k, form, w)
+        assert lds == lds_for(w) and lds <= 64 << 10
+    assert table["phased_via_windows"] == [[ch, k, 0, int((4 if ch else 3) <= k <= 5)] for ch in (0, 1)
+                                           for k in range(1, 9)]

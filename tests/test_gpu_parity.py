@@ -375,6 +375,64 @@ def test_misaligned_destination_tile_orders(dccl, k):
                 assert not to[:roff].any() and not to[roff + n * esz:].any()
 
 
+def _torch_op(op):
+    return {0: torch.add, 1: torch.mul, 2: torch.maximum, 3: torch.minimum}[op]
+
+
+@pytest.mark.parametrize("k", [3, 4, 5, 6, 8])
+def test_windows_tuned_forms_full_size(dccl, k):
+    """From caps::kWindowTunedBytes (96 MiB per operand) reduce_windows_kernel takes its tuned forms (caps.hpp
+    kWindow: block order under a 26-wave cap with sources in phase; group order, loads-first at k = 4, 5 under
+    14 / 12 waves, with sources off phase) and takes over the phased launches at k = 3..5.  Destination not
+    element-aligned, and element-aligned at 16-B phases 0 and 4; sources at phase 0 and 4; k-way and chain in
+    place; fp32 Sum, int32 Max, bf16 Sum, against torch applied on the device in the kernels' order, bit for
+    bit; nothing outside the destination written."""
+    nb = (96 << 20) + 4096
+    for dt, tdt, ibits, op in [(7, torch.float32, torch.int32, 0), (2, torch.int32, torch.int32, 2),
+                               (9, torch.bfloat16, torch.int16, 0)]:
+        esz = torch.empty(0, dtype=tdt).element_size()
+        n = nb // esz
+        mis = 1 if esz == 2 else 2
+        g = torch.Generator(device="cuda").manual_seed(2400 + k + dt)
+
+        def operand():
+            if tdt == torch.int32:
+                return torch.randint(-(1 << 30), 1 << 30, (n,), device="cuda", dtype=tdt, generator=g)
+            return (torch.rand(n, device="cuda", generator=g) * 2 - 1).to(tdt)
+
+        def placed(x, off):
+            buf = torch.zeros(nb + 1024, dtype=torch.uint8, device="cuda")
+            buf[off:off + nb].copy_(x.view(torch.uint8))
+            return buf
+
+        f = _torch_op(op)
+        for roff, soff in [(mis, 0), (mis, 4), (0, 4), (4, 0)]:
+            sends = [operand() for _ in range(k)]
+            r = operand()
+            sbufs = [placed(x, 64 * (j + 1) + soff) for j, x in enumerate(sends)]
+            sptrs = [b.data_ptr() + 64 * (j + 1) + soff for j, b in enumerate(sbufs)]
+            want_m = r
+            for x in sends:
+                want_m = f(want_m, x)
+            acc = sends[0]
+            for x in sends[1:]:
+                acc = f(x, acc)
+            want_c = f(r, acc)
+            for form, want in (("multi", want_m), ("chain", want_c)):
+                d = placed(r, roff)
+                p = d.data_ptr() + roff
+                rc = dccl.local_reduce_multi(sptrs, p, dt, n, op, 0) if form == "multi" else \
+                    dccl.local_reduce_chain(sptrs, p, p, dt, n, op, 0)
+                assert rc == 0
+                torch.cuda.synchronize()
+                got = d[roff:roff + nb].clone().view(tdt)
+                assert torch.equal(got.view(ibits), want.view(ibits)), (form, k, dt, roff, soff)
+                assert not d[:roff].any() and not d[roff + nb:].any(), (form, k, dt, roff, soff)
+                del d
+            del sbufs, sends
+        torch.cuda.empty_cache()
+
+
 # ----------------------------------------------------------------------------- host path
 @pytest.mark.parametrize("zero_copy", ["default", "0"])
 @pytest.mark.parametrize("pinned", ["none", "both", "send"])

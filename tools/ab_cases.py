@@ -69,6 +69,11 @@ def case_table(ptrs):
         t[f"chain{k}_dst+2_src+4"] = (k, chain([p + 4 for p in ptrs[:k]], recv + 2, recv + 2))
         t[f"chain{k}_src+4"] = (k, chain([p + 4 for p in ptrs[:k]], recv, recv))
         t[f"chain{k}_strad"] = (k, chain([p + 16 * (2 * j + 1) for j, p in enumerate(ptrs[:k])], recv, recv))
+        # element-aligned destinations off the 128-B line grid (phased launches)
+        t[f"multi{k}_dst+4"] = (k, multi(ptrs[:k], recv + 4))
+        t[f"chain{k}_dst+4"] = (k, chain(ptrs[:k], recv + 4, recv + 4))
+        t[f"multi{k}_dst+16_src+4"] = (k, multi([p + 4 for p in ptrs[:k]], recv + 16))
+        t[f"chain{k}_dst+16_src+4"] = (k, chain([p + 4 for p in ptrs[:k]], recv + 16, recv + 16))
     return t
 
 

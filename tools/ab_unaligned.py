@@ -5,7 +5,9 @@ allocation, 4 KiB x (j+1) stagger (tools/ab_cases.py's layout).  Every case is c
 the product on a 1 Mi-element slice, then timed interleaved (HIP events around --launches back-to-back
 launches per round, median over --rounds), as a fraction of (k+2) * N * 4 B at 8 TB/s.
 
-    python tools/ab_unaligned.py [--variants 11,111,211,...] [--cases ...] [--rounds 5] [--out f.json]
+    python tools/ab_unaligned.py [--variants 110,260110,...] [--ks 4,8] [--cases ...] [--rounds 5] [--out f.json]
+
+Variant codes: tools/tune/unaligned_v4.hip (10000 * waves + 1000 * loads-first + 100 * order + 10).
 """
 import argparse
 import ctypes
@@ -24,10 +26,10 @@ PEAK = 8e12
 LIB = os.path.join(ROOT, "tools", "lib", "libunaligned_v4.so")
 
 
-def cases(ptrs):
+def cases(ptrs, ks):
     recv, src = ptrs[0], ptrs[1:9]
     t = {}
-    for k in (4, 8):
+    for k in ks:
         for so, sname in ((0, ""), (4, "_src+4")):
             s = [p + so for p in src[:k]]
             t[f"multi{k}_dst+2{sname}"] = (k, s, None, recv + 2)
@@ -39,7 +41,8 @@ def cases(ptrs):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="10,11,20,21,40,110,111,120,210,211,220")
+    ap.add_argument("--variants", default="110,260110,121110,121210")
+    ap.add_argument("--ks", default="4,8")
     ap.add_argument("--cases", default="")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=10)
@@ -59,7 +62,7 @@ def main():
         ptrs.append(pool.data_ptr() + off)
         dccl_amd.check(dccl_amd.synth_fill(ptrs[-1], 7, nbytes // 4, 0, 0xDCC1, 10 + j, st), "synth")
         off += nbytes + 4096 * (j + 1)
-    table = cases(ptrs)
+    table = cases(ptrs, [int(x) for x in a.ks.split(",")])
     names = a.cases.split(",") if a.cases else list(table)
     variants = [int(v) for v in a.variants.split(",")]
 

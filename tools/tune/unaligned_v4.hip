@@ -9,14 +9,14 @@
 //   * the host passes each operand's 16-B aligned base and phase (UArgs), the order is a template parameter;
 //   * tiles whose every vector (and lane 63's extra vector) is inside the body take a path without bounds
 //     checks;
-//   * U vectors per lane per operand (U = 1, 2, 4), so every per-operand branch (phase 0 or not, the lane-63
-//     extra loads, the funnel's 4-way switch) is paid once per U vectors; one operand at a time, as the
-//     product kernels (loading every operand first needs twice the VGPRs and lost in round 2).
+//   * U vectors per lane per operand (U = 2, 4 lost, round 4; U = 1 kept);
+//   * the loads-first tile (every operand's loads before any lane exchange) under a resident-wave cap.
 //
 //   extern "C" int uv4_combine(int variant, const void* const* sends, int k, const void* own, void* dst,
 //                              size_t count, void* stream)       own == nullptr: k-way into dst; else chain
 #include <hip/hip_runtime.h>
 
+#include "caps.hpp"
 #include "reduce_kernels.hpp"
 
 namespace dccl_amd {
@@ -123,14 +123,70 @@ __device__ __forceinline__ void tile(const UArgs& A, size_t t) {
     }
 }
 
-template <int K, bool CHAIN, int ORDER, int U, bool SB>
+// Loads-first form of one U = 1 tile: every operand's aligned load (and lane 63's extra vector) is issued
+// before any lane exchange, so a wave waits once per tile instead of once per operand (the product kernel's
+// per-operand phase branches keep the compiler from hoisting the next operand's load above the exchange).
+template <int K, bool CHAIN, bool FULL>
+__device__ __forceinline__ void tile_first(const UArgs& A, size_t t) {
+    const unsigned lane = threadIdx.x;
+    const size_t v = t * 64 + lane;
+    u32x4 lo[K + 1], ex[K + 1];
+#pragma unroll
+    for (int k = 0; k <= K; ++k) {
+        lo[k] = u32x4{0u, 0u, 0u, 0u};
+        ex[k] = u32x4{0u, 0u, 0u, 0u};
+        if (FULL || (A.p[k] != 0 ? v <= A.nvec : v < A.nvec)) lo[k] = __builtin_nontemporal_load(A.a[k] + v);
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int k = 0; k <= K; ++k)
+            if (A.p[k] != 0 && (FULL || v < A.nvec)) ex[k] = A.a[k][v + 1];
+    }
+    u32x4 w[K + 1];
+#pragma unroll
+    for (int k = 0; k <= K; ++k) {
+        const unsigned p = A.p[k];
+        if (p == 0) {
+            w[k] = lo[k];
+            continue;
+        }
+        const u32x4 hi = from_next_lane_or(lo[k], ex[k]);
+        const unsigned b = p & 3;
+        switch (p >> 2) {
+        case 0: w[k] = funnel16<0>(lo[k], hi, b); break;
+        case 1: w[k] = funnel16<1>(lo[k], hi, b); break;
+        case 2: w[k] = funnel16<2>(lo[k], hi, b); break;
+        default: w[k] = funnel16<3>(lo[k], hi, b); break;
+        }
+    }
+    u32x4 acc;
+    if constexpr (CHAIN) {
+        acc = w[0];
+#pragma unroll
+        for (int k = 1; k < K; ++k) acc = combine16<float, kSum>(w[k], acc);
+        acc = combine16<float, kSum>(w[K], acc);
+    } else {
+        acc = w[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = combine16<float, kSum>(acc, w[k]);
+    }
+    if (FULL || v < A.nvec) __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_u*>(A.dst + 16 * v));
+}
+
+template <int K, bool CHAIN, int ORDER, int U, bool SB, bool FIRST = false>
 __global__ __launch_bounds__(64) void uv4_kernel(UArgs A) {
     const size_t g = gridDim.x;
     const size_t span = size_t(U) * 64;
     const size_t ntiles = (A.nvec + span - 1) / span;
     for (size_t t = first_tile<ORDER>(blockIdx.x, g); t < ntiles; t += g) {
-        if ((t + 1) * span < A.nvec) tile<K, CHAIN, U, true, SB>(A, t);  // lane 63's extra vector inside too
-        else tile<K, CHAIN, U, false, SB>(A, t);
+        if constexpr (FIRST) {
+            if ((t + 1) * span < A.nvec) tile_first<K, CHAIN, true>(A, t);
+            else tile_first<K, CHAIN, false>(A, t);
+        } else if ((t + 1) * span < A.nvec) {
+            tile<K, CHAIN, U, true, SB>(A, t);  // lane 63's extra vector inside too
+        } else {
+            tile<K, CHAIN, U, false, SB>(A, t);
+        }
     }
     if (blockIdx.x == 0)
         for (size_t j = A.nvec * 4 + threadIdx.x; j < A.count; j += 64) {
@@ -149,32 +205,33 @@ __global__ __launch_bounds__(64) void uv4_kernel(UArgs A) {
         }
 }
 
-template <int K, bool CHAIN, int ORDER, int U, bool SB>
-int launch_v(const UArgs& A, hipStream_t st) {
+template <int K, bool CHAIN, int ORDER, int U, bool SB, bool FIRST = false>
+int launch_v(const UArgs& A, hipStream_t st, int waves) {
     const size_t ntiles = ceil_div(A.nvec, size_t(U) * 64);
     size_t g = ceil_div(ntiles, size_t(8)) * 8;
     if (g == 0) g = 8;
     UArgs a = A;
     void* args[] = {&a};
-    return launch(reinterpret_cast<const void*>(&uv4_kernel<K, CHAIN, ORDER, U, SB>), g, args, st, 64);
+    return launch(reinterpret_cast<const void*>(&uv4_kernel<K, CHAIN, ORDER, U, SB, FIRST>), g, args, st, 64,
+                  caps::lds_for_waves(waves));
 }
 
-// variant = 100 * order + 10 * U + sb   (order 0 xcd, 1 block, 2 group; U 1, 2, 4 vectors per lane; sb 1: a
-// scheduling barrier between operands, so the compiler cannot hoist every operand's loads to the top)
+// variant = 10000 * waves + 1000 * first + 100 * order + 10 * U   (waves: resident-wave cap per CU, 0
+// uncapped; first 1: the loads-first tile (U = 1); order 0 xcd, 1 block, 2 group; U 1 vector per lane --
+// the U = 2, 4 and scheduling-barrier variants lost in round 4, profiles/r4_s3_ab_unaligned.json)
 template <int K, bool CHAIN>
 int dispatch(int variant, const UArgs& A, hipStream_t st) {
-    const int order = variant / 100, u = (variant / 10) % 10;
-    const bool sb = variant % 10 != 0;
-    auto by_u = [&](auto O) -> int {
+    const int waves = variant / 10000, first = (variant / 1000) % 10, order = (variant / 100) % 10,
+              u = (variant / 10) % 10;
+    if (u != 1 || variant % 10 != 0) return DCCL_INVALID_ARGUMENT;
+    auto by_order = [&](auto O) -> int {
         constexpr int ORD = decltype(O)::value;
-        if (u == 1) return sb ? launch_v<K, CHAIN, ORD, 1, true>(A, st) : launch_v<K, CHAIN, ORD, 1, false>(A, st);
-        if (u == 2) return sb ? launch_v<K, CHAIN, ORD, 2, true>(A, st) : launch_v<K, CHAIN, ORD, 2, false>(A, st);
-        if (u == 4) return sb ? launch_v<K, CHAIN, ORD, 4, true>(A, st) : launch_v<K, CHAIN, ORD, 4, false>(A, st);
-        return DCCL_INVALID_ARGUMENT;
+        return first ? launch_v<K, CHAIN, ORD, 1, false, true>(A, st, waves)
+                     : launch_v<K, CHAIN, ORD, 1, false, false>(A, st, waves);
     };
-    if (order == 0) return by_u(std::integral_constant<int, kOrderXcd>{});
-    if (order == 1) return by_u(std::integral_constant<int, kOrderBlock>{});
-    if (order == 2) return by_u(std::integral_constant<int, kOrderGroup>{});
+    if (order == 0) return by_order(std::integral_constant<int, kOrderXcd>{});
+    if (order == 1) return by_order(std::integral_constant<int, kOrderBlock>{});
+    if (order == 2) return by_order(std::integral_constant<int, kOrderGroup>{});
     return DCCL_INVALID_ARGUMENT;
 }
 
@@ -185,7 +242,7 @@ using namespace dccl_amd;
 
 extern "C" int uv4_combine(int variant, const void* const* sends, int k, const void* own, void* dst, size_t count,
                            void* stream) {
-    if (k != 4 && k != 8) return DCCL_INVALID_ARGUMENT;
+    if (k < 2 || k > 8) return DCCL_INVALID_ARGUMENT;
     uv4::UArgs A{};
     const unsigned char* d = static_cast<unsigned char*>(dst);
     for (int j = 0; j < k; ++j) {
@@ -203,7 +260,6 @@ extern "C" int uv4_combine(int variant, const void* const* sends, int k, const v
     A.count = count;
     (void)d;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (own)
-        return k == 4 ? uv4::dispatch<4, true>(variant, A, st) : uv4::dispatch<8, true>(variant, A, st);
-    return k == 4 ? uv4::dispatch<4, false>(variant, A, st) : uv4::dispatch<8, false>(variant, A, st);
+    if (own) return with_k<2, 8>(k, [&](auto K) { return uv4::dispatch<K.value, true>(variant, A, st); });
+    return with_k<2, 8>(k, [&](auto K) { return uv4::dispatch<K.value, false>(variant, A, st); });
 }
