@@ -147,30 +147,34 @@ constexpr size_t pair_lds(bool shifted, bool separate_allocations, size_t bytes)
 // (profiles/r4_s11_ab_first.json, r4_s12_*.json, r4_s13_ab_forms.json, three boxes):
 //   sources in phase, per-operand, block order, 26 waves: k = 3 +3.5, 4 +2.6..+3.2, 5 +2.1, 6 +1.1,
 //     7 +0.9, 8 +0.7..+1.2 points (k <= 2 keeps the round-3 kernels, unaligned_multi.hip);
-//   sources off phase, group-interleaved order: k = 3 per-operand at 26 +1.9..+3.7; k = 4 loads-first at 14
-//     +4.9..+5.3; k = 5 loads-first at 12 +4.6; k = 6..8 per-operand at 26 +0.0..+1.4.
-// The same forms beat the phased kernels (element-aligned destination, sources at other phases) at k = 3..5
-// (+1.2..+2.8, +4.2..+5.0, +2.9..+4.3): those launches take reduce_windows_kernel too (phased_via_windows),
-// except the chain at k = 3, which lost 0.8-1.1 points with the destination off the line grid
-// (profiles/r4_s15_ab_windows_forms.json).
+//   sources off phase: k = 3 per-operand, group-interleaved order, 26 waves +1.9..+3.7; k = 4 loads-first,
+//     group order, 14 waves +4.9..+5.3; k = 5 the same at 12 +4.6; k = 6..8 loads-first in runs of 4 tiles
+//     (run_tile<4>) at 13 waves: k = 6, 7 +2.5..+3.6, k = 8 +0.5..+1.2 (r4_s17_ab_runs.json, r4_s18_ab_runs2.json).
+// PMC traffic stays within 2 % of (k+1)·N reads and N writes (k = 8 sources + 4 B: 1.02 x, r4_s18_pmc/): what
+// is left at k = 8 off phase (75 %) is how the DRAM serves ten concurrent streams, not re-reads.
+// The same forms beat the phased kernels (element-aligned destination, sources at other phases) at k-way
+// k = 3..5 (+1.2..+2.8, +4.2..+5.0, +2.9..+4.3) and chain k = 4..7 (+4.2..+5.0, +2.8..+4.3, +2.9..+3.0,
+// +1.9..+2.1): those launches take reduce_windows_kernel too (phased_via_windows).  Not the chain at k = 3
+// (-0.8..-1.1 with the destination off the line grid, r4_s15_ab_windows_forms.json), nor k-way k = 6, 7
+// (+0.4..+1.0, below the 2-point bar), nor k = 8 (the phased kernels lead).
 // Launches below kWindowTunedBytes per operand keep the uncapped per-operand form (not swept).
 inline constexpr size_t kWindowTunedBytes = size_t(96) << 20;
 enum WindowClass : int { kWinInPhase = 0, kWinOffPhase, kNumWindowClasses };
 struct WindowForm {
     unsigned char first;  // 1: loads-first tile
-    unsigned char order;  // reduce_kernels.hpp kOrderXcd (0), kOrderBlock (1), kOrderGroup (2)
+    unsigned char order;  // reduce_kernels.hpp kOrderXcd (0), kOrderBlock (1), kOrderGroup (2), kOrderRun4 (3)
     unsigned char waves;  // resident-wave cap (32 = uncapped)
 };
 inline constexpr WindowForm kWindow[kNumWindowClasses][9] = {
     // k = 0, 1, 2: the round-3 kernels (in phase) or the uncapped XCD-range form (off phase)
     {{0, 1, 32}, {0, 1, 32}, {0, 1, 32}, {0, 1, 26}, {0, 1, 26}, {0, 1, 26}, {0, 1, 26}, {0, 1, 26}, {0, 1, 26}},
-    {{0, 0, 32}, {0, 0, 32}, {0, 0, 32}, {0, 2, 26}, {1, 2, 14}, {1, 2, 12}, {0, 2, 26}, {0, 2, 26}, {0, 2, 26}},
+    {{0, 0, 32}, {0, 0, 32}, {0, 0, 32}, {0, 2, 26}, {1, 2, 14}, {1, 2, 12}, {1, 3, 13}, {1, 3, 13}, {1, 3, 13}},
 };
 constexpr WindowForm window_form(WindowClass c, int k) { return kWindow[c][k < 0 ? 0 : k > 8 ? 8 : k]; }
 // Element-aligned destinations with sources at other phases: reduce_windows_kernel's tuned form instead of
 // the phased kernels, from kWindowTunedBytes.
 constexpr bool phased_via_windows(bool chain, int k, size_t bytes) {
-    return k >= (chain ? 4 : 3) && k <= 5 && bytes >= kWindowTunedBytes;
+    return k >= (chain ? 4 : 3) && k <= (chain ? 7 : 5) && bytes >= kWindowTunedBytes;
 }
 
 // ---- checks of the table, at every build ----
@@ -197,11 +201,11 @@ constexpr bool window_table_ok() {
     for (int c = 0; c < kNumWindowClasses; ++c)
         for (int k = 0; k <= 8; ++k) {
             const WindowForm f = kWindow[c][k];
-            if (f.order > 2 || f.first > 1 || f.waves < 7 || f.waves > kUncapped) return false;
+            if (f.order > 3 || f.first > 1 || f.waves < 7 || f.waves > kUncapped) return false;
             if (f.first && f.waves == kUncapped) return false;  // the loads-first tile only under a cap
             if (lds_for_waves(f.waves) > kMaxLdsPerBlock) return false;
         }
-    for (int k = 3; k <= 5; ++k)  // the phased launches routed to the windows kernel take a tuned off-phase form
+    for (int k = 3; k <= 7; ++k)  // the phased launches routed to the windows kernel take a tuned off-phase form
         if (kWindow[kWinOffPhase][k].waves == kUncapped) return false;
     return true;
 }

@@ -535,6 +535,8 @@ template <int ORDER>
 __device__ __forceinline__ size_t first_tile(size_t b, size_t g) {
     if constexpr (ORDER == kOrderXcd) return (b % 8) * (g / 8) + b / 8;
     else if constexpr (ORDER == kOrderBlock) return b;
+    else if constexpr (ORDER == kOrderRun4) return run_tile<4>(b, g);
+    else if constexpr (ORDER == kOrderRun2) return run_tile<2>(b, g);
     else return xcd_group_tile(b, g);
 }
 

@@ -149,12 +149,14 @@ def test_separate_allocation_rule(table):
 
 def test_window_forms(table):
     """reduce_windows_kernel's tuned forms (caps.hpp kWindow): per-operand block order under 26
-    waves in phase from k = 3; off phase group order, per-operand at 26 except loads-first at k = 4 (14 waves)
-    and k = 5 (12); k <= 2 uncapped; the phased launches at k = 3..5 (chain 4..5) from 96 MiB per operand."""
+    waves in phase from k = 3; off phase per-operand in group order at k = 3 (26), loads-first in group order at
+    k = 4 (14 waves) and 5 (12), loads-first in runs of 4 at k = 6..8 (13); k <= 2 uncapped; the phased launches
+    at k-way k = 3..5 and chain k = 4..7 from 96 MiB per operand."""
     want = {0: {k: (10, 26 if k >= 3 else 32) for k in range(9)},
-            1: {k: (0, 32) if k <= 2 else (120, 14) if k == 4 else (120, 12) if k == 5 else (20, 26) for k in range(9)}}
+            1: {k: (0, 32) if k <= 2 else (20, 26) if k == 3 else (120, 14) if k == 4 else (120, 12) if k == 5
+                else (130, 13) for k in range(9)}}
     for c, k, form, w, lds in table["windows"]:
         assert (form, w) == want[c][k], (c, k, form, w)
         assert lds == lds_for(w) and lds <= 64 << 10
-    assert table["phased_via_windows"] == [[ch, k, 0, int((4 if ch else 3) <= k <= 5)] for ch in (0, 1)
+    assert table["phased_via_windows"] == [[ch, k, 0, int((4 <= k <= 7) if ch else (3 <= k <= 5))] for ch in (0, 1)
                                            for k in range(1, 9)]

@@ -379,11 +379,12 @@ def _torch_op(op):
     return {0: torch.add, 1: torch.mul, 2: torch.maximum, 3: torch.minimum}[op]
 
 
-@pytest.mark.parametrize("k", [3, 4, 5, 6, 8])
+@pytest.mark.parametrize("k", [3, 4, 5, 6, 7, 8])
 def test_windows_tuned_forms_full_size(dccl, k):
     """From caps::kWindowTunedBytes (96 MiB per operand) reduce_windows_kernel takes its tuned forms (caps.hpp
-    kWindow: block order under a 26-wave cap with sources in phase; group order, loads-first at k = 4, 5 under
-    14 / 12 waves, with sources off phase) and takes over the phased launches at k = 3..5.  Destination not
+    kWindow: block order under a 26-wave cap with sources in phase; with sources off phase group order, loads-
+    first at k = 4, 5 under 14 / 12 waves, loads-first in runs of 4 tiles at k = 6..8) and takes over the phased
+    launches at k-way k = 3..5 and chain k = 4..7.  Destination not
     element-aligned, and element-aligned at 16-B phases 0 and 4; sources at phase 0 and 4; k-way and chain in
     place; fp32 Sum, int32 Max, bf16 Sum, against torch applied on the device in the kernels' order, bit for
     bit; nothing outside the destination written."""

@@ -35,6 +35,8 @@ template <int ORDER>
 __device__ __forceinline__ size_t first_tile(size_t b, size_t g) {
     if constexpr (ORDER == kOrderXcd) return (b % 8) * (g / 8) + b / 8;
     else if constexpr (ORDER == kOrderBlock) return b;
+    else if constexpr (ORDER == kOrderRun4) return run_tile<4>(b, g);
+    else if constexpr (ORDER == kOrderRun2) return run_tile<2>(b, g);
     else return xcd_group_tile(b, g);
 }
 
@@ -217,7 +219,7 @@ int launch_v(const UArgs& A, hipStream_t st, int waves) {
 }
 
 // variant = 10000 * waves + 1000 * first + 100 * order + 10 * U   (waves: resident-wave cap per CU, 0
-// uncapped; first 1: the loads-first tile (U = 1); order 0 xcd, 1 block, 2 group; U 1 vector per lane --
+// uncapped; first 1: the loads-first tile (U = 1); order 0 xcd, 1 block, 2 group, 3 runs of 4, 4 runs of 2; U 1 vector per lane --
 // the U = 2, 4 and scheduling-barrier variants lost in round 4, profiles/r4_s3_ab_unaligned.json)
 template <int K, bool CHAIN>
 int dispatch(int variant, const UArgs& A, hipStream_t st) {
@@ -232,6 +234,8 @@ int dispatch(int variant, const UArgs& A, hipStream_t st) {
     if (order == 0) return by_order(std::integral_constant<int, kOrderXcd>{});
     if (order == 1) return by_order(std::integral_constant<int, kOrderBlock>{});
     if (order == 2) return by_order(std::integral_constant<int, kOrderGroup>{});
+    if (order == 3) return by_order(std::integral_constant<int, kOrderRun4>{});
+    if (order == 4) return by_order(std::integral_constant<int, kOrderRun2>{});
     return DCCL_INVALID_ARGUMENT;
 }
 
