@@ -43,6 +43,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="110,260110,121110,121210")
     ap.add_argument("--ks", default="4,8")
+    ap.add_argument("--mib", type=int, default=1024, help="bytes per operand (MiB)")
     ap.add_argument("--cases", default="")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=10)
@@ -54,7 +55,7 @@ def main():
                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
     lib = dccl_amd.lib
     st = torch.cuda.current_stream().cuda_stream
-    nbytes = 1 << 30
+    nbytes = a.mib << 20
     n = nbytes // 4 - 64
     pool = torch.empty(10 * nbytes + 4096 * 55 + 1024, dtype=torch.uint8, device="cuda")
     ptrs, off = [], 0
