@@ -446,11 +446,14 @@ struct Peers {
     Peers() = default;
     Peers(const Peers&) = delete;
     Peers& operator=(const Peers&) = delete;
-    ~Peers() {
+    ~Peers() { release(); }
+    // This rank no longer reads through the mappings (its stream has drained past the last kernel that did).
+    void release() {
         if (held.empty()) return;
         ProcCache& pc = cache();
         std::lock_guard<std::mutex> lock(pc.mu);
         for (const auto& k : held) pc.imports.release(k.first, k.second);
+        held.clear();
     }
 };
 
@@ -499,11 +502,15 @@ ncclResult_t import_desc(ProcCache& pc, uint32_t peer, int64_t pid, const Desc& 
 // complete) and every rank got here.  It agrees on success: a rank whose step failed (rc) still comes
 // here, and every rank returns an error from the same phase point if any rank failed, so no rank is
 // left waiting at a later barrier and no rank goes on to read a peer's unfinished chunk.
-ncclResult_t arrive(dcclComm* c, hipStream_t st, ncclResult_t rc = dccl::ncclSuccess) {
+// `done` (the collective's last phase point): its peer mappings are released once the stream has drained,
+// before the barrier, so no use is held while this rank waits for the others (another thread's
+// communicator can then retire and close them without waiting for this collective to return).
+ncclResult_t arrive(dcclComm* c, hipStream_t st, ncclResult_t rc = dccl::ncclSuccess, Peers* done = nullptr) {
     if (hipStreamSynchronize(st) != hipSuccess) {  // drained even after a failed launch: peers' reads end
         (void)hipGetLastError();
         if (rc == dccl::ncclSuccess) rc = dccl::ncclUnhandledCudaError;
     }
+    if (done != nullptr) done->release();
     const bool ok = rc == dccl::ncclSuccess;
     const ncclResult_t all = c->ipc ? shm_barrier(xport(c), ok)
                                     : (c->group->barrier(ok) ? dccl::ncclSuccess : dccl::ncclRemoteError);
@@ -878,7 +885,7 @@ ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t
         src.push_back(P.out[(k + W - 1) % W] + k * slot);  // chunk k lives on rank k-1
         dst.push_back(static_cast<unsigned char*>(recv) + k * slot);
     }
-    return arrive(c, st, copy_pairs(src, dst, slot, st));  // peers are done reading our buffers
+    return arrive(c, st, copy_pairs(src, dst, slot, st), &P);  // peers are done reading our buffers
 }
 
 bool host_direct_selected(const dcclComm* c, size_t slot_bytes) {
@@ -958,7 +965,7 @@ ncclResult_t direct_reduce_scatter(dcclComm* c, const void* send, void* recv, si
     ncclResult_t rc = exchange(c, &pub, st, &P, &met);
     if (!met) return rc;
     if (rc == dccl::ncclSuccess) rc = chain(P, W, (r + 1) % W, r * slot, P.in[r] + r * slot, recv, recvcount, dtype, op, st, r);
-    return arrive(c, st, rc);
+    return arrive(c, st, rc, &P);
 }
 
 // ncclReduce: the reference runs the reduce-scatter ring with the same maps, then gathers the slots
@@ -979,7 +986,7 @@ ncclResult_t direct_reduce(dcclComm* c, const void* send, void* recv, size_t cou
         for (uint32_t o = 0; o < W && rc == dccl::ncclSuccess; ++o)
             rc = chain(P, W, (o + 1) % W, o * slot, P.in[o] + o * slot, static_cast<unsigned char*>(recv) + o * slot,
                        slot_elems, dtype, op, st, r);
-    return arrive(c, st, rc);
+    return arrive(c, st, rc, &P);
 }
 
 ncclResult_t direct_all_gather(dcclComm* c, const void* send, void* recv, size_t sendcount, int dtype,
@@ -1006,7 +1013,7 @@ ncclResult_t direct_all_gather(dcclComm* c, const void* send, void* recv, size_t
         }
         rc = copy_pairs(src, dst, slot, st);
     }
-    return arrive(c, st, rc);
+    return arrive(c, st, rc, &P);
 }
 
 ncclResult_t direct_broadcast(dcclComm* c, const void* send, void* recv, size_t count, int dtype, uint32_t root,
@@ -1028,7 +1035,7 @@ ncclResult_t direct_broadcast(dcclComm* c, const void* send, void* recv, size_t 
         std::vector<void*> dst{recv};
         rc = copy_pairs(src, dst, bytes, st);
     }
-    return arrive(c, st, rc);
+    return arrive(c, st, rc, &P);
 }
 
 }  // namespace dccl_amd

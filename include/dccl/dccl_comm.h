@@ -29,7 +29,9 @@
  *                         ends every other rank's wait with ncclRemoteError within ~0.1 s; a live peer that
  *                         never arrives, after DCCL_IPC_TIMEOUT_S (default 60 s).  Communicators of one
  *                         process share one mapping cache under one mutex: collectives driven from several
- *                         threads at once serialise while they map peer buffers.
+ *                         threads at once serialise while they map peer buffers (a failing open retries
+ *                         for up to ~0.5 s under it); a collective releases its mappings once its stream
+ *                         has drained, before its last barrier.
  *   dccl_comm_register /  dcclRegisterCacheMemory / dcclDeregisterCacheMemory (/root/reference/src/core/
  *   dccl_comm_deregister  dccl.cpp:503-549): 64-byte aligned address and size.  Host memory is page-locked.
  *                         Device memory on an IPC communicator becomes an export peers map in place until

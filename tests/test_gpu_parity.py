@@ -386,18 +386,18 @@ def test_windows_tuned_forms_full_size(dccl, k):
     first at k = 4, 5 under 14 / 12 waves, loads-first in runs of 4 tiles at k = 6..8) and takes over the phased
     launches at k-way k = 3..5 and chain k = 4..7.  Destination not
     element-aligned, and element-aligned at 16-B phases 0 and 4; sources at phase 0 and 4; k-way and chain in
-    place; fp32 Sum, int32 Max, bf16 Sum, against torch applied on the device in the kernels' order, bit for
+    place; fp32 Sum, int32 Max, bf16 Sum, int64 Min, against torch applied on the device in the kernels' order, bit for
     bit; nothing outside the destination written."""
     nb = (96 << 20) + 4096
     for dt, tdt, ibits, op in [(7, torch.float32, torch.int32, 0), (2, torch.int32, torch.int32, 2),
-                               (9, torch.bfloat16, torch.int16, 0)]:
+                               (9, torch.bfloat16, torch.int16, 0), (4, torch.int64, torch.int64, 3)]:
         esz = torch.empty(0, dtype=tdt).element_size()
         n = nb // esz
         mis = 1 if esz == 2 else 2
         g = torch.Generator(device="cuda").manual_seed(2400 + k + dt)
 
         def operand():
-            if tdt == torch.int32:
+            if tdt in (torch.int32, torch.int64):
                 return torch.randint(-(1 << 30), 1 << 30, (n,), device="cuda", dtype=tdt, generator=g)
             return (torch.rand(n, device="cuda", generator=g) * 2 - 1).to(tdt)
 
