@@ -34,7 +34,8 @@ def main():
     a = ap.parse_args()
     lib = ctypes.CDLL(LIB)
     lib.ps_combine.restype = ctypes.c_int
-    lib.ps_combine.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    lib.ps_combine.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                               ctypes.c_void_p]
     variants = [int(v) for v in a.variants.split(",")]
     dev = torch.device("cuda", 0)
     rows = []
@@ -52,7 +53,7 @@ def main():
         def call(v, ps, pr, sh):
             if v < 0:
                 return dccl_amd.local_reduce(ps, pr, 7, n, 0, sh)
-            return lib.ps_combine(v, ps, pr, n, sh)
+            return lib.ps_combine(v, 0, ps, pr, n, sh)
 
         # bit-exactness on pair 0 (recv restored between runs)
         saved = bufs[0][:nb].clone()
