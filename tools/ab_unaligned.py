@@ -36,6 +36,8 @@ def cases(ptrs, ks):
             t[f"chain{k}_dst+2{sname}"] = (k, s, recv + 2, recv + 2)
         t[f"chain{k}_src+4"] = (k, [p + 4 for p in src[:k]], recv, recv)
         t[f"multi{k}_src+4"] = (k, [p + 4 for p in src[:k]], None, recv)
+        t[f"chain{k}"] = (k, src[:k], recv, recv)  # every operand in phase and on the line grid
+        t[f"multi{k}"] = (k, src[:k], None, recv)
     return t
 
 
