@@ -190,7 +190,7 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
     }
     if (!vec_ok) {  // an element-aligned recv and sources at other 16-B (or byte) phases: the phased kernel
         if constexpr (sizeof(T) > 1) {
-            if (caps::phased_via_windows(false, nsend, count * sizeof(T))) {  // or the windows kernel (caps.hpp)
+            if (caps::phased_via_windows(false, nsend, count * sizeof(T), (ar & 15) == 0)) {  // or the windows kernel (caps.hpp)
                 PhaseList ph{};
                 for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], 0);
                 return multi_unaligned_typed<T, OP>(sl, ph, nsend, r, count, stream);
@@ -274,7 +274,7 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
     }
     if (!vec_ok) {  // an element-aligned dst and operands at other 16-B (or byte) phases: the phased kernel
         if constexpr (sizeof(T) > 1) {
-            if (caps::phased_via_windows(true, nsend, count * sizeof(T))) {  // or the windows kernel (caps.hpp)
+            if (caps::phased_via_windows(true, nsend, count * sizeof(T), (ad & 15) == 0)) {  // or the windows kernel (caps.hpp)
                 PhaseList ph{};
                 for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], 0);
                 ph.p[nsend] = phase_word(o, 0);

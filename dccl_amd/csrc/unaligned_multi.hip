@@ -1,6 +1,6 @@
 // dccl_amd/csrc/unaligned_multi.hip — the k-way and chain combines into a destination that is not
 // element-aligned (reduce_windows_kernel, and the round-3 forms for k <= 2, in reduce_kernels.hpp), and the
-// phased launches that caps::phased_via_windows routes here (element-aligned destination, k = 3..5).
+// phased launches that caps::phased_via_windows routes here (element-aligned destination).
 // Instantiated for every (T, OP) with sizeof(T) > 1 (a one-byte element is always aligned), in a
 // translation unit of its own, so the build compiles it beside local_reduce.hip.
 #include <hip/hip_runtime.h>
@@ -88,6 +88,10 @@ int launch_windows(const SendList& sl, const PhaseList& ph, const unsigned char*
     if (count * sizeof(T) >= caps::kWindowTunedBytes)
         return off ? launch_tuned<T, OP, K, CHAIN, caps::kWinOffPhase>(A, stream)
                    : launch_tuned<T, OP, K, CHAIN, caps::kWinInPhase>(A, stream);
+    if (off && caps::window_mid(K, count * sizeof(T))) {
+        constexpr caps::WindowForm f = caps::kWindowMidOff;
+        return launch_form<T, OP, K, CHAIN, f.first != 0, int(f.order)>(A, stream, caps::lds_for_waves(f.waves));
+    }
     switch (unaligned_order(ph, K)) {  // smaller launches: the per-operand form, uncapped
     case kOrderXcd: return launch_form<T, OP, K, CHAIN, false, kOrderXcd>(A, stream, 0);
     case kOrderBlock: return launch_form<T, OP, K, CHAIN, false, kOrderBlock>(A, stream, 0);

@@ -50,6 +50,13 @@ int main() {
             std::printf("%s[%d, %d, %d, %d, %zu]", (c || k) ? ", " : "", c, k, f.first * 100 + f.order * 10, f.waves,
                         lds_for_waves(f.waves));
         }
+    std::printf("], \"window_mid\": [");
+    const size_t mids[] = {kWindowMidBytes - 1, kWindowMidBytes, kWindowTunedBytes - 1, kWindowTunedBytes};
+    for (int k = 1; k <= 8; ++k)
+        for (size_t b : mids)
+            std::printf("%s[%d, %zu, %d, %d, %d]", (k > 1 || b != mids[0]) ? ", " : "", k, b, int(window_mid(k, b)),
+                        int(phased_via_windows(false, k, b, true)), int(phased_via_windows(true, k, b, false)));
+    std::printf("], \"mid_form\": [%d, %d, %d", int(kWindowMidOff.first), int(kWindowMidOff.order), int(kWindowMidOff.waves));
     std::printf("], \"phased_via_windows\": [");
     for (int ch = 0; ch < 2; ++ch)
         for (int k = 1; k <= 8; ++k)
@@ -160,3 +167,17 @@ def test_window_forms(table):
         assert lds == lds_for(w) and lds <= 64 << 10
     assert table["phased_via_windows"] == [[ch, k, 0, int((4 <= k <= 7) if ch else (3 <= k <= 5))] for ch in (0, 1)
                                            for k in range(1, 9)]
+
+
+def test_window_mid_sizes(table):
+    """From 48 to 96 MiB per operand (caps.hpp window_mid): k = 5..8 with sources off phase take the loads-first
+    tile in group order under 14 waves, and phased launches with the destination at 16-B phase 0 take it too;
+    from 96 MiB the 1 GiB table rules (phased routing independent of the destination's phase)."""
+    assert table["mid_form"] == [1, 2, 14]
+    for k, b, mid, via_multi_dst16, via_chain_not16 in table["window_mid"]:
+        in_mid = (48 << 20) <= b < (96 << 20)
+        assert mid == int(5 <= k <= 8 and in_mid), (k, b)
+        if b >= 96 << 20:
+            assert via_multi_dst16 == int(3 <= k <= 5) and via_chain_not16 == int(4 <= k <= 7), (k, b)
+        else:
+            assert via_multi_dst16 == mid and via_chain_not16 == 0, (k, b)

@@ -379,16 +379,19 @@ def _torch_op(op):
     return {0: torch.add, 1: torch.mul, 2: torch.maximum, 3: torch.minimum}[op]
 
 
+@pytest.mark.parametrize("mib", [64, 96])
 @pytest.mark.parametrize("k", [3, 4, 5, 6, 7, 8])
-def test_windows_tuned_forms_full_size(dccl, k):
+def test_windows_tuned_forms_full_size(dccl, k, mib):
     """From caps::kWindowTunedBytes (96 MiB per operand) reduce_windows_kernel takes its tuned forms (caps.hpp
     kWindow: block order under a 26-wave cap with sources in phase; with sources off phase group order, loads-
     first at k = 4, 5 under 14 / 12 waves, loads-first in runs of 4 tiles at k = 6..8) and takes over the phased
-    launches at k-way k = 3..5 and chain k = 4..7.  Destination not
+    launches at k-way k = 3..5 and chain k = 4..7; at 64 MiB (caps.hpp window_mid) k = 5..8 with sources off
+    phase take the loads-first tile in group order, phased launches into a 16-B aligned destination too.
+    Destination not
     element-aligned, and element-aligned at 16-B phases 0 and 4; sources at phase 0 and 4; k-way and chain in
     place; fp32 Sum, int32 Max, bf16 Sum, int64 Min, against torch applied on the device in the kernels' order, bit for
     bit; nothing outside the destination written."""
-    nb = (96 << 20) + 4096
+    nb = (mib << 20) + 4096
     for dt, tdt, ibits, op in [(7, torch.float32, torch.int32, 0), (2, torch.int32, torch.int32, 2),
                                (9, torch.bfloat16, torch.int16, 0), (4, torch.int64, torch.int64, 3)]:
         esz = torch.empty(0, dtype=tdt).element_size()
