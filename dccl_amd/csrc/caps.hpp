@@ -157,14 +157,15 @@ constexpr size_t pair_lds(bool shifted, bool separate_allocations, size_t bytes)
 // +1.9..+2.1): those launches take reduce_windows_kernel too (phased_via_windows).  Not the chain at k = 3
 // (-0.8..-1.1 with the destination off the line grid, r4_s15_ab_windows_forms.json), nor k-way k = 6, 7
 // (+0.4..+1.0, below the 2-point bar), nor k = 8 (the phased kernels lead).
-// From kWindowMidBytes to kWindowTunedBytes per operand (operands partly inside the 256 MiB Infinity Cache,
-// so only k >= 5 was judged, r4_s20_ab_64mib.json, 64 MiB): with sources off phase the loads-first tile in group
-// order under 14 waves, +0.5..+1.6 points into a misaligned destination and +4.0..+7.3 over the phased kernels
-// (element-aligned destination at 16-B phase 0); everything else there, and every launch below
-// kWindowMidBytes, keeps the uncapped per-operand form (not swept).
+// From kWindowMidBytes to kWindowTunedBytes per operand (r4_s20_ab_64mib.json; 64-88 MiB A/B of the shipped
+// build, r4_s26_ab_mid*.json, r4_s27_ab_mid*_k34.json), sources off phase: k = 4..8 the loads-first tile in
+// group order under 14 waves, +0.0..+2.6 points into a misaligned destination and +3.0..+6.6 over the phased
+// kernels (element-aligned destination at 16-B phase 0); the chain at k = 3 per-operand in group order under
+// 26 waves (+4.9..+6.0 over the phased kernel; the k-way at k = 3 lost 0.3-3.8 and keeps its kernels);
+// everything else there, and every launch below kWindowMidBytes, keeps the uncapped per-operand form.
 inline constexpr size_t kWindowTunedBytes = size_t(96) << 20;
 inline constexpr size_t kWindowMidBytes = size_t(48) << 20;
-inline constexpr int kWindowMidMinK = 5;
+inline constexpr int kWindowMidMinK = 4;  // k-way; the chain from k = 3
 enum WindowClass : int { kWinInPhase = 0, kWinOffPhase, kNumWindowClasses };
 struct WindowForm {
     unsigned char first;  // 1: loads-first tile
@@ -177,16 +178,18 @@ inline constexpr WindowForm kWindow[kNumWindowClasses][9] = {
     {{0, 0, 32}, {0, 0, 32}, {0, 0, 32}, {0, 2, 26}, {1, 2, 14}, {1, 2, 12}, {1, 3, 13}, {1, 3, 13}, {1, 3, 13}},
 };
 constexpr WindowForm window_form(WindowClass c, int k) { return kWindow[c][k < 0 ? 0 : k > 8 ? 8 : k]; }
-inline constexpr WindowForm kWindowMidOff = {1, 2, 14};
-constexpr bool window_mid(int k, size_t bytes) {
-    return k >= kWindowMidMinK && k <= 8 && bytes >= kWindowMidBytes && bytes < kWindowTunedBytes;
+inline constexpr WindowForm kWindowMidOff[9] = {{0, 0, 32}, {0, 0, 32}, {0, 0, 32}, {0, 2, 26}, {1, 2, 14},
+                                                 {1, 2, 14}, {1, 2, 14}, {1, 2, 14}, {1, 2, 14}};
+constexpr WindowForm window_mid_form(int k) { return kWindowMidOff[k < 0 ? 0 : k > 8 ? 8 : k]; }
+constexpr bool window_mid(bool chain, int k, size_t bytes) {
+    return k >= (chain ? 3 : kWindowMidMinK) && k <= 8 && bytes >= kWindowMidBytes && bytes < kWindowTunedBytes;
 }
 // Element-aligned destinations with sources at other phases: reduce_windows_kernel's tuned form instead of
 // the phased kernels, from kWindowTunedBytes; and its mid-size form (window_mid) for a destination at 16-B
 // phase 0 (so some source is off phase).
 constexpr bool phased_via_windows(bool chain, int k, size_t bytes, bool dst16 = false) {
     if (bytes >= kWindowTunedBytes) return k >= (chain ? 4 : 3) && k <= (chain ? 7 : 5);
-    return dst16 && window_mid(k, bytes);
+    return dst16 && window_mid(chain, k, bytes);
 }
 
 // ---- checks of the table, at every build ----

@@ -88,8 +88,8 @@ int launch_windows(const SendList& sl, const PhaseList& ph, const unsigned char*
     if (count * sizeof(T) >= caps::kWindowTunedBytes)
         return off ? launch_tuned<T, OP, K, CHAIN, caps::kWinOffPhase>(A, stream)
                    : launch_tuned<T, OP, K, CHAIN, caps::kWinInPhase>(A, stream);
-    if (off && caps::window_mid(K, count * sizeof(T))) {
-        constexpr caps::WindowForm f = caps::kWindowMidOff;
+    if (off && caps::window_mid(CHAIN, K, count * sizeof(T))) {
+        constexpr caps::WindowForm f = caps::window_mid_form(K);
         return launch_form<T, OP, K, CHAIN, f.first != 0, int(f.order)>(A, stream, caps::lds_for_waves(f.waves));
     }
     switch (unaligned_order(ph, K)) {  // smaller launches: the per-operand form, uncapped

@@ -52,11 +52,16 @@ int main() {
         }
     std::printf("], \"window_mid\": [");
     const size_t mids[] = {kWindowMidBytes - 1, kWindowMidBytes, kWindowTunedBytes - 1, kWindowTunedBytes};
-    for (int k = 1; k <= 8; ++k)
-        for (size_t b : mids)
-            std::printf("%s[%d, %zu, %d, %d, %d]", (k > 1 || b != mids[0]) ? ", " : "", k, b, int(window_mid(k, b)),
-                        int(phased_via_windows(false, k, b, true)), int(phased_via_windows(true, k, b, false)));
-    std::printf("], \"mid_form\": [%d, %d, %d", int(kWindowMidOff.first), int(kWindowMidOff.order), int(kWindowMidOff.waves));
+    for (int ch = 0; ch < 2; ++ch)
+        for (int k = 1; k <= 8; ++k)
+            for (size_t b : mids)
+                std::printf("%s[%d, %d, %zu, %d, %d, %d]", (ch || k > 1 || b != mids[0]) ? ", " : "", ch, k, b,
+                            int(window_mid(ch, k, b)), int(phased_via_windows(ch, k, b, true)),
+                            int(phased_via_windows(ch, k, b, false)));
+    std::printf("], \"mid_form\": [");
+    for (int k = 0; k <= 8; ++k)
+        std::printf("%s%d", k ? ", " : "", window_mid_form(k).first * 1000 + window_mid_form(k).order * 100 +
+                                               window_mid_form(k).waves);
     std::printf("], \"phased_via_windows\": [");
     for (int ch = 0; ch < 2; ++ch)
         for (int k = 1; k <= 8; ++k)
@@ -170,14 +175,16 @@ def test_window_forms(table):
 
 
 def test_window_mid_sizes(table):
-    """From 48 to 96 MiB per operand (caps.hpp window_mid): k = 5..8 with sources off phase take the loads-first
-    tile in group order under 14 waves, and phased launches with the destination at 16-B phase 0 take it too;
-    from 96 MiB the 1 GiB table rules (phased routing independent of the destination's phase)."""
-    assert table["mid_form"] == [1, 2, 14]
-    for k, b, mid, via_multi_dst16, via_chain_not16 in table["window_mid"]:
+    """From 48 to 96 MiB per operand (caps.hpp window_mid): with sources off phase, k = 4..8 take the loads-first
+    tile in group order under 14 waves and the chain at k = 3 the per-operand tile in group order under 26;
+    phased launches with the destination at 16-B phase 0 take them too.  From 96 MiB the 1 GiB table rules
+    (phased routing independent of the destination's phase)."""
+    assert table["mid_form"] == [32, 32, 32, 226, 1214, 1214, 1214, 1214, 1214]
+    for ch, k, b, mid, via_dst16, via_not16 in table["window_mid"]:
         in_mid = (48 << 20) <= b < (96 << 20)
-        assert mid == int(5 <= k <= 8 and in_mid), (k, b)
+        assert mid == int((3 if ch else 4) <= k <= 8 and in_mid), (ch, k, b)
         if b >= 96 << 20:
-            assert via_multi_dst16 == int(3 <= k <= 5) and via_chain_not16 == int(4 <= k <= 7), (k, b)
+            want = int((4 <= k <= 7) if ch else (3 <= k <= 5))
+            assert via_dst16 == want and via_not16 == want, (ch, k, b)
         else:
-            assert via_multi_dst16 == mid and via_chain_not16 == 0, (k, b)
+            assert via_dst16 == mid and via_not16 == 0, (ch, k, b)
