@@ -38,6 +38,9 @@ def cases(ptrs, ks):
         t[f"multi{k}_src+4"] = (k, [p + 4 for p in src[:k]], None, recv)
         t[f"chain{k}"] = (k, src[:k], recv, recv)  # every operand in phase and on the line grid
         t[f"multi{k}"] = (k, src[:k], None, recv)
+        strad = [p + 16 * (2 * j + 1) for j, p in enumerate(src[:k])]  # in phase, off recv's 128-B lines
+        t[f"chain{k}_strad"] = (k, strad, recv, recv)
+        t[f"multi{k}_strad"] = (k, strad, None, recv)
     return t
 
 
