@@ -191,6 +191,22 @@ constexpr bool phased_via_windows(bool chain, int k, size_t bytes, bool dst16 = 
     if (bytes >= kWindowTunedBytes) return k >= (chain ? 4 : 3) && k <= (chain ? 7 : 5);
     return dst16 && window_mid(chain, k, bytes);
 }
+// Straddling sources (every operand at the 16-B aligned destination's phase, some off its 128-B lines): the
+// mid-size window form (window_mid_form) instead of the straddle kernels in a per-k size band.  The window
+// form runs flat at 77-80 % of (k+2)·N from 48 to 96 MiB; the straddle kernels climb with size at k = 7, 8,
+// so the band ends where they catch up.  tools/ab_cases.py, shipped build against the build with this route
+// from 48 to 96 MiB at k = 5..8, fp32 Sum, 7 rounds, two boxes (profiles/r4_s31_ab_strad*.json at 48/64/88
+// MiB, r4_s32_ab_strad*.json at 56/64/72/80/88 MiB), k-way / chain: k = 5 from 72 MiB +2.2..+3.3 / +2.5..+3.0
+// (64 MiB +0.1..+0.7); k = 6 from 56 MiB +2.8..+5.0 / +1.2..+2.0 (48 MiB -0.4..+0.2); k = 7 56-80 MiB
+// +1.3..+3.0 / +0.6..+3.1 (88 MiB +0.6..+1.7); k = 8 56-72 MiB +2.1..+4.2 / +0.8..+3.9 (80 MiB -0.8..+1.2,
+// 88 MiB -1.5..-0.5).  Every result bit-exact against the straddle kernels.
+struct MibBand { unsigned short lo, hi; };  // [lo, hi) MiB per operand
+inline constexpr MibBand kStradMid[9] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {72, 96}, {56, 96}, {56, 80}, {56, 72}};
+constexpr bool strad_via_windows(int k, size_t bytes) {
+    if (k < 0 || k > 8) return false;
+    const MibBand b = kStradMid[k];
+    return bytes >= (size_t(b.lo) << 20) && bytes < (size_t(b.hi) << 20);
+}
 
 // ---- checks of the table, at every build ----
 constexpr bool table_ok() {
@@ -225,6 +241,18 @@ constexpr bool window_table_ok() {
     return true;
 }
 static_assert(window_table_ok(), "window forms: legal orders and caps, loads-first only capped");
+constexpr bool strad_table_ok() {
+    for (int k = 0; k <= 8; ++k) {
+        const MibBand b = kStradMid[k];
+        if (b.lo == b.hi) continue;
+        // inside window_mid's range, where launch_windows takes the mid-size form
+        if (b.lo >= b.hi || (size_t(b.lo) << 20) < kWindowMidBytes || (size_t(b.hi) << 20) > kWindowTunedBytes ||
+            k < kWindowMidMinK)
+            return false;
+    }
+    return true;
+}
+static_assert(strad_table_ok(), "straddle bands lie inside the mid-size window range");
 static_assert(size_class((size_t(24) << 20) - 1) == 0 && size_class(size_t(24) << 20) == 1 &&
                   size_class(size_t(48) << 20) == 2 && size_class(size_t(96) << 20) == 3,
               "size-class boundaries at 24 / 48 / 96 MiB");

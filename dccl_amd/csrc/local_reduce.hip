@@ -202,8 +202,15 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
         return multi_phased_typed<T, OP>(sl, ph, nsend, r, sp, stream);
     }
     const Split sp = split_for_vectors<T>(ar, count, recv_align());
-    if (any_straddles(sl, nsend, sp.head * sizeof(T)))
+    if (any_straddles(sl, nsend, sp.head * sizeof(T))) {
+        if constexpr (sizeof(T) > 1) {
+            if ((ar & 15) == 0 && caps::strad_via_windows(nsend, count * sizeof(T))) {  // mid-size form (caps.hpp)
+                PhaseList ph{};
+                return multi_unaligned_typed<T, OP>(sl, ph, nsend, r, count, stream);
+            }
+        }
         return multi_straddle_typed<T, OP>(sl, nsend, r, sp, stream);
+    }
     return with_k<2, 8>(nsend, [&](auto K) { return launch_multi_vec<T, OP, K.value>(sl, r, sp, stream); });
 }
 
@@ -288,8 +295,15 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
         return chain_phased_typed<T, OP>(sl, ph, nsend, o, d, sp, stream);
     }
     const Split sp = split_for_vectors<T>(ad, count, recv_align());
-    if (any_straddles(sl, nsend, sp.head * sizeof(T)))
+    if (any_straddles(sl, nsend, sp.head * sizeof(T))) {
+        if constexpr (sizeof(T) > 1) {
+            if ((ad & 15) == 0 && caps::strad_via_windows(nsend, count * sizeof(T))) {  // mid-size form (caps.hpp)
+                PhaseList ph{};
+                return chain_unaligned_typed<T, OP>(sl, ph, nsend, o, d, count, stream);
+            }
+        }
         return chain_straddle_typed<T, OP>(sl, nsend, o, d, sp, stream);
+    }
     return with_k<1, 8>(nsend, [&](auto K) { return launch_chain_vec<T, OP, K.value>(sl, o, d, sp, stream); });
 }
 

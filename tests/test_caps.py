@@ -67,6 +67,16 @@ int main() {
         for (int k = 1; k <= 8; ++k)
             std::printf("%s[%d, %d, %d, %d]", (ch || k > 1) ? ", " : "", ch, k,
                         int(phased_via_windows(ch, k, kWindowTunedBytes - 1)), int(phased_via_windows(ch, k, kWindowTunedBytes)));
+    std::printf("], \"strad\": [");
+    const size_t mibs[] = {48, 56, 64, 72, 80, 88, 96};
+    first = true;
+    for (int k = -1; k <= 9; ++k)
+        for (size_t m : mibs)
+            for (int d = -1; d <= 0; ++d) {
+                const size_t b = m * MiB + size_t(d);
+                std::printf("%s[%d, %zu, %d]", first ? "" : ", ", k, b, int(strad_via_windows(k, b)));
+                first = false;
+            }
     std::printf("]}\n");
 }
 """
@@ -188,3 +198,15 @@ def test_window_mid_sizes(table):
             assert via_dst16 == want and via_not16 == want, (ch, k, b)
         else:
             assert via_dst16 == mid and via_not16 == 0, (ch, k, b)
+
+
+def test_straddle_mid_bands(table):
+    """Straddling k-way / chain sources take the mid-size window form in a per-k band (caps.hpp kStradMid):
+    k = 5 from 72 to 96 MiB, k = 6 56-96, k = 7 56-80, k = 8 56-72 per operand; never at k <= 4 or outside."""
+    bands = {5: (72, 96), 6: (56, 96), 7: (56, 80), 8: (56, 72)}
+    seen = 0
+    for k, b, on in table["strad"]:
+        lo, hi = bands.get(k, (0, 0))
+        assert on == int((lo << 20) <= b < (hi << 20)), (k, b)
+        seen += on
+    assert seen == sum(2 * (hi - lo) // 8 for lo, hi in bands.values())

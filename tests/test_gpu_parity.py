@@ -379,16 +379,17 @@ def _torch_op(op):
     return {0: torch.add, 1: torch.mul, 2: torch.maximum, 3: torch.minimum}[op]
 
 
-@pytest.mark.parametrize("mib", [64, 96])
+@pytest.mark.parametrize("mib", [64, 72, 96])
 @pytest.mark.parametrize("k", [3, 4, 5, 6, 7, 8])
 def test_windows_tuned_forms_full_size(dccl, k, mib):
     """From caps::kWindowTunedBytes (96 MiB per operand) reduce_windows_kernel takes its tuned forms (caps.hpp
     kWindow: block order under a 26-wave cap with sources in phase; with sources off phase group order, loads-
     first at k = 4, 5 under 14 / 12 waves, loads-first in runs of 4 tiles at k = 6..8) and takes over the phased
     launches at k-way k = 3..5 and chain k = 4..7; at 64 MiB (caps.hpp window_mid) k-way k = 4..8 and chain
-    k = 3..8 with sources off phase take the mid-size forms, phased launches into a 16-B aligned destination too.
-    Destination not
-    element-aligned, and element-aligned at 16-B phases 0 and 4; sources at phase 0 and 4; k-way and chain in
+    k = 3..8 with sources off phase take the mid-size forms, phased launches into a 16-B aligned destination too,
+    and so do straddling sources (16-B in phase, off the destination's lines) in caps.hpp kStradMid's bands
+    (k = 6..8 at 64 MiB, k = 5..7 at 72 MiB).  Destination not
+    element-aligned, and element-aligned at 16-B phases 0 and 4; sources at phase 0, 4 and 16; k-way and chain in
     place; fp32 Sum, int32 Max, bf16 Sum, int64 Min, against torch applied on the device in the kernels' order, bit for
     bit; nothing outside the destination written."""
     nb = (mib << 20) + 4096
@@ -410,7 +411,7 @@ def test_windows_tuned_forms_full_size(dccl, k, mib):
             return buf
 
         f = _torch_op(op)
-        for roff, soff in [(mis, 0), (mis, 4), (0, 4), (4, 0)]:
+        for roff, soff in [(mis, 0), (mis, 4), (0, 4), (4, 0), (0, 16)]:
             sends = [operand() for _ in range(k)]
             r = operand()
             sbufs = [placed(x, 64 * (j + 1) + soff) for j, x in enumerate(sends)]
