@@ -7,6 +7,8 @@ of 100 launches, replayed 10 times, median of three windows), as a fraction of 3
 variant is checked bit for bit against the product on one pair first.
 
     python tools/pair_small.py [--variants 0,1,2,3,4,5,6,7] [--mib 4,8,16,32,64,128] [--out f.json]
+
+A variant "V@L" runs variant V with L bytes of unused dynamic LDS per one-wave block (a resident-wave cap).
 """
 import argparse
 import ctypes
@@ -36,7 +38,7 @@ def main():
     lib.ps_combine.restype = ctypes.c_int
     lib.ps_combine.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                ctypes.c_void_p]
-    variants = [int(v) for v in a.variants.split(",")]
+    variants = a.variants.split(",")
     dev = torch.device("cuda", 0)
     rows = []
     for mib in (int(x) for x in a.mib.split(",")):
@@ -51,14 +53,15 @@ def main():
         pairs = [(b.data_ptr() + nb + 4096, b.data_ptr()) for b in bufs]  # (send, recv)
 
         def call(v, ps, pr, sh):
-            if v < 0:
+            if v == "-1":
                 return dccl_amd.local_reduce(ps, pr, 7, n, 0, sh)
-            return lib.ps_combine(v, 0, ps, pr, n, sh)
+            var, _, lds = v.partition("@")
+            return lib.ps_combine(int(var), int(lds or 0), ps, pr, n, sh)
 
         # bit-exactness on pair 0 (recv restored between runs)
         saved = bufs[0][:nb].clone()
         outs = []
-        for v in [-1] + variants:
+        for v in ["-1"] + variants:
             bufs[0][:nb].copy_(saved)
             torch.cuda.synchronize()
             assert call(v, *pairs[0], st.cuda_stream) == 0, v
@@ -69,9 +72,9 @@ def main():
         del outs, saved
         launches = max(20, min(400, int(200 * 64 / mib)))
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        eager = {v: [] for v in [-1] + variants}
+        eager = {v: [] for v in ["-1"] + variants}
         for _ in range(a.rounds):
-            for v in [-1] + variants:
+            for v in ["-1"] + variants:
                 for i in range(3):
                     call(v, *pairs[i % sets], st.cuda_stream)
                 ev0.record(st)
@@ -81,7 +84,7 @@ def main():
                 ev1.synchronize()
                 eager[v].append(ev0.elapsed_time(ev1) * 1e3 / launches)
         graph = {}
-        for v in [-1] + variants:
+        for v in ["-1"] + variants:
             side = torch.cuda.Stream(dev)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.stream(side):
