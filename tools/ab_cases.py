@@ -3,7 +3,7 @@
 both libraries loaded side by side (RTLD_LOCAL), every case timed interleaved on the same operands (ten 1 GiB
 fp32 operands from one allocation, 4 KiB x (j+1) stagger), HIP events around --launches back-to-back
 launches per round, the median over --rounds rounds reported per library; each case's result is also
-compared bit for bit between the two libraries on a 1 Mi-element slice (at the destination's offset).
+compared bit for bit between the two libraries at the timed count (so at the size whose dispatch is timed).
 
     python tools/ab_cases.py LIB_A LIB_B [--cases pair_dst+1,multi4_dst+2] [--rounds 5] [--out f.json]
 """
@@ -101,9 +101,9 @@ def main():
         off += nbytes + 4096 * (j + 1)
     table = case_table(ptrs)
     names = a.cases.split(",")
-    # bit-exactness of B against A on a 1 Mi-element slice (the destination restored between the two runs)
+    # bit-exactness of B against A at the timed count (the destination restored between the two runs)
     exact = {}
-    m = 1 << 20
+    m = n
     for name in names:
         k, call = table[name]
         dst = ptrs[0]
