@@ -29,7 +29,7 @@ c5 (BASELINE config C5 on every run: --c5-gib GiB per operand sharded over the N
 combine time and, N>1, the RCCL all-gather of the reduced shards),
 dccl_allreduce (N>1: the namespace-dccl ncclAllReduce over RCCL (the ring step loop, and the grouped form:
 one RCCL group per phase and one chain combine) and over the direct IPC peer-read transport (inputs through
-the scratch, and registered), checked against each other and RCCL's own all_reduce, timed beside it, plus
+the communicator's scratch), checked against each other and RCCL's own all_reduce, timed beside it, plus
 the namespace-dccl all_gather of each transport against RCCL's all_gather (`dccl_allgather`), and the
 direct all_gather at C5's size beside RCCL's (`c5_allgather`);
 in a child process per rank, so a fault or hang there cannot take the bench line with it).
@@ -242,9 +242,11 @@ def cpu_baseline(budget_s: float, nbytes: int) -> dict | None:
     of internal_common.hpp:496-586 with its head/pack/tail split) compiled with the reference's Release
     flags (-O3 -mprefer-vector-width=512, CMakeLists.txt:25), on the headline's own operands: the same
     counter-based fp32 values, 1 GiB per operand, in host memory.  Timed (i) on 1 core, as the reference
-    runs its combine (one thread per rank), (ii) on EVERY core this process may use (its affinity mask),
-    and (iii) on 16 threads (the GPU box's per-GPU CPU share), the buffer split into 64-B aligned
-    contiguous slices, one persistent thread each (ctypes drops the GIL).  The cgroup quota is stated."""
+    runs its combine (one thread per rank), (ii) on all the cores this process is granted (`all_cores`: the
+    cgroup CPU quota, 16 on the GPU box, or the affinity mask when there is no quota), and (iii) when the
+    affinity mask is wider than the quota, on one thread per CPU of the mask (`affinity_threads`, throttled by
+    the quota), the buffer split into 64-B aligned contiguous slices, one persistent thread each (ctypes drops
+    the GIL)."""
     try:
         import oracle  # test infrastructure: the CPU baseline leg only
     except Exception:
@@ -253,6 +255,8 @@ def cpu_baseline(budget_s: float, nbytes: int) -> dict | None:
     fn = lambda s, r, n: lib.oracle_host_reduce(s, r, n, 7, 0)  # noqa: E731
     n = nbytes // 4
     affinity = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    granted = max(1, min(affinity, int(quota))) if quota else affinity
 
     def slices(nthr):
         per = (n // nthr) // 16 * 16
@@ -294,8 +298,8 @@ def cpu_baseline(budget_s: float, nbytes: int) -> dict | None:
                 "payload_gib_s": round(nbytes / tmt / GIB, 2), "ms_per_pass": round(tmt * 1e3, 2),
                 "slices": "64-B aligned contiguous, one thread each"}
 
-    every = threaded(affinity, budget_s * 0.2)
-    sixteen = threaded(min(16, affinity), budget_s * 0.15)
+    every = threaded(granted, budget_s * 0.2)
+    wide = threaded(affinity, budget_s * 0.15) if affinity > granted else None
     del s, r
     variant = benchflags_variant(budget_s * 0.3, n)
     cpu_model = ""
@@ -306,7 +310,6 @@ def cpu_baseline(budget_s: float, nbytes: int) -> dict | None:
                 break
     except OSError:
         pass
-    quota = cgroup_cpu_quota()
     return {
         "value": round(3 * nbytes / t1 / GIB, 2), "unit": "GiB/s (HBM-traffic basis 3*N*4 B, fp32 Sum)",
         "cores": 1, "kind": "port",
@@ -315,11 +318,12 @@ def cpu_baseline(budget_s: float, nbytes: int) -> dict | None:
                   f"internal_common.hpp:496-586) with the Release flags -O3 -mprefer-vector-width=512",
         "payload_gib_s": round(nbytes / t1 / GIB, 2),
         "ms_per_pass": round(t1 * 1e3, 2),
-        "all_cores": every, "threads_16": sixteen,
+        "all_cores": every, "affinity_threads": wide,
         "affinity_cpus": affinity, "machine_cpus": os.cpu_count(), "cgroup_cpu_quota": quota,
-        "cores_note": (f"all_cores = every CPU in this process's affinity mask ({affinity}); "
-                       + (f"the cgroup quota grants {quota} CPUs of time, so threads beyond that are throttled"
-                          if quota else "no cgroup CPU quota")),
+        "cores_note": (f"all_cores = the {granted} CPUs this process is granted "
+                       + (f"(cgroup quota {quota} CPUs of time); affinity_threads = one thread per CPU of the "
+                          f"{affinity}-CPU affinity mask, throttled by that quota" if quota and affinity > granted
+                          else "(its affinity mask; no narrower cgroup quota)")),
         "benchmark_flags_variant": variant,
         "cpu_model": cpu_model,
     }
@@ -638,31 +642,6 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
             torch.cuda.synchronize(dev)
             t = (time.perf_counter() - t0) / iters
             res.update({"ms": round(t * 1e3, 3), "busbw_gb_s": round(2 * (world - 1) / world * count * 4 / t / 1e9, 1)})
-            if name == "direct":
-                # the same all_reduce with the buffer registered (dcclRegisterCacheMemory) and
-                # DCCL_IPC_ZERO_COPY=1: peers read it in place instead of through the scratch copy
-                os.environ["DCCL_IPC_ZERO_COPY"] = "1"
-                dccl_amd.check(comm.register(yf.data_ptr(), count * 4), "register")
-                yr, zr = xf.clone(), xf.clone()
-                dccl_amd.check(comm.register(yr.data_ptr(), count * 4), "register")
-                torch.cuda.synchronize(dev)
-                dccl_amd.check(comm.all_reduce(yr.data_ptr(), yr.data_ptr(), count, 7, 0, st.cuda_stream), name)
-                dccl_amd.check(comm.all_reduce(zr.data_ptr(), zr.data_ptr(), count, 7, 0, st.cuda_stream), name)
-                torch.cuda.synchronize(dev)
-                res["registered_fp32_bit_exact_vs_scratch"] = bool(torch.equal(
-                    zr.view(torch.int32), yr.view(torch.int32)))
-                dist.barrier()
-                t0 = time.perf_counter()
-                for _ in range(iters):
-                    dccl_amd.check(comm.all_reduce(yf.data_ptr(), yf.data_ptr(), count, 7, 0, st.cuda_stream), name)
-                torch.cuda.synchronize(dev)
-                t = (time.perf_counter() - t0) / iters
-                res["registered_ms"] = round(t * 1e3, 3)
-                res["registered_busbw_gb_s"] = round(2 * (world - 1) / world * count * 4 / t / 1e9, 1)
-                for buf in (yf, yr):
-                    dccl_amd.check(comm.deregister(buf.data_ptr()), "deregister")
-                os.environ.pop("DCCL_IPC_ZERO_COPY", None)
-                del yr, zr
             if name != "grouped":  # broadcast / reduce do not depend on the all-reduce algorithm
                 res.update(root_ops(comm, world, rank, dev, st, xi, ri, iters))
             out[name] = res
@@ -1034,8 +1013,7 @@ def allreduce_summary(ar) -> dict:
     for name in ("ring", "grouped", "direct"):
         if isinstance(ar.get(name), dict):
             out[name] = {k: ar[name][k] for k in ("int32_sum_bit_exact_vs_rccl", "fp32_within_bound", "ms",
-                                                  "busbw_gb_s", "registered_ms", "registered_busbw_gb_s",
-                                                  "registered_fp32_bit_exact_vs_scratch", "broadcast_bit_exact",
+                                                  "busbw_gb_s", "broadcast_bit_exact",
                                                   "broadcast_ms", "reduce_bit_exact", "reduce_ms") if k in ar[name]}
     if isinstance(ar.get("rccl_allreduce"), dict):
         out["rccl"] = {k: ar["rccl_allreduce"][k] for k in ("ms", "busbw_gb_s")}
@@ -1048,7 +1026,7 @@ def allreduce_summary(ar) -> dict:
     if isinstance(ar.get("ipc_stats"), dict):
         out["ipc_stats"] = {k: ar["ipc_stats"][k] for k in (
             "alias_errors", "alias_evictions", "mappings_retired", "retire_log_overflows", "open_retries",
-            "size_mismatches", "scratch_copies", "registered_hits", "registered_fallbacks", "verify_failures",
+            "size_mismatches", "scratch_copies", "verify_failures",
             "exports_made") if k in ar["ipc_stats"]}
     return out
 

@@ -273,7 +273,8 @@ Algorithm allreduce_algorithm() {
 }
 
 // The grouped forms of algorithms.hpp on the RCCL transport's device buffers, when DCCL_ALLREDUCE_ALGORITHM
-// is "grouped" or "direct".  Results are the ring's bit for bit.  Not the default yet: on the one-GPU
+// is "grouped" ("direct" keeps its meaning: the peer-read collectives of in-process and IPC groups; on RCCL it
+// runs the ring).  Results are the ring's bit for bit.  Not the default yet: on the one-GPU
 // rehearsal (4 RCCL ranks over loopback sockets) a 64 MiB all-reduce took 28 ms grouped against 16 ms for the
 // ring, while its combine time per collective fell from 45 to 22 us; the xGMI mesh, where
 // the grouped form's W - 1 concurrent transfers use W - 1 links, is measured by the driver's 8-GPU bench.
@@ -281,8 +282,7 @@ bool grouped_selected(const dcclComm* c, bool device) {
     if (!device || c->rccl == nullptr || c->world < 2) return false;
     const char* a = std::getenv(DCCL_ALLREDUCE_ALGORITHM_CONFSTR);
     if (a == nullptr) return false;
-    const std::string s(a);
-    return s == "grouped" || s == "direct";
+    return std::string(a) == "grouped";
 }
 
 uint32_t floor_log2_u32(uint32_t n) {

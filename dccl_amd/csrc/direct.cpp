@@ -78,28 +78,28 @@ struct ShmCtl {
     ShmSlot slot[kMaxRanks];
 };
 
-// An allocation of this process that peers may map: a registered user allocation or a scratch buffer.
-// `serial` numbers this process's exports and is never reused, whatever the runtime's handle bytes do.
+// An allocation of this process that peers may map: a communicator's scratch buffer (peers never read user
+// memory).  `serial` numbers this process's exports and is never reused, whatever the runtime's handle bytes do.
 struct Export {
     size_t size;
     uint64_t buffer_id;
     uint64_t serial;
     ipc::Handle handle;
-    uint32_t regs;  // registered ranges on it (0 for a scratch buffer)
-    bool fresh;     // its handle bytes never named another allocation of this process (see make_export)
+    bool fresh;  // its handle bytes never named another allocation of this process (see make_export)
 };
 
-// A range registered with dcclRegisterCacheMemory, and the allocation (export) holding it.
+// A device range registered with dcclRegisterCacheMemory: tracked only (round 5: peers read every input through
+// the verified scratch, so a registration exports nothing).
 struct Range {
     size_t len;
-    uintptr_t base;
     uint32_t refs;  // registrations of this start address (e.g. one per communicator)
 };
 
 struct IpcXport {
     ShmCtl* ctl = nullptr;
     uint32_t rank = 0, world = 0;
-    double timeout_s = 60.0;
+    double timeout_s = 0;  // 0: no limit (a dead peer is caught by the liveness check)
+    bool liveness = true;   // peers' pids are visible here (checked at join)
     // scratch: inputs that are not registered are copied here (one allocation, exported once)
     void* scratch = nullptr;        // allocation base: header (token), then scratch_bytes of data
     size_t scratch_bytes = 0;
@@ -148,15 +148,15 @@ struct ProcCache {
     std::mutex mu;
     uint64_t next_serial = 1;
     std::map<uintptr_t, Export> exports;  // allocation base -> export
-    std::map<uintptr_t, Range> ranges;    // registered range start -> range
+    std::map<uintptr_t, Range> ranges;    // registered device range start -> range (tracked only)
     HipOps ops;
     ipc::ImportCache imports{&ops, kMaxOpenMappings, kMaxOpenBytes};
     std::vector<IpcXport*> xports;  // live IPC communicators of this process
     // handle bytes of every export this process made -> the buffer id of the allocation they named
     std::map<std::string, uint64_t> handle_owner;
     // exporter-side counters (dccl_ipc_stats)
-    uint64_t exports_made = 0, retirements = 0, registered_hits = 0, scratch_copies = 0, scratch_bytes = 0,
-             scratch_grows = 0, stale_registrations = 0, recycled_handles = 0, registered_fallbacks = 0;
+    uint64_t exports_made = 0, retirements = 0, scratch_copies = 0, scratch_bytes = 0, scratch_grows = 0,
+             recycled_handles = 0;
 };
 
 ProcCache& cache() {
@@ -178,14 +178,18 @@ bool ipc_debug() {
     return on;
 }
 
-// False once peer p's process is gone (or its pid names another process now).
-// DCCL_IPC_LIVENESS=0 turns the check off (ranks in different pid namespaces cannot see each other's pids).
-bool peer_alive(const ShmSlot& s) {
-    static const bool check = [] {
+// DCCL_IPC_LIVENESS=0 turns the liveness check off for every communicator of the process.
+bool liveness_requested() {
+    static const bool on = [] {
         const char* v = std::getenv("DCCL_IPC_LIVENESS");
         return v == nullptr || *v != '0';
     }();
-    if (!check || s.pid <= 0) return true;  // not joined yet
+    return on;
+}
+
+// False once peer p's process is gone (or its pid names another process now).
+bool peer_alive(const ShmSlot& s) {
+    if (s.pid <= 0) return true;  // not joined yet
     if (::kill(static_cast<pid_t>(s.pid), 0) != 0 && errno == ESRCH) return false;
     return proc_start_time(static_cast<long>(s.pid)) == s.start;  // 0 for a zombie (exited, not reaped)
 }
@@ -216,7 +220,8 @@ void apply_retirements(ProcCache& pc) {
 // completes with the flag up.  The flag is sticky (the transport is unusable after a failed collective,
 // like an aborted NCCL communicator).  A waiter checks every ~100 ms that its peers' processes still
 // exist, so a peer that died (a runtime abort, a kill) ends every other rank's wait with ncclRemoteError
-// at once; a live peer that never arrives ends it after timeout_s (DCCL_IPC_TIMEOUT_S, default 60 s).
+// at once.  A live peer may take as long as it likes between collectives (a checkpoint, an evaluation): the
+// wait has no limit unless DCCL_IPC_TIMEOUT_S sets one, or the liveness check is off (then 300 s).
 ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
     ShmCtl* s = x->ctl;
     if (!ok) s->abort.store(1, std::memory_order_relaxed);
@@ -232,7 +237,8 @@ ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
     constexpr auto kSpin = std::chrono::milliseconds(2);
     constexpr auto kLiveness = std::chrono::milliseconds(100);
     const auto start = std::chrono::steady_clock::now();
-    const auto deadline = start + std::chrono::duration<double>(x->timeout_s);
+    const bool limited = x->timeout_s > 0;
+    const auto deadline = start + std::chrono::duration<double>(limited ? x->timeout_s : 0.0);
     auto next_check = start + kLiveness;
     for (uint64_t i = 0; s->gen.load(std::memory_order_acquire) == g; ++i) {
         if (s->abort.load(std::memory_order_relaxed)) return dccl::ncclRemoteError;
@@ -241,11 +247,11 @@ ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
             continue;
         }
         const auto now = std::chrono::steady_clock::now();
-        if (now > deadline) {
+        if (limited && now > deadline) {
             s->abort.store(1, std::memory_order_relaxed);
             return dccl::ncclSystemError;
         }
-        if (now > next_check) {
+        if (x->liveness && now > next_check) {
             next_check = now + kLiveness;
             for (uint32_t p = 0; p < s->world; ++p)
                 if (p != x->rank && !peer_alive(s->slot[p])) {
@@ -276,14 +282,12 @@ void write_retirement(ProcCache& pc, uint64_t serial) {
 
 void drop_export(ProcCache& pc, std::map<uintptr_t, Export>::iterator it) {
     write_retirement(pc, it->second.serial);
-    for (auto r = pc.ranges.begin(); r != pc.ranges.end();)
-        r = r->second.base == it->first ? pc.ranges.erase(r) : std::next(r);
     pc.exports.erase(it);
 }
 
 // Export the allocation [base, base + size) with buffer id `id`; exports whose range it overlaps name
 // freed allocations and are retired.
-ncclResult_t make_export(ProcCache& pc, uintptr_t base, size_t size, uint64_t id, uint32_t regs) {
+ncclResult_t make_export(ProcCache& pc, uintptr_t base, size_t size, uint64_t id) {
     for (auto o = pc.exports.lower_bound(base); o != pc.exports.begin();) {
         --o;
         if (o->first + o->second.size <= base) break;
@@ -293,7 +297,7 @@ ncclResult_t make_export(ProcCache& pc, uintptr_t base, size_t size, uint64_t id
     for (auto o = pc.exports.lower_bound(base); o != pc.exports.end() && o->first < base + size;
          o = pc.exports.lower_bound(base))
         drop_export(pc, o);
-    Export e{size, id, pc.next_serial++, {}, regs, true};
+    Export e{size, id, pc.next_serial++, {}, true};
     hipIpcMemHandle_t h;
     // exporting an allocation at the address of a freed one that a peer still maps can fail for a moment
     for (int attempt = 0, us = 100;; ++attempt, us = std::min(2 * us, 100000)) {
@@ -307,7 +311,7 @@ ncclResult_t make_export(ProcCache& pc, uintptr_t base, size_t size, uint64_t id
     // that mapped them once and opens them again can be handed the earlier import's pages by the runtime,
     // even after it closed that mapping (registered-buffer churn read stale data in 6 of 6
     // runs at W = 2 although every mapping was closed before the new open).  Such an export stays unused
-    // (`fresh` false): a registered buffer then goes through the scratch, a scratch is allocated again.
+    // (`fresh` false): the scratch is allocated again.
     // Without a buffer id, or past a bound on the table, nothing counts as fresh.
     const std::string key(reinterpret_cast<const char*>(e.handle.b), kHandleBytes);
     auto owner = pc.handle_owner.find(key);
@@ -330,41 +334,13 @@ ncclResult_t make_export(ProcCache& pc, uintptr_t base, size_t size, uint64_t id
     return dccl::ncclSuccess;
 }
 
-// The registered export holding [p, p + bytes), or exports.end().  A registration whose allocation was
-// freed (its base now holds another buffer id) is dropped (retired) rather than trusted.
-std::map<uintptr_t, Export>::iterator find_registered(ProcCache& pc, const void* p, size_t bytes) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    auto r = pc.ranges.upper_bound(a);
-    if (r == pc.ranges.begin()) return pc.exports.end();
-    --r;
-    if (a + bytes > r->first + r->second.len) return pc.exports.end();
-    auto e = pc.exports.find(r->second.base);
-    if (e == pc.exports.end()) return e;
-    if (buffer_id_of(reinterpret_cast<void*>(e->first)) != e->second.buffer_id) {
-        ++pc.stale_registrations;
-        drop_export(pc, e);
-        return pc.exports.end();
-    }
-    ++pc.registered_hits;
-    return e;
-}
-
 void describe(const Export& e, uintptr_t base, const void* p, const uint64_t* token, Desc* d) {
     std::memcpy(d->handle, e.handle.b, kHandleBytes);
     d->serial = e.serial;
     d->off = reinterpret_cast<uintptr_t>(p) - base;
     d->size = e.size;
-    d->token[0] = token ? token[0] : 0;
-    d->token[1] = token ? token[1] : 0;
-}
-
-// DCCL_IPC_ZERO_COPY=1 (read per call): peers read registered buffers in place.  Off by default: a peer's
-// first read through a NEW export of a user allocation returned another allocation's data in about one of
-// 1,000 first uses under registration churn on ROCm 7.2, and a user allocation cannot carry
-// the token that lets a scratch mapping be verified.  Registered buffers then go through the scratch too.
-bool zero_copy_enabled() {
-    const char* v = std::getenv("DCCL_IPC_ZERO_COPY");
-    return v != nullptr && *v == '1';
+    d->token[0] = token[0];
+    d->token[1] = token[1];
 }
 
 // Make the communicator's scratch hold at least `bytes`.  A replaced buffer is retired now and freed at
@@ -394,7 +370,7 @@ ncclResult_t ensure_ipc_scratch(ProcCache& pc, IpcXport* x, size_t bytes) {
             rc = dccl::ncclUnhandledCudaError;
             break;
         }
-        rc = make_export(pc, reinterpret_cast<uintptr_t>(base), size, buffer_id_of(base), 0);
+        rc = make_export(pc, reinterpret_cast<uintptr_t>(base), size, buffer_id_of(base));
         if (rc != dccl::ncclSuccess) {
             recycled.push_back(p);
             p = nullptr;
@@ -518,41 +494,30 @@ ncclResult_t arrive(dcclComm* c, hipStream_t st, ncclResult_t rc = dccl::ncclSuc
 }
 
 // What one rank publishes for a collective: `in` (peers read it; nullptr: nothing) of in_bytes, and
-// `out` (peers read the reduced chunks from it; nullptr: nothing) of out_bytes.  On the IPC transport a
-// buffer that is not registered is replaced by the communicator's scratch: `in` is copied there on `st`
-// (copy_in), and `out` becomes the scratch itself (the caller copies the result out).
+// `out` (peers read the reduced chunks from it; nullptr: nothing) of out_bytes.  On the IPC transport both
+// are replaced by the communicator's scratch: `in` is copied there on `st`, and `out` becomes the scratch
+// itself (the caller copies the result out).
 struct Publish {
     const void* in = nullptr;
     size_t in_bytes = 0;
     void* out = nullptr;
     size_t out_bytes = 0;
-    bool in_scratch = false, out_scratch = false;
+    bool out_scratch = false;
 };
 
-// Decide and describe what this rank publishes (IPC): registered buffers as they are, the rest through
-// the scratch.  Fills this rank's slot.
+// Copy `in` into the scratch and describe it (and `out`, the scratch itself) in this rank's slot (IPC).  Peers
+// only ever read the library-owned scratch, whose every new mapping they verify by its token: the round-4
+// opt-in that let them read registered user buffers in place returned another allocation's data in about one
+// of 1,000 first uses under registration churn, with no way to verify a user allocation, and is gone.
 ncclResult_t plan_ipc(dcclComm* c, Publish* pub, hipStream_t st) {
     IpcXport* x = xport(c);
     ProcCache& pc = cache();
     std::lock_guard<std::mutex> lock(pc.mu);
     for (void* p : x->old_scratch) (void)hipFree(p);  // every peer closed them in the previous collective
     x->old_scratch.clear();
-    const bool zc = zero_copy_enabled();
-    auto in_e = zc && pub->in ? find_registered(pc, pub->in, pub->in_bytes) : pc.exports.end();
-    auto out_e = zc && pub->out ? find_registered(pc, pub->out, pub->out_bytes) : pc.exports.end();
-    // a registration whose handle bytes are recycled is never published: through the scratch instead
-    if (in_e != pc.exports.end() && !in_e->second.fresh) {
-        ++pc.registered_fallbacks;
-        in_e = pc.exports.end();
-    }
-    if (out_e != pc.exports.end() && !out_e->second.fresh) {
-        ++pc.registered_fallbacks;
-        out_e = pc.exports.end();
-    }
-    pub->in_scratch = pub->in != nullptr && in_e == pc.exports.end();
-    pub->out_scratch = pub->out != nullptr && out_e == pc.exports.end();
+    pub->out_scratch = pub->out != nullptr;
     // `out` in the scratch shares it with `in` (the all_reduce combines in place there)
-    const size_t need = std::max(pub->in_scratch ? pub->in_bytes : 0, pub->out_scratch ? pub->out_bytes : 0);
+    const size_t need = std::max(pub->in ? pub->in_bytes : 0, pub->out ? pub->out_bytes : 0);
     if (need > 0) {
         const ncclResult_t rc = ensure_ipc_scratch(pc, x, need);
         if (rc != dccl::ncclSuccess) return rc;
@@ -561,7 +526,7 @@ ncclResult_t plan_ipc(dcclComm* c, Publish* pub, hipStream_t st) {
     s.in.serial = s.out.serial = 0;
     const uintptr_t sb = reinterpret_cast<uintptr_t>(x->scratch);
     unsigned char* data = static_cast<unsigned char*>(x->scratch) + kScratchHeader;
-    if (pub->in_scratch) {
+    if (pub->in) {
         if (hipMemcpyAsync(data, pub->in, pub->in_bytes, hipMemcpyDeviceToDevice, st) != hipSuccess) {
             (void)hipGetLastError();
             return dccl::ncclUnhandledCudaError;
@@ -570,15 +535,10 @@ ncclResult_t plan_ipc(dcclComm* c, Publish* pub, hipStream_t st) {
         pc.scratch_bytes += pub->in_bytes;
         pub->in = data;
     }
-    if (pub->out_scratch) pub->out = data;
-    if (pub->in) {
-        auto e = pub->in_scratch ? pc.exports.find(sb) : in_e;
-        describe(e->second, e->first, pub->in, pub->in_scratch ? x->token : nullptr, &s.in);
-    }
-    if (pub->out) {
-        auto e = pub->out_scratch ? pc.exports.find(sb) : out_e;
-        describe(e->second, e->first, pub->out, pub->out_scratch ? x->token : nullptr, &s.out);
-    }
+    if (pub->out) pub->out = data;
+    const auto e = pc.exports.find(sb);
+    if (pub->in) describe(e->second, e->first, pub->in, x->token, &s.in);
+    if (pub->out) describe(e->second, e->first, pub->out, x->token, &s.out);
     return dccl::ncclSuccess;
 }
 
@@ -710,10 +670,12 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
     x->rank = rank;
     x->world = world;
     x->seen.assign(world, 0);
+    x->liveness = liveness_requested();
     if (const char* t = std::getenv("DCCL_IPC_TIMEOUT_S")) {
         const double v = std::strtod(t, nullptr);
         if (v > 0) x->timeout_s = v;
     }
+    if (!x->liveness && x->timeout_s <= 0) x->timeout_s = 300;  // no liveness check: a dead peer ends the wait
     ShmSlot& me = ctl->slot[rank];
     me.start = proc_start_time(static_cast<long>(::getpid()));
     me.pid = ::getpid();
@@ -722,6 +684,19 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
     c->rank = rank;
     c->world = world;
     const ncclResult_t rc = shm_barrier(x);  // everyone mapped the segment
+    // Ranks that share /dev/shm but not a pid namespace (containers with --ipc=host), or a /proc mounted with
+    // hidepid, cannot see each other's processes: a live peer would look dead.  Then this communicator goes
+    // without the liveness check (and with the 300 s default limit), said once.
+    if (rc == dccl::ncclSuccess && x->liveness) {
+        for (uint32_t p = 0; p < world; ++p)
+            if (p != rank && !peer_alive(ctl->slot[p])) {
+                x->liveness = false;
+                if (x->timeout_s <= 0) x->timeout_s = 300;
+                std::fprintf(stderr, "[dccl ipc %d] rank %u's process (pid %lld) is not visible from here: liveness "
+                                     "check off for this communicator\n", ::getpid(), p, (long long)ctl->slot[p].pid);
+                break;
+            }
+    }
     {
         // retirements written from here on reach this segment's peers (none can refer to an earlier export:
         // nothing was published here before)
@@ -769,6 +744,9 @@ ncclResult_t ipc_leave(dcclComm* c) {
     return rc;
 }
 
+// dcclRegisterCacheMemory of device memory on an IPC communicator: validated (a device allocation of this
+// process, the range inside it) and counted, nothing exported.  The reference registers RDMA memory for its
+// transport (/root/reference/src/core/dccl.cpp:503-549); peers here read the scratch, which needs none.
 ncclResult_t ipc_register(void* buffer, size_t size) {
     hipDeviceptr_t base = nullptr;
     size_t asize = 0;
@@ -778,53 +756,21 @@ ncclResult_t ipc_register(void* buffer, size_t size) {
     }
     const uintptr_t b = reinterpret_cast<uintptr_t>(base), a = reinterpret_cast<uintptr_t>(buffer);
     if (a + size > b + asize) return dccl::ncclInvalidArgument;  // past its allocation
-    const uint64_t id = buffer_id_of(base);
     ProcCache& pc = cache();
     std::lock_guard<std::mutex> lock(pc.mu);
-    auto e = pc.exports.find(b);
-    if (e != pc.exports.end() && (e->second.size != asize || e->second.buffer_id != id)) {
-        ++pc.stale_registrations;  // a freed allocation's export at this address
-        drop_export(pc, e);
-        e = pc.exports.end();
-    }
-    if (e != pc.exports.end() && e->second.regs == 0) return dccl::ncclInvalidUsage;  // a communicator's scratch
-    auto old = pc.ranges.find(a);
-    if (old != pc.ranges.end() && old->second.base == b && e != pc.exports.end()) {
-        // the same start registered again (another communicator, or the same one): counted, deregistered as often
-        old->second.len = std::max(old->second.len, size);
-        ++old->second.refs;
-        ++e->second.regs;
-        return dccl::ncclSuccess;
-    }
-    if (old != pc.ranges.end()) {  // a range of another allocation at this start: it was freed
-        auto oe = pc.exports.find(old->second.base);
-        const uint32_t refs = old->second.refs;
-        pc.ranges.erase(old);
-        if (oe != pc.exports.end()) {
-            oe->second.regs = oe->second.regs > refs ? oe->second.regs - refs : 0;
-            if (oe->second.regs == 0) drop_export(pc, oe);
-        }
-        e = pc.exports.find(b);
-    }
-    if (e == pc.exports.end()) {
-        const ncclResult_t rc = make_export(pc, b, asize, id, 0);
-        if (rc != dccl::ncclSuccess) return rc;
-        e = pc.exports.find(b);
-    }
-    ++e->second.regs;
-    pc.ranges[a] = Range{size, b, 1};
+    Range& r = pc.ranges[a];
+    r.len = std::max(r.len, size);
+    ++r.refs;
     return dccl::ncclSuccess;
 }
 
-// dcclDeregisterCacheMemory: the export ends now; every peer closes its mapping before it maps anything new.
+// dcclDeregisterCacheMemory: as often as the start was registered; an unknown start is an error.
 ncclResult_t ipc_deregister(void* buffer) {
     ProcCache& pc = cache();
     std::lock_guard<std::mutex> lock(pc.mu);
     auto r = pc.ranges.find(reinterpret_cast<uintptr_t>(buffer));
     if (r == pc.ranges.end()) return dccl::ncclInvalidArgument;
-    auto e = pc.exports.find(r->second.base);
     if (--r->second.refs == 0) pc.ranges.erase(r);
-    if (e != pc.exports.end() && --e->second.regs == 0) drop_export(pc, e);
     return dccl::ncclSuccess;
 }
 
@@ -832,11 +778,13 @@ int ipc_stats(uint64_t* out, int n) {
     ProcCache& pc = cache();
     std::lock_guard<std::mutex> lock(pc.mu);
     const ipc::ImportStats& s = pc.imports.stats;
-    const uint64_t v[] = {pc.exports_made, pc.retirements, pc.registered_hits, pc.scratch_copies, pc.scratch_bytes,
-                          pc.scratch_grows, pc.stale_registrations, s.opened, s.reused, s.retired, s.retired_pid,
+    // slots 2, 6 and 19 (registered-buffer hits, stale registrations, registered fallbacks) counted the
+    // registered in-place path removed in round 5; they stay in the ABI, always 0
+    const uint64_t v[] = {pc.exports_made, pc.retirements, 0, pc.scratch_copies, pc.scratch_bytes,
+                          pc.scratch_grows, 0, s.opened, s.reused, s.retired, s.retired_pid,
                           s.trimmed, s.alias_evicted, s.alias_errors, s.open_retries, s.size_mismatch,
                           uint64_t(pc.imports.size()), uint64_t(pc.imports.bytes()), pc.recycled_handles,
-                          pc.registered_fallbacks, s.verify_failures};
+                          0, s.verify_failures};
     const int m = std::min<int>(n, int(sizeof(v) / sizeof(v[0])));
     for (int i = 0; i < m; ++i) out[i] = v[i];
     return int(sizeof(v) / sizeof(v[0]));

@@ -59,50 +59,6 @@ size_t recv_align() {
     }();
     return v;
 }
-// Occupancy caps of the pairwise launches, as bytes of (unused) dynamic LDS per one-wave block (caps.hpp:
-// caps::pair_lds, with the measurements behind it).  DCCL_REDUCE_LDS_CAP, read once per process, forces a
-// value for the vector and shifted kernels (0 = uncapped).  Unset, the cap follows the operands' allocations:
-// uncapped for one allocation (the bench's pooled pair), capped for two allocations of at least 512 MiB on
-// the current device.  The line-straddling vector launch (StraddleCfg) gains nothing from any cap (+0.0
-// median) and stays uncapped.
-constexpr size_t kUnsetCap = ~size_t(0);
-size_t forced_occupancy_lds() {
-    static const size_t v = [] {
-        const char* e = std::getenv("DCCL_REDUCE_LDS_CAP");
-        if (e == nullptr || *e == '\0') return kUnsetCap;
-        const unsigned long long x = std::strtoull(e, nullptr, 10);
-        return static_cast<size_t>(x > (64ull << 10) ? (64ull << 10) : x);
-    }();
-    return v;
-}
-// True when p is device memory of the current device (not a peer GPU's buffer, an IPC import or host memory).
-bool on_current_device(const void* p) {
-    int dev = -1;
-    hipPointerAttribute_t at{};
-    if (hipGetDevice(&dev) != hipSuccess || hipPointerGetAttributes(&at, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return at.type == hipMemoryTypeDevice && at.device == dev;
-}
-// The pairwise launch's LDS request (the forced value, or caps::pair_lds): whether send and recv lie in two
-// allocations on the current device costs one hipPointerGetAttributes and one hipMemGetAddressRange per
-// operand, only for launches of at least caps::kSeparateCapBytes.  The caps were measured on two local HBM
-// allocations; reads of a peer's buffer over xGMI (the direct collectives' W = 2 step) stay uncapped.
-size_t pair_occupancy_lds(const void* send, const void* recv, size_t bytes, bool shifted) {
-    const size_t forced = forced_occupancy_lds();
-    if (forced != kUnsetCap) return forced;
-    if (bytes < caps::kSeparateCapBytes) return 0;
-    if (!on_current_device(send) || !on_current_device(recv)) return 0;
-    hipDeviceptr_t bs = nullptr, br = nullptr;
-    size_t ls = 0, lr = 0;
-    if (hipMemGetAddressRange(&bs, &ls, const_cast<void*>(send)) != hipSuccess ||
-        hipMemGetAddressRange(&br, &lr, const_cast<void*>(recv)) != hipSuccess) {
-        (void)hipGetLastError();  // not runtime-allocated device memory: no cap, and no stale error left behind
-        return 0;
-    }
-    return caps::pair_lds(shifted, bs != br, bytes);
-}
 template <typename T, int OP>
 int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream) {
     const auto s = static_cast<const unsigned char*>(send);
@@ -119,28 +75,20 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
                         const_cast<size_t*>(&nvec), &count, &order};
         return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<T, OP>), grid, args, stream, 64);
     }
-    const size_t bytes = count * sizeof(T);
     if (as % sizeof(T)) {  // an element-aligned recv and a send at any byte address: the shifted kernel
         const Split sp = split_for_vectors<T>(ar, count, align);
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);
-        const size_t lds = pair_occupancy_lds(send, recv, bytes, true);
-        return (a & 127)
-                   ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, false, kShiftRun>(s, r, count, stream, align, lds)
-                   : launch_shift<T, OP, ShiftPolicy, false, 0, false, kShiftRun>(s, r, count, stream, align, lds);
+        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, false, kShiftRun>(s, r, count, stream, align)
+                         : launch_shift<T, OP, ShiftPolicy, false, 0, false, kShiftRun>(s, r, count, stream, align);
     }
     const Split sp = split_for_vectors<T>(ar, count, align);
     if ((as ^ ar) & 15) {
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);  // the shifted kernel's send vectors
-        const size_t lds = pair_occupancy_lds(send, recv, bytes, true);
-        return (a & 127)
-                   ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, true, kShiftRun>(s, r, count, stream, align, lds)
-                   : launch_shift<T, OP, ShiftPolicy, false, 0, true, kShiftRun>(s, r, count, stream, align, lds);
+        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, true, kShiftRun>(s, r, count, stream, align)
+                         : launch_shift<T, OP, ShiftPolicy, false, 0, true, kShiftRun>(s, r, count, stream, align);
     }
-    if ((as ^ ar) & 127) {
-        const size_t forced = forced_occupancy_lds();
-        return launch_vec<T, OP, StraddleCfg>(s, r, sp, stream, 0, forced == kUnsetCap ? 0 : forced);
-    }
-    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream, 0, pair_occupancy_lds(send, recv, bytes, false));
+    if ((as ^ ar) & 127) return launch_vec<T, OP, StraddleCfg>(s, r, sp, stream);
+    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream);
 }
 
 // k-way combine: every resident wave keeps k+1 16-B loads per lane in flight, so the resident waves
@@ -202,15 +150,7 @@ int reduce_multi_typed(const void* const* sends, int nsend, void* recv, size_t c
         return multi_phased_typed<T, OP>(sl, ph, nsend, r, sp, stream);
     }
     const Split sp = split_for_vectors<T>(ar, count, recv_align());
-    if (any_straddles(sl, nsend, sp.head * sizeof(T))) {
-        if constexpr (sizeof(T) > 1) {
-            if ((ar & 15) == 0 && caps::strad_via_windows(nsend, count * sizeof(T))) {  // mid-size form (caps.hpp)
-                PhaseList ph{};
-                return multi_unaligned_typed<T, OP>(sl, ph, nsend, r, count, stream);
-            }
-        }
-        return multi_straddle_typed<T, OP>(sl, nsend, r, sp, stream);
-    }
+    if (any_straddles(sl, nsend, sp.head * sizeof(T))) return multi_straddle_typed<T, OP>(sl, nsend, r, sp, stream);
     return with_k<2, 8>(nsend, [&](auto K) { return launch_multi_vec<T, OP, K.value>(sl, r, sp, stream); });
 }
 
@@ -264,11 +204,12 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
     if (nsend == 1 && own == dst) return reduce_typed<T, OP>(sends[0], dst, count, stream);
     SendList sl{};
     const uintptr_t ad = reinterpret_cast<uintptr_t>(dst), ao = reinterpret_cast<uintptr_t>(own);
-    bool vec_ok = (ad % sizeof(T)) == 0 && ((ad ^ ao) & 15) == 0;
+    bool src_off = false;  // some source at another 16-B phase than dst
     for (int k = 0; k < nsend; ++k) {
         sl.p[k] = static_cast<const unsigned char*>(sends[k]);
-        if ((reinterpret_cast<uintptr_t>(sends[k]) ^ ad) & 15) vec_ok = false;
+        if ((reinterpret_cast<uintptr_t>(sends[k]) ^ ad) & 15) src_off = true;
     }
+    const bool vec_ok = (ad % sizeof(T)) == 0 && ((ad ^ ao) & 15) == 0 && !src_off;
     const auto o = static_cast<const unsigned char*>(own);
     auto d = static_cast<unsigned char*>(dst);
     if (ad % sizeof(T)) {  // dst not element-aligned: 16-B accesses at its own address, operands at any phase
@@ -281,7 +222,9 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
     }
     if (!vec_ok) {  // an element-aligned dst and operands at other 16-B (or byte) phases: the phased kernel
         if constexpr (sizeof(T) > 1) {
-            if (caps::phased_via_windows(true, nsend, count * sizeof(T), (ad & 15) == 0)) {  // or the windows kernel (caps.hpp)
+            // or the windows kernel (caps.hpp), whose off-phase forms were measured with sources off phase (not
+            // with `own` alone off phase: that launch keeps the phased kernels)
+            if (src_off && caps::phased_via_windows(true, nsend, count * sizeof(T), (ad & 15) == 0)) {
                 PhaseList ph{};
                 for (int k = 0; k < nsend; ++k) ph.p[k] = phase_word(sl.p[k], 0);
                 ph.p[nsend] = phase_word(o, 0);
@@ -295,15 +238,7 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
         return chain_phased_typed<T, OP>(sl, ph, nsend, o, d, sp, stream);
     }
     const Split sp = split_for_vectors<T>(ad, count, recv_align());
-    if (any_straddles(sl, nsend, sp.head * sizeof(T))) {
-        if constexpr (sizeof(T) > 1) {
-            if ((ad & 15) == 0 && caps::strad_via_windows(nsend, count * sizeof(T))) {  // mid-size form (caps.hpp)
-                PhaseList ph{};
-                return chain_unaligned_typed<T, OP>(sl, ph, nsend, o, d, count, stream);
-            }
-        }
-        return chain_straddle_typed<T, OP>(sl, nsend, o, d, sp, stream);
-    }
+    if (any_straddles(sl, nsend, sp.head * sizeof(T))) return chain_straddle_typed<T, OP>(sl, nsend, o, d, sp, stream);
     return with_k<1, 8>(nsend, [&](auto K) { return launch_chain_vec<T, OP, K.value>(sl, o, d, sp, stream); });
 }
 

@@ -760,7 +760,7 @@ inline Split split_for_vectors(uintptr_t recv, size_t count, size_t align = 16) 
 }
 
 template <typename T, int OP, typename C>
-int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t stream, size_t grid_cap,
+int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t stream, size_t grid_cap = 0,
                size_t lds_bytes = 0) {
     size_t grid = ceil_div(sp.nvec, C::TILE);
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;

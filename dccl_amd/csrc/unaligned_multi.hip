@@ -88,11 +88,8 @@ int launch_windows(const SendList& sl, const PhaseList& ph, const unsigned char*
     if (count * sizeof(T) >= caps::kWindowTunedBytes)
         return off ? launch_tuned<T, OP, K, CHAIN, caps::kWinOffPhase>(A, stream)
                    : launch_tuned<T, OP, K, CHAIN, caps::kWinInPhase>(A, stream);
-    // straddling sources routed here (local_reduce.hip): every window at phase 0, the destination 16-B aligned
-    const bool strad = !off && A.p[K] == 0 && (reinterpret_cast<uintptr_t>(d) & 15) == 0 &&
-                       caps::strad_via_windows(K, count * sizeof(T));
-    if ((off || strad) && caps::window_mid(CHAIN, K, count * sizeof(T))) {
-        constexpr caps::WindowForm f = caps::window_mid_form(K);
+    if (off && caps::window_mid(CHAIN, K, count * sizeof(T))) {
+        constexpr caps::WindowForm f = (CHAIN && K == 3) ? caps::kWindowMidChain3 : caps::kWindowMid;
         return launch_form<T, OP, K, CHAIN, f.first != 0, int(f.order)>(A, stream, caps::lds_for_waves(f.waves));
     }
     switch (unaligned_order(ph, K)) {  // smaller launches: the per-operand form, uncapped

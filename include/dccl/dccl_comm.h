@@ -24,29 +24,28 @@
  *                         in-process transport agrees per collective and stays usable after a failure.)
  *                         Inputs are first copied (on the collective's stream) into the communicator's
  *                         scratch, one library-owned allocation exported once, whose token every peer
- *                         checks through its new mapping; with DCCL_IPC_ZERO_COPY=1 peers read device
- *                         memory registered with dccl_comm_register in place instead (unverified).  A peer whose process dies
- *                         ends every other rank's wait with ncclRemoteError within ~0.1 s; a live peer that
- *                         never arrives, after DCCL_IPC_TIMEOUT_S (default 60 s).  Communicators of one
+ *                         checks through its new mapping; peers never read user memory.  A peer whose
+ *                         process dies ends every other rank's wait with ncclRemoteError within ~0.1 s; a
+ *                         live peer may take any time between collectives (no limit unless
+ *                         DCCL_IPC_TIMEOUT_S sets one; 300 s when peers' processes are not visible, e.g.
+ *                         another pid namespace, which turns the liveness check off).  Communicators of one
  *                         process share one mapping cache under one mutex: collectives driven from several
  *                         threads at once serialise while they map peer buffers (a failing open retries
  *                         for up to ~0.5 s under it); a collective releases its mappings once its stream
  *                         has drained, before its last barrier.
  *   dccl_comm_register /  dcclRegisterCacheMemory / dcclDeregisterCacheMemory (/root/reference/src/core/
  *   dccl_comm_deregister  dccl.cpp:503-549): 64-byte aligned address and size.  Host memory is page-locked.
- *                         Device memory on an IPC communicator becomes an export peers map in place until
- *                         it is deregistered, with DCCL_IPC_ZERO_COPY=1 (the registration belongs to the
- *                         process; registering a start address again counts, deregister as often); the
- *                         caller keeps the allocation alive until then.  Other communicators: accepted,
- *                         nothing to do.
+ *                         Device memory: validated (an IPC communicator checks it is a device allocation
+ *                         of this process and the range lies inside it) and tracked, nothing exported
+ *                         (registering a start address again counts; deregister as often).
  *   dccl_ipc_stats        the process's IPC transport counters, in this order: exports made, exports
- *                         retired, registered-buffer hits, scratch copies, scratch bytes copied, scratch
- *                         grows, stale registrations dropped, mappings opened, mappings reused, mappings
- *                         closed on retirement, retirement-log overflows, mappings trimmed, alias
- *                         evictions, alias errors, open retries, size mismatches, mappings open, bytes
- *                         mapped, exports with recycled handle bytes (never published), registered buffers
- *                         sent through the scratch for that reason, new scratch mappings whose token did
- *                         not read back.  Fills min(n, count) values; returns count.
+ *                         retired, (0), scratch copies, scratch bytes copied, scratch grows, (0),
+ *                         mappings opened, mappings reused, mappings closed on retirement, retirement-log
+ *                         overflows, mappings trimmed, alias evictions, alias errors, open retries, size
+ *                         mismatches, mappings open, bytes mapped, exports with recycled handle bytes (never
+ *                         published), (0), new scratch mappings whose token did not read back.  The (0)
+ *                         slots counted the registered in-place path removed in round 5.  Fills min(n,
+ *                         count) values; returns count.
  *   dccl_bootstrap_unique_id  single-node exchange of the RCCL id through DCCL_BOOTSTRAP_DIR: rank 0
  *                         creates and publishes it, the others wait (DCCL_BOOTSTRAP_TIMEOUT_S, default
  *                         120 s) for a file published by a LIVE rank 0 of the same world size, so a

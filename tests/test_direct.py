@@ -375,7 +375,7 @@ def test_ipc_transport_processes(gpu, W, n, dt, op):
     assert all(results[r]["finalize"] == 0 for r in range(W))
 
 
-def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=False, register=False, zc=False):
+def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=False, register=False):
     """All-gathers over fresh allocations: before each round every buffer of the previous round is freed back to
     the driver (torch.cuda.empty_cache), so the next allocation may reuse its address; every round carries new
     data.  `grow`: odd rounds send W times as much, so a round's input lands where the previous round's output
@@ -383,11 +383,9 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=
     communicators of the same ranks, which share the process's peer mappings.  `hold`: nothing is freed, so
     every round's buffers are new allocations and the peer mappings pile up past the cache's bound.
     `register`: every round registers its buffers (dcclRegisterCacheMemory) and deregisters them before the
-    free, so peers read them in place and the exports churn; otherwise inputs go through the scratch."""
+    free (tracked only: inputs go through the scratch either way)."""
     os.environ["DCCL_BOOTSTRAP_TAG"] = tag
     os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")
-    if zc:
-        os.environ["DCCL_IPC_ZERO_COPY"] = "1"
     log_dir = os.environ.get("DCCL_STRESS_LOG_DIR")  # tools/ipc_churn_stress.py --trace: this rank's stderr to a file
     if log_dir:
         fd = os.open(os.path.join(log_dir, f"rank{r}.log"), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
@@ -459,17 +457,15 @@ def _ipc_realloc_rank(r, W, nbytes, rounds, grow, tag, q, two_comms=False, hold=
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,nbytes,rounds,grow,two,hold,reg,zc", [
+@pytest.mark.parametrize("W,nbytes,rounds,grow,two,hold,reg", [
     # VERDICT r3's churn cases: 1 MiB buffers freed and re-allocated every round
-    (2, 1 << 20, 140, False, False, False, False, False), (4, 1 << 20, 100, False, False, False, False, False),
-    (2, 1 << 20, 140, False, False, False, True, False), (4, 1 << 20, 100, False, False, False, True, False),
-    (4, 1 << 20, 40, True, True, False, True, False),
-    (2, 64 << 20, 4, False, False, False, False, False), (4, 256 << 20, 4, False, False, False, False, False),
-    (4, 64 << 20, 4, True, False, False, True, False), (4, 64 << 20, 4, True, True, False, False, False),
-    (2, 64 << 20, 6, False, True, False, True, False), (2, 16 << 20, 140, False, False, True, True, False),
-    # DCCL_IPC_ZERO_COPY=1: registered buffers read in place, kept allocated (each a new export once)
-    (2, 16 << 20, 4, False, False, True, True, True)])
-def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold, reg, zc):
+    (2, 1 << 20, 140, False, False, False, False), (4, 1 << 20, 100, False, False, False, False),
+    (2, 1 << 20, 140, False, False, False, True), (4, 1 << 20, 100, False, False, False, True),
+    (4, 1 << 20, 40, True, True, False, True),
+    (2, 64 << 20, 4, False, False, False, False), (4, 256 << 20, 4, False, False, False, False),
+    (4, 64 << 20, 4, True, False, False, True), (4, 64 << 20, 4, True, True, False, False),
+    (2, 64 << 20, 6, False, True, False, True), (2, 16 << 20, 140, False, False, True, True)])
+def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold, reg):
     """A peer's buffer freed and a new one of the same size allocated must be mapped afresh: a cache of peer
     mappings keyed by the IPC handle alone can hand back the freed buffer's mapping (the handle bytes of a
     dmabuf export can repeat once the old export is closed), and the collective then reads stale data.
@@ -478,14 +474,12 @@ def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold, reg, z
     `two`: two communicators of the same ranks share the process's mappings (a stale mapping one of them still
     held used to shadow the other's re-import).  `reg`: the buffers are registered every round (and registered
     on both communicators with `two`: counted registrations); inputs reach the peers through each
-    communicator's scratch, exported once and verified by its token.  `zc` (DCCL_IPC_ZERO_COPY=1): peers read
-    registered buffers in place; a registration whose handle bytes once named another (freed) allocation of its
-    process is never published (it goes through the scratch).  No mapping may alias another and every new
+    communicator's scratch, exported once and verified by its token.  No mapping may alias another and every new
     scratch mapping must read back its token (alias_errors == verify_failures == 0 in every process)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     tag = "test_" + uuid.uuid4().hex[:12]
-    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q, two, hold, reg, zc))
+    ps = [ctx.Process(target=_ipc_realloc_rank, args=(r, W, nbytes, rounds, grow, tag, q, two, hold, reg))
           for r in range(W)]
     for p in ps:
         p.start()
@@ -504,11 +498,8 @@ def test_ipc_reallocated_buffers(gpu, W, nbytes, rounds, grow, two, hold, reg, z
         bad, fin, stats, _ = results[r]
         assert not bad and fin == 0, (r, bad[:8], len(bad), fin, stats)
         assert stats["alias_errors"] == 0 and stats["verify_failures"] == 0, (r, stats)
-        if zc:  # registered inputs read in place, or through the scratch when their handle bytes are recycled
-            assert stats["registered_hits"] >= rounds, (r, stats)
-            assert stats["scratch_copies"] == stats["registered_fallbacks"], (r, stats)
-        else:  # every input through the verified scratch, registered or not
-            assert stats["scratch_copies"] >= rounds and stats["registered_hits"] == 0, (r, stats)
+        # every input through the verified scratch, registered or not
+        assert stats["scratch_copies"] >= rounds and stats["registered_hits"] == 0, (r, stats)
 
 
 def _ipc_dying_rank(r, tag, q):

@@ -385,10 +385,8 @@ def test_windows_tuned_forms_full_size(dccl, k, mib):
     """From caps::kWindowTunedBytes (96 MiB per operand) reduce_windows_kernel takes its tuned forms (caps.hpp
     kWindow: block order under a 26-wave cap with sources in phase; with sources off phase group order, loads-
     first at k = 4, 5 under 14 / 12 waves, loads-first in runs of 4 tiles at k = 6..8) and takes over the phased
-    launches at k-way k = 3..5 and chain k = 4..7; at 64 MiB (caps.hpp window_mid) k-way k = 4..8 and chain
-    k = 3..8 with sources off phase take the mid-size forms, phased launches into a 16-B aligned destination too,
-    and so do straddling sources (16-B in phase, off the destination's lines) in caps.hpp kStradMid's bands
-    (k = 6..8 at 64 MiB, k = 5..7 at 72 MiB).  Destination not
+    launches at k-way k = 3..5 and chain k = 4..7; below it (64, 72 MiB) the uncapped per-operand form and the
+    phased kernels run.  Destination not
     element-aligned, and element-aligned at 16-B phases 0 and 4; sources at phase 0, 4 and 16; k-way and chain in
     place; fp32 Sum, int32 Max, bf16 Sum, int64 Min, against torch applied on the device in the kernels' order, bit for
     bit; nothing outside the destination written."""
@@ -756,40 +754,6 @@ def test_separate_allocations_capped_launch_eager_and_graph(dccl):
                              torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
     assert bool(torch.all(pool[:n] == 8)) and bool(torch.all(pool[n:n + 1024] == 5))
-
-
-_FORCED_CAP_CHILD = r"""
-import sys, torch
-sys.path.insert(0, sys.argv[1])
-import dccl_amd
-n = (512 << 20) // 4 + 5
-st = torch.cuda.current_stream().cuda_stream
-s = torch.full((n + 4,), 3, dtype=torch.int32, device="cuda")
-r = torch.full((n,), 5, dtype=torch.int32, device="cuda")
-assert dccl_amd.local_reduce(s.data_ptr(), r.data_ptr(), 2, n, 0, st) == 0        # aligned
-assert dccl_amd.local_reduce(s.data_ptr() + 4, r.data_ptr(), 2, n, 0, st) == 0    # shifted
-assert dccl_amd.local_reduce(s.data_ptr() + 16, r.data_ptr(), 2, n - 4, 0, st) == 0  # line-straddling send
-torch.cuda.synchronize()
-assert bool(torch.all(r[:n - 4] == 14)) and bool(torch.all(r[n - 4:] == 11))
-print("ok")
-"""
-
-
-@pytest.mark.parametrize("cap", ["", "0", "7168", "20480"])
-def test_forced_occupancy_cap(dccl, cap):
-    """DCCL_REDUCE_LDS_CAP (read once per process, hence a child process per value) forces the occupancy cap of
-    the aligned, shifted and line-straddling pairwise launches: unset (the allocation rule), 0 (uncapped), 22 and
-    8 waves per CU.  512 MiB operands in two allocations, so the unset case takes the allocation lookup; every
-    result exact."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = {k: v for k, v in os.environ.items() if k != "DCCL_REDUCE_LDS_CAP"}
-    if cap:
-        env["DCCL_REDUCE_LDS_CAP"] = cap
-    p = subprocess.run([sys.executable, "-c", _FORCED_CAP_CHILD, root], env=env, capture_output=True, text=True,
-                       timeout=120)
-    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stderr[-2000:]
 
 
 def test_graph_capture_every_kernel_family(dccl):

@@ -65,6 +65,7 @@ def case_table(ptrs):
         t[f"multi{k}_dst+2_src+4"] = (k, multi([p + 4 for p in ptrs[:k]], recv + 2))
         t[f"multi{k}_src+4"] = (k, multi([p + 4 for p in ptrs[:k]], recv))
         t[f"multi{k}_strad"] = (k, multi([p + 16 * (2 * j + 1) for j, p in enumerate(ptrs[:k])], recv))
+        t[f"chain{k}"] = (k, chain(ptrs[:k], recv, recv))
         t[f"chain{k}_dst+2"] = (k, chain(ptrs[:k], recv + 2, recv + 2))
         t[f"chain{k}_dst+2_src+4"] = (k, chain([p + 4 for p in ptrs[:k]], recv + 2, recv + 2))
         t[f"chain{k}_src+4"] = (k, chain([p + 4 for p in ptrs[:k]], recv, recv))
@@ -88,6 +89,7 @@ def main():
     p.add_argument("--launches", type=int, default=10)
     p.add_argument("--mib", type=int, default=1024)
     p.add_argument("--out", default="")
+    p.add_argument("--all-k", default="", help="comma-separated case stems expanded over k = 2..8, e.g. multi,chain_strad")
     a = p.parse_args()
     libs = [bind(x) for x in a.libs]
     st = torch.cuda.current_stream().cuda_stream
@@ -100,7 +102,10 @@ def main():
         dccl_amd.check(dccl_amd.synth_fill(ptrs[-1], 7, nbytes // 4, 0, 0xDCC1, 10 + j, st), "synth")
         off += nbytes + 4096 * (j + 1)
     table = case_table(ptrs)
-    names = a.cases.split(",")
+    names = a.cases.split(",") if a.cases else []
+    for stem in filter(None, a.all_k.split(",")):
+        head, _, tail = stem.partition("_")
+        names += [f"{head}{k}" + (f"_{tail}" if tail else "") for k in range(2, 9)]
     # bit-exactness of B against A at the timed count (the destination restored between the two runs)
     exact = {}
     m = n

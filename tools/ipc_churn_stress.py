@@ -31,7 +31,6 @@ def main():
     p.add_argument("--grow", action="store_true")
     p.add_argument("--two", action="store_true")
     p.add_argument("--register", action="store_true")
-    p.add_argument("--zero-copy", action="store_true", help="DCCL_IPC_ZERO_COPY=1: registered buffers read in place")
     p.add_argument("--trace", default="", help="directory: DCCL_IPC_DEBUG=1, every rank's stderr kept per run "
                                                "(runs without a wrong slice are deleted)")
     a = p.parse_args()
@@ -49,8 +48,7 @@ def main():
         q = ctx.Queue()
         tag = "stress_" + uuid.uuid4().hex[:10]
         ps = [ctx.Process(target=_ipc_realloc_rank,
-                          args=(r, a.world, a.mib << 20, a.rounds, a.grow, tag, q, a.two, False, a.register,
-                                a.zero_copy))
+                          args=(r, a.world, a.mib << 20, a.rounds, a.grow, tag, q, a.two, False, a.register))
               for r in range(a.world)]
         for x in ps:
             x.start()
@@ -80,7 +78,7 @@ def main():
             shutil.rmtree(run_dir, ignore_errors=True)
         print(f"run {run}: {'FAILED ' + repr(bad) if bad else 'ok'}", file=sys.stderr, flush=True)
     print(json.dumps({"runs": a.runs, "world": a.world, "mib": a.mib, "rounds": a.rounds, "grow": a.grow,
-                      "two": a.two, "register": a.register, "zero_copy": a.zero_copy, "failed_runs": failed, "reports": reports[:5]}, default=str), flush=True)
+                      "two": a.two, "register": a.register, "failed_runs": failed, "reports": reports[:5]}, default=str), flush=True)
 
 
 if __name__ == "__main__":
