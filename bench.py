@@ -624,6 +624,8 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
         dist.all_reduce(rf)
         yf_by = {}
         for name, comm in comms.items():
+            if rank == 0:
+                progress(f"child: all_reduce over {name}, {count * 4 >> 20} MiB, W = {world}")
             os.environ["DCCL_ALLREDUCE_ALGORITHM"] = algo_env[name]
             yi = xi.clone()
             yf = xf.clone()
@@ -673,6 +675,8 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
                                  "backend": dist.get_backend(),
                                  "note": "the torch.distributed backend's own all_reduce (RCCL when the backend is "
                                          "nccl), informational: its combine is the backend's"}
+        if rank == 0:
+            progress("child: all_gather of every transport")
         out["dccl_allgather"] = allgather_compare({k: v for k, v in comms.items() if k != "grouped"}, world, rank,
                                                   dev, st, count, iters)
         # BASELINE C5's exchange step at its own size (the reduced shards of DCCL_BENCH_C5_GIB GiB of fp32,
@@ -680,6 +684,8 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
         c5_gib = float(os.environ.get("DCCL_BENCH_C5_GIB", "0") or 0)
         if c5_gib > 0 and "direct" in comms:
             c5_count = int(c5_gib * GIB) // 4 // world * world
+            if rank == 0:
+                progress(f"child: C5's all_gather, {c5_gib:g} GiB")
             torch.cuda.empty_cache()
             out["c5_allgather"] = allgather_compare({"direct": comms["direct"]}, world, rank, dev, st, c5_count, 3)
     finally:
@@ -853,6 +859,17 @@ def progress(msg: str) -> None:
 
 
 CHILD_TIMEOUT_S = 150.0
+# DCCL_BENCH_RCCL_REHEARSAL=1 with more ranks than GPUs: RCCL runs over loopback sockets, ~100x slower than
+# xGMI, so the child's collectives are sized down (the paths are the same) and given longer
+REHEARSAL_CHILD_TIMEOUT_S = 420.0
+REHEARSAL_AR_MIB = 32
+REHEARSAL_C5_GIB = 1.0
+
+
+def socket_rehearsal(world: int, backend: str) -> bool:
+    """N RCCL ranks sharing fewer GPUs over loopback sockets (DCCL_BENCH_RCCL_REHEARSAL=1)."""
+    return (backend == "nccl" and os.environ.get("DCCL_BENCH_RCCL_REHEARSAL") == "1"
+            and world > torch.cuda.device_count())
 
 
 def collective_in_child(world: int, rank: int, local: int, backend: str, c5_gib: float = 0.0) -> dict:
@@ -872,17 +889,23 @@ def collective_in_child(world: int, rank: int, local: int, backend: str, c5_gib:
     # not the launcher's agent store (torchrun exports TORCHELASTIC_USE_AGENT_STORE): the child's rank 0
     # hosts its own store on the fresh port
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    rehearsal = socket_rehearsal(world, backend)
+    timeout = REHEARSAL_CHILD_TIMEOUT_S if rehearsal else CHILD_TIMEOUT_S
     env = {**env, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port[0]), "RANK": str(rank),
            "WORLD_SIZE": str(world), "LOCAL_RANK": str(local), "DCCL_BENCH_BACKEND": backend,
-           "DCCL_BOOTSTRAP_TAG": f"bench_child_{port[0]}", "DCCL_BENCH_C5_GIB": str(c5_gib)}
+           "DCCL_BOOTSTRAP_TAG": f"bench_child_{port[0]}",
+           "DCCL_BENCH_C5_GIB": str(min(c5_gib, REHEARSAL_C5_GIB) if rehearsal else c5_gib),
+           "DCCL_BENCH_AR_MIB": str(REHEARSAL_AR_MIB if rehearsal else 256),
+           "DCCL_BENCH_CHILD_TIMEOUT_S": str(timeout)}
     torch.cuda.synchronize()
-    progress(f"namespace-dccl all_reduce extras in a child process (port {port[0]})")
+    progress(f"namespace-dccl all_reduce extras in a child process (port {port[0]}"
+             + (f", socket rehearsal: {REHEARSAL_AR_MIB} MiB all-reduces, timeout {timeout:.0f}s)" if rehearsal else ")"))
     t0 = time.perf_counter()
     try:
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--collective-child"], env=env,
-                           stdout=subprocess.PIPE, stderr=None, text=True, timeout=CHILD_TIMEOUT_S)
+                           stdout=subprocess.PIPE, stderr=None, text=True, timeout=timeout)
     except subprocess.TimeoutExpired:
-        return {"error": f"child timed out after {CHILD_TIMEOUT_S:.0f}s and was killed"}
+        return {"error": f"child timed out after {timeout:.0f}s and was killed"}
     progress(f"child exited with {p.returncode} after {time.perf_counter() - t0:.1f}s")
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     res = json.loads(lines[-1]) if lines else {}
@@ -905,8 +928,9 @@ def collective_child() -> None:
         dist.init_process_group("nccl", device_id=dev, timeout=limit)
     else:
         dist.init_process_group(backend, timeout=limit)
-    count = (256 << 20) // 4 // world * world
-    res, finished = run_with_watchdog(lambda: dccl_allreduce_multi(world, rank, dev, count), CHILD_TIMEOUT_S - 30)
+    count = (int(os.environ.get("DCCL_BENCH_AR_MIB", "256")) << 20) // 4 // world * world
+    limit_s = float(os.environ.get("DCCL_BENCH_CHILD_TIMEOUT_S", str(CHILD_TIMEOUT_S)))
+    res, finished = run_with_watchdog(lambda: dccl_allreduce_multi(world, rank, dev, count), limit_s - 30)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if not finished or "error" in res:

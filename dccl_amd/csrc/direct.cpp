@@ -152,6 +152,8 @@ struct ProcCache {
     HipOps ops;
     ipc::ImportCache imports{&ops, kMaxOpenMappings, kMaxOpenBytes};
     std::vector<IpcXport*> xports;  // live IPC communicators of this process
+    void* token_buf = nullptr;      // 16 device bytes and a stream for read_token
+    hipStream_t token_stream = nullptr;
     // handle bytes of every export this process made -> the buffer id of the allocation they named
     std::map<std::string, uint64_t> handle_owner;
     // exporter-side counters (dccl_ipc_stats)
@@ -413,6 +415,34 @@ ncclResult_t ensure_ipc_scratch(ProcCache& pc, IpcXport* x, size_t bytes) {
 
 // --- importer side (caller holds pc.mu) ---------------------------------------------------------------
 
+// Read a new mapping's token through a compute kernel (dccl_copy_multi into 16 device bytes, then to the
+// host), i.e. through the address translation the combine kernels use, not a DMA engine's.  The round-4
+// zero-copy failures were a recycled importer address reading other pages on first use.
+bool read_token(ProcCache& pc, const void* mapped, uint64_t got[2]) {
+    if (pc.token_buf == nullptr) {
+        if (hipMalloc(&pc.token_buf, 16) != hipSuccess) {
+            (void)hipGetLastError();
+            pc.token_buf = nullptr;
+            return false;
+        }
+        if (hipStreamCreateWithFlags(&pc.token_stream, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(pc.token_buf);
+            pc.token_buf = nullptr;
+            return false;
+        }
+    }
+    const void* src = mapped;
+    void* dst = pc.token_buf;
+    if (dccl_copy_multi(&src, &dst, 1, 16, pc.token_stream) != DCCL_SUCCESS ||
+        hipMemcpyAsync(got, pc.token_buf, 16, hipMemcpyDeviceToHost, pc.token_stream) != hipSuccess ||
+        hipStreamSynchronize(pc.token_stream) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return true;
+}
+
 // Peer addresses of one collective's two buffers, own rank included.  On the IPC transport it holds a use
 // of every peer mapping it resolved, released when the collective returns (after its last phase point).
 struct Peers {
@@ -450,7 +480,7 @@ ncclResult_t import_desc(ProcCache& pc, uint32_t peer, int64_t pid, const Desc& 
         r = pc.imports.acquire(pid, d.serial, h, d.size, &base, 15, &opened);
         if (r != ipc::kOk || !opened || (d.token[0] == 0 && d.token[1] == 0)) break;
         uint64_t got[2] = {0, 0};
-        if (hipMemcpy(got, base, sizeof(got), hipMemcpyDeviceToHost) != hipSuccess) (void)hipGetLastError();
+        (void)read_token(pc, base, got);  // a failed read leaves {0, 0}: never a valid token
         if (got[0] == d.token[0] && got[1] == d.token[1]) break;
         ++pc.imports.stats.verify_failures;
         if (ipc_debug())

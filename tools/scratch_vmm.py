@@ -38,6 +38,7 @@ def main():
     p.add_argument("--sizes", default="512,256,128")
     p.add_argument("--out", default="")
     a = p.parse_args()
+    bench._native()
     vmm = ctypes.CDLL(LIB)
     vmm.vmm_alloc.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     vmm.vmm_free.argtypes = [ctypes.c_void_p]
