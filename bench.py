@@ -6,7 +6,7 @@ operands resident in HBM (BASELINE.json metric: ncclSum fp32, 1 GiB).  Each rank
 own 1 GiB shard pair (the combine is element-wise: no data-path collective), so the
 aggregate is weak scaling.  Operands are carved from one HBM allocation (recv, then send 4 KiB
 past its end); the separately allocated layout is timed too and reported as `other_layout`
-(DESIGN.md §3.1: separate 1 GiB allocations land in one of two physical placement modes).
+(DESIGN.md §3.2: separate 1 GiB allocations land in one of two physical placement modes).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--mib 1024] [--dtype float32] [--op sum]
 
@@ -127,7 +127,7 @@ def operand_pair(n: int, dt: int, op: int, buffer_id: int, device, layout: str):
     """(send, recv) synthetic operands.  "pooled": both carved from ONE HBM allocation, recv first
     and send PAIR_GAP bytes past its end; "separate": two allocations (DCCL's own shape: scratchpad
     + user chunk).  Separately allocated 1 GiB operands land in one of two physical placement modes
-    (0.476 vs 0.508 ms on MI355X, DESIGN.md §3.1); the pooled layout is consistently in the fast one."""
+    (0.476 vs 0.508 ms on MI355X, DESIGN.md §3.2); the pooled layout is consistently in the fast one."""
     nbytes = n * dccl_amd.size_of_type(dt)
     tdt = dccl_amd.TORCH_DTYPES[dt]
     if layout == "separate":
@@ -1013,7 +1013,7 @@ def launch_ranks(a, argv) -> int:
 def other_layout_median(n: int, dt: int, op: int, rank: int, dev, stream, layout: str, pairs: int,
                         launches: int) -> dict:
     """The other operand layout, timed on `pairs` operand pairs allocated side by side (each separately
-    allocated pair lands in its own physical placement, DESIGN.md §3.1; the pooled layout has one), every
+    allocated pair lands in its own physical placement, DESIGN.md §3.2; the pooled layout has one), every
     pair `launches` back-to-back launches; the median pair is reported (DCCL's own operand shape is the
     separate one: scratchpad + user chunk)."""
     import statistics

@@ -127,7 +127,7 @@ ncclResult_t all_reduce_ring(dccl::dcclComm* c, void* buffer, void* scratch, siz
 // the reference's.  One deliberate fix: the reference's recursive-doubling all-gather sends one slice
 // per step (its step_bsize doubling sits inside a comment, all_gather_recursive_doubling.cpp:85), so
 // with a subworld of 4 or more ranks some blocks never arrive; here step s moves 2^s slices and every
-// rank ends with the whole result (DESIGN.md §7.4).
+// rank ends with the whole result (DESIGN.md §7.1).
 // ------------------------------------------------------------------------------------------
 namespace {
 

@@ -235,7 +235,7 @@ ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
     }
     // Spin (with the pause hint) for up to kSpin before sleeping: peers arrive within microseconds of
     // each other in a collective, and a 20 us sleep costs 50-80 us once the kernel's timer slack is
-    // added, which set the latency of small collectives (DESIGN.md §5.3).
+    // added, which set the latency of small collectives (DESIGN.md §7.3).
     constexpr auto kSpin = std::chrono::milliseconds(2);
     constexpr auto kLiveness = std::chrono::milliseconds(100);
     const auto start = std::chrono::steady_clock::now();
@@ -822,7 +822,7 @@ int ipc_stats(uint64_t* out, int n) {
 
 // In-process groups take the direct collectives for device buffers unless DCCL_ALLREDUCE_ALGORITHM names
 // another algorithm: "direct", "auto" and unset select them.  They are faster than the ring at every
-// size measured (DESIGN.md §5.3) and give the ring's results bit for bit.  Host buffers, the RCCL
+// size measured (DESIGN.md §7.3) and give the ring's results bit for bit.  Host buffers, the RCCL
 // transport and groups above 8 ranks keep the ring.
 bool direct_selected(const dcclComm* c) {
     if (c->ipc != nullptr) return true;

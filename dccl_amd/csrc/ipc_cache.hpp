@@ -10,7 +10,7 @@
 // (direct.cpp).  Mappings here are keyed by (exporter pid, serial), so two exports can never share a key.
 //
 // What the runtime does underneath is still guarded, because the handle BYTES of a new allocation may
-// repeat those of a freed one (dmabuf handles on ROCm 7.2, DESIGN.md §5.4), and opening handle bytes that
+// repeat those of a freed one (dmabuf handles on ROCm 7.2, DESIGN.md §7.3), and opening handle bytes that
 // this process already has open hands back that earlier import (the freed allocation's pages):
 //   * before an open, any mapping of the same exporter with the same handle bytes names an export that
 //     has ended (two live allocations never share a handle): it is closed first if unused, and the open
@@ -87,13 +87,15 @@ public:
         Handle handle{};
         uint32_t users = 0;    // collectives of this process that resolved it and have not returned
         bool retired = false;  // its export ended while in use: closed at the last release
+        bool suspect = false;  // in use when its exporter's retirement log overflowed: maybe ended, maybe not
     };
 
     ImportCache(Ops* ops, size_t max_mappings, size_t max_bytes)
         : ops_(ops), max_mappings_(max_mappings), max_bytes_(max_bytes) {}
 
     // Map export (pid, serial) with handle `h` of an allocation of `size` bytes and take a use of it.
-    // *opened (optional): true when this call opened the mapping (the caller may verify it before trusting it).
+    // *opened (optional): true when the caller must verify the mapping before trusting it: this call opened
+    // it, or it was suspect (see retire_pid).  A failed verification is followed by release + retire.
     Result acquire(int64_t pid, uint64_t serial, const Handle& h, uint64_t size, void** base, int max_attempts = 15,
                    bool* opened = nullptr) {
         const Key k{pid, serial};
@@ -103,6 +105,8 @@ public:
             ++it->second.users;
             ++stats.reused;
             *base = it->second.base;
+            if (it->second.suspect && opened) *opened = true;  // re-verified by the caller, then trusted again
+            it->second.suspect = false;
             return kOk;
         }
         if (it != map_.end()) {  // a retired export published again: the exporter broke its serials
@@ -173,14 +177,17 @@ public:
         else it->second.retired = true;
     }
 
-    // The exporter's retirement log overflowed: every mapping of it may be stale.
+    // The exporter's retirement log overflowed: every mapping of it may be stale.  Unused ones are closed; one
+    // in use (possibly a live export, such as the peer's current scratch that another communicator's collective
+    // is reading) becomes SUSPECT rather than retired: its next acquire hands it out for re-verification
+    // (retiring it made a concurrent acquire fail with kAliasInUse although nothing was stale).
     void retire_pid(int64_t pid) {
         ++stats.retired_pid;
         for (auto it = map_.begin(); it != map_.end();) {
             auto next = std::next(it);
             if (it->first.pid == pid && !it->second.retired) {
                 if (it->second.users == 0) close_entry(it);
-                else it->second.retired = true;
+                else it->second.suspect = true;
             }
             it = next;
         }

@@ -70,7 +70,7 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
         size_t grid = ceil_div(ceil_div(nvec, size_t(64)), size_t(8)) * 8;  // a multiple of 8 (kMaxGrid is one)
         if (grid == 0) grid = 8;
         unsigned p = unsigned(as & 15);
-        int order = kOrderGroup;  // one front, shared lines in one L2: +4.5 points over the XCD ranges
+        int order = kOrderGroup;  // one front, shared lines in one L2: +4.5 points over the XCD ranges (round 3)
         void* args[] = {const_cast<unsigned char**>(&s), &p, const_cast<unsigned char**>(&r),
                         const_cast<size_t*>(&nvec), &count, &order};
         return launch(reinterpret_cast<const void*>(&reduce_unaligned_kernel<T, OP>), grid, args, stream, 64);

@@ -335,7 +335,7 @@ __global__ __launch_bounds__(C::BLOCK) void reduce_chain_vec_kernel(SendList sen
 // the 32 bytes are funnel-shifted by p_j (v_alignbyte_b32, any byte count).  An operand with p_j == 0 is
 // a plain vector load.  The head / tail scalars read operands bytewise (any alignment).  One operand at a
 // time, uncapped (74-79 % of peak, profiles/r1_s5_phased_probe.json), or, from k = 5 (k-way) / k = 4 (chain),
-// every operand's loads first under caps of their own (below).
+// every operand's loads first under caps of their own (below; DESIGN.md §3, caps.hpp).
 // One-wave blocks and a per-tile loop uniform per wave: every lane reaches the lane exchange.
 // ---------------------------------------------------------------------------------
 struct PhaseList { unsigned p[9]; };
@@ -375,7 +375,7 @@ __device__ __forceinline__ u32x4 ld_phased_finish(const PhasedLoad& x, unsigned 
 inline constexpr int kPhasedXcdMaxK = 4;
 // Where caps::kMultiPhasedFirst / kChainPhasedFirst (caps.hpp) have an entry, the phased kernels take the
 // loads-first form (ld_phased_issue / ld_phased_finish) under that cap and in the tile-run order caps::kRun
-// (DESIGN.md §12, §13); uncapped it loses (too many streams in flight).
+// (caps.hpp); uncapped it loses (too many streams in flight).
 
 // The 16 body bytes of vector v (zero for v >= nvec) of an operand whose body starts at `body`,
 // phase p.  All 64 lanes must call it (p is uniform).

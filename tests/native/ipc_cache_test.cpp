@@ -174,10 +174,41 @@ void test_retire_pid() {
     c.release(100, 2);
     c.retire_pid(100);
     CHECK(c.find(100, 1) == nullptr && c.find(100, 2) == nullptr);
-    CHECK(c.find(100, 3) != nullptr && c.find(100, 3)->retired);
-    CHECK(c.find(200, 1) != nullptr && !c.find(200, 1)->retired);
+    // in use: suspect, not retired (it may be a live export another collective is reading)
+    CHECK(c.find(100, 3) != nullptr && !c.find(100, 3)->retired && c.find(100, 3)->suspect);
+    CHECK(c.find(200, 1) != nullptr && !c.find(200, 1)->retired && !c.find(200, 1)->suspect);
     c.release(100, 3);
-    CHECK(c.find(100, 3) == nullptr && rt.bad_closes == 0);
+    CHECK(c.find(100, 3) != nullptr && rt.bad_closes == 0);
+}
+
+// a retirement-log overflow while a mapping is in use.  A concurrent acquire of the same live
+// export gets it for re-verification instead of kAliasInUse; when verification passes it is trusted again; when
+// it fails (the export had ended) the caller's release + retire close it with its last use.
+void test_overflow_while_in_use() {
+    FakeRuntime rt;
+    ImportCache c(&rt, 16, 1 << 30);
+    void *a = nullptr, *b = nullptr;
+    bool opened = false;
+    CHECK(c.acquire(100, 5, handle(5), 4096, &a, 15, &opened) == kOk && opened);  // collective 1 holds it
+    c.retire_pid(100);
+    CHECK(c.acquire(100, 5, handle(5), 4096, &b, 15, &opened) == kOk && opened);  // collective 2: verify it
+    CHECK(a == b && rt.opens == 1 && c.stats.alias_errors == 0 && c.find(100, 5)->users == 2);
+    CHECK(!c.find(100, 5)->suspect);
+    CHECK(c.acquire(100, 5, handle(5), 4096, &b, 15, &opened) == kOk && !opened);  // verified: trusted again
+    c.release(100, 5);
+    c.release(100, 5);
+    c.release(100, 5);
+    CHECK(c.find(100, 5) != nullptr && c.find(100, 5)->users == 0);
+    // the same with a failed verification: collective 2 releases and retires; closed at collective 1's release
+    CHECK(c.acquire(100, 6, handle(6), 4096, &a, 15, &opened) == kOk && opened);
+    c.retire_pid(100);  // closes the unused (100, 5), marks (100, 6) suspect
+    CHECK(c.find(100, 5) == nullptr && c.find(100, 6)->suspect);
+    CHECK(c.acquire(100, 6, handle(6), 4096, &b, 15, &opened) == kOk && opened);
+    c.release(100, 6);
+    c.retire(100, 6);
+    CHECK(c.find(100, 6) != nullptr && c.find(100, 6)->retired);  // collective 1 still reads it
+    c.release(100, 6);
+    CHECK(c.find(100, 6) == nullptr && rt.bad_closes == 0 && c.stats.alias_errors == 0);
 }
 
 void test_trim() {
@@ -237,6 +268,7 @@ int main() {
     test_open_returns_cached_base();
     test_retire_while_in_use_closes_at_release();
     test_retire_pid();
+    test_overflow_while_in_use();
     test_trim();
     test_size_mismatch_and_open_failure();
     test_churn();

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of the unaligned-destination k-way / chain variants (tools/tune/unaligned_v4.hip) against the product
-kernels, fp32 Sum, 1 GiB per operand (tuning only; DESIGN.md §4.3).  Operands: ten 1 GiB buffers from one
+kernels, fp32 Sum, 1 GiB per operand (tuning only; DESIGN.md §3.4).  Operands: ten 1 GiB buffers from one
 allocation, 4 KiB x (j+1) stagger (tools/ab_cases.py's layout).  Every case is checked bit for bit against
 the product on a 1 Mi-element slice, then timed interleaved (HIP events around --launches back-to-back
 launches per round, median over --rounds), as a fraction of (k+2) * N * 4 B at 8 TB/s.

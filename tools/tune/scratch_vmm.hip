@@ -85,3 +85,10 @@ extern "C" int vmm_free(void* base) {
     live.erase(it);
     return 0;
 }
+
+// hipExtMallocWithFlags with a flag (hipDeviceMallocContiguous = 4: physically contiguous), for the placement
+// probe (tools/alloc_probe.py); free with hipFree.
+extern "C" int ext_alloc(size_t bytes, unsigned flags, void** out) {
+    return hipExtMallocWithFlags(out, bytes, flags) == hipSuccess ? 0 : 1;
+}
+extern "C" int ext_free(void* p) { return hipFree(p) == hipSuccess ? 0 : 1; }
