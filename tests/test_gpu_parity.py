@@ -436,6 +436,41 @@ def test_windows_tuned_forms_full_size(dccl, k, mib):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("k", [4, 7])
+def test_chain_own_only_off_phase_full_size(dccl, k):
+    """A chain whose sources share the destination's 16-B phase while `own` sits at another phase (own != dst),
+    at 96 MiB per operand, where the phased chain launches with sources off phase take reduce_windows_kernel:
+    this one keeps the phased kernels (the windows forms were measured with sources off phase).
+    fp32 Sum and int32 Max against torch in the ring's order, bit for bit; nothing outside dst written."""
+    nb = (96 << 20) + 4096
+    for dt, tdt, op in [(7, torch.float32, 0), (2, torch.int32, 2)]:
+        n = nb // 4
+        g = torch.Generator(device="cuda").manual_seed(3100 + k + dt)
+
+        def operand():
+            if tdt == torch.int32:
+                return torch.randint(-(1 << 30), 1 << 30, (n,), device="cuda", dtype=tdt, generator=g)
+            return torch.rand(n, device="cuda", generator=g) * 2 - 1
+
+        sends = [operand() for _ in range(k)]
+        own = operand()
+        obuf = torch.zeros(nb + 1024, dtype=torch.uint8, device="cuda")
+        obuf[4:4 + nb].copy_(own.view(torch.uint8))
+        d = torch.zeros(nb + 1024, dtype=torch.uint8, device="cuda")
+        f = _torch_op(op)
+        acc = sends[0]
+        for x in sends[1:]:
+            acc = f(x, acc)
+        want = f(own, acc)
+        rc = dccl.local_reduce_chain([x.data_ptr() for x in sends], obuf.data_ptr() + 4, d.data_ptr(), dt, n, op, 0)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert torch.equal(d[:nb].view(torch.int32), want.view(torch.int32)), (k, dt)
+        assert not d[nb:].any()
+        del sends, own, obuf, d
+        torch.cuda.empty_cache()
+
+
 # ----------------------------------------------------------------------------- host path
 @pytest.mark.parametrize("zero_copy", ["default", "0"])
 @pytest.mark.parametrize("pinned", ["none", "both", "send"])

@@ -6,9 +6,9 @@ with a wrong slice or an error, and the first few reports.
 
     python tools/ipc_churn_stress.py [--runs 20] [--world 2] [--mib 1] [--rounds 140] [--grow] [--two] [--register]
 
-With --register every round registers its buffers (peers map them in place) and deregisters them before
-the free; a wrong slice is reported with whether its exporter's input sat at the same address as the round
-before (`va_reused`).
+With --register every round registers its buffers and deregisters them before the free (tracked only since
+round 5: peers read the scratch either way); a wrong slice is reported with whether its exporter's input sat at
+the same address as the round before (`va_reused`).
 """
 import argparse
 import json
