@@ -152,8 +152,8 @@ struct ProcCache {
     HipOps ops;
     ipc::ImportCache imports{&ops, kMaxOpenMappings, kMaxOpenBytes};
     std::vector<IpcXport*> xports;  // live IPC communicators of this process
-    void* token_buf = nullptr;      // 16 device bytes and a stream for read_token
-    hipStream_t token_stream = nullptr;
+    // read_token's 16 device bytes and stream, per device (a mapping belongs to the device it was opened on)
+    std::map<int, std::pair<void*, hipStream_t>> token_io;
     // handle bytes of every export this process made -> the buffer id of the allocation they named
     std::map<std::string, uint64_t> handle_owner;
     // exporter-side counters (dccl_ipc_stats)
@@ -419,24 +419,31 @@ ncclResult_t ensure_ipc_scratch(ProcCache& pc, IpcXport* x, size_t bytes) {
 // host), i.e. through the address translation the combine kernels use, not a DMA engine's.  The round-4
 // zero-copy failures were a recycled importer address reading other pages on first use.
 bool read_token(ProcCache& pc, const void* mapped, uint64_t got[2]) {
-    if (pc.token_buf == nullptr) {
-        if (hipMalloc(&pc.token_buf, 16) != hipSuccess) {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    auto io = pc.token_io.find(dev);
+    if (io == pc.token_io.end()) {
+        void* buf = nullptr;
+        hipStream_t st = nullptr;
+        if (hipMalloc(&buf, 16) != hipSuccess) {
             (void)hipGetLastError();
-            pc.token_buf = nullptr;
             return false;
         }
-        if (hipStreamCreateWithFlags(&pc.token_stream, hipStreamNonBlocking) != hipSuccess) {
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
             (void)hipGetLastError();
-            (void)hipFree(pc.token_buf);
-            pc.token_buf = nullptr;
+            (void)hipFree(buf);
             return false;
         }
+        io = pc.token_io.emplace(dev, std::make_pair(buf, st)).first;
     }
     const void* src = mapped;
-    void* dst = pc.token_buf;
-    if (dccl_copy_multi(&src, &dst, 1, 16, pc.token_stream) != DCCL_SUCCESS ||
-        hipMemcpyAsync(got, pc.token_buf, 16, hipMemcpyDeviceToHost, pc.token_stream) != hipSuccess ||
-        hipStreamSynchronize(pc.token_stream) != hipSuccess) {
+    void* dst = io->second.first;
+    hipStream_t st = io->second.second;
+    if (dccl_copy_multi(&src, &dst, 1, 16, st) != DCCL_SUCCESS ||
+        hipMemcpyAsync(got, dst, 16, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }

@@ -385,8 +385,9 @@ def test_windows_tuned_forms_full_size(dccl, k, mib):
     """From caps::kWindowTunedBytes (96 MiB per operand) reduce_windows_kernel takes its tuned forms (caps.hpp
     kWindow: block order under a 26-wave cap with sources in phase; with sources off phase group order, loads-
     first at k = 4, 5 under 14 / 12 waves, loads-first in runs of 4 tiles at k = 6..8) and takes over the phased
-    launches at k-way k = 3..5 and chain k = 4..7; below it (64, 72 MiB) the uncapped per-operand form and the
-    phased kernels run.  Destination not
+    launches at k-way k = 3..5 and chain k = 4..7; at 64 and 72 MiB (caps.hpp window_mid) sources off phase take
+    the mid-size form, phased launches into a 16-B aligned destination too, in-phase sources the per-operand
+    form uncapped.  Destination not
     element-aligned, and element-aligned at 16-B phases 0 and 4; sources at phase 0, 4 and 16; k-way and chain in
     place; fp32 Sum, int32 Max, bf16 Sum, int64 Min, against torch applied on the device in the kernels' order, bit for
     bit; nothing outside the destination written."""
