@@ -84,3 +84,20 @@ def test_allreduce_summary_keeps_the_flags():
     assert s["rccl"] == {"ms": 1.5, "busbw_gb_s": 1.0} and s["fp32_direct_bit_exact_vs_ring"]
     assert s["dccl_allgather"] == {"direct": {"bit_exact": True, "ms": 0.1, "busbw_gb_s": 3.0}}
     assert bench.allreduce_summary({"error": "x"}) == {"error": "x"}
+
+
+def test_socket_rehearsal_sizes_only_when_ranks_share_gpus(monkeypatch):
+    """The N > 1 child's collectives are sized down only for a socket rehearsal (DCCL_BENCH_RCCL_REHEARSAL=1 with
+    more RCCL ranks than GPUs); a real one-GPU-per-rank run keeps 256 MiB all-reduces and C5's full size."""
+    import bench
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setenv("DCCL_BENCH_RCCL_REHEARSAL", "1")
+    assert bench.socket_rehearsal(8, "nccl") and not bench.socket_rehearsal(1, "nccl")
+    assert not bench.socket_rehearsal(8, "gloo")
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert not bench.socket_rehearsal(8, "nccl")
+    monkeypatch.delenv("DCCL_BENCH_RCCL_REHEARSAL")
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert not bench.socket_rehearsal(8, "nccl")
+    assert bench.REHEARSAL_CHILD_TIMEOUT_S > bench.CHILD_TIMEOUT_S and bench.REHEARSAL_AR_MIB < 256
