@@ -143,7 +143,8 @@ EXPORTED_SYMBOLS = [
     "dccl_bootstrap_done", "dccl_comm_register", "dccl_comm_deregister", "dccl_ipc_stats",
 ]
 
-#: names of the dccl_ipc_stats counters, in order (include/dccl/dccl_comm.h)
+#: names of the dccl_ipc_stats counters, in order (include/dccl/dccl_comm.h); registered_hits,
+#: stale_registrations and registered_fallbacks counted the registered in-place path removed in round 5 (always 0)
 IPC_STAT_NAMES = [
     "exports_made", "exports_retired", "registered_hits", "scratch_copies", "scratch_bytes", "scratch_grows",
     "stale_registrations", "mappings_opened", "mappings_reused", "mappings_retired", "retire_log_overflows",
@@ -298,8 +299,8 @@ class Comm:
         return int(lib.dccl_broadcast(send, recv, count, dtype, root, self.handle, stream or None))
 
     def register(self, ptr: int, size: int) -> int:
-        """dcclRegisterCacheMemory: on an IPC communicator, peers then read device memory in
-        [ptr, ptr + size) in place until deregister(ptr); 64-byte aligned address and size."""
+        """dcclRegisterCacheMemory: host memory is page-locked; device memory is validated and tracked
+        until deregister(ptr) (peers read inputs through the scratch); 64-byte aligned address and size."""
         return int(lib.dccl_comm_register(self.handle, ptr, size))
 
     def deregister(self, ptr: int) -> int:

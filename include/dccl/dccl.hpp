@@ -86,9 +86,9 @@ ncclResult_t dcclCommInitRccl(ncclComm_t* comm, uint32_t world_size, uint32_t ra
 ncclResult_t dcclCommInitIpc(ncclComm_t* comm, uint32_t world_size, uint32_t rank);
 ncclResult_t ncclCommFinalize(ncclComm_t comm);
 
-/** Page-lock host memory for direct DMA.  Device memory on an IPC communicator: peers read the range
- *  in place until it is deregistered (other device buffers are copied into the communicator's scratch
- *  for them); on other communicators: accepted, nothing to do. */
+/** Page-lock host memory for direct DMA.  Device memory: validated (on an IPC communicator: a device
+ *  allocation of this process, the range inside it) and tracked; peers read every input through the
+ *  communicator's scratch, never user memory. */
 ncclResult_t dcclRegisterCacheMemory(ncclComm_t comm, void* buffer, size_t size);
 ncclResult_t dcclDeregisterCacheMemory(ncclComm_t comm, void* buffer, size_t size = 0UL);
 
