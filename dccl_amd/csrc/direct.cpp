@@ -715,7 +715,9 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
     if (!x->liveness && x->timeout_s <= 0) x->timeout_s = 300;  // no liveness check: a dead peer ends the wait
     ShmSlot& me = ctl->slot[rank];
     me.start = proc_start_time(static_cast<long>(::getpid()));
-    me.pid = ::getpid();
+    // tests only (DCCL_FAULT_INJECT=hidden_pid:<rank>): publish a pid no peer can see, as a rank in another pid
+    // namespace would
+    me.pid = fault_injected("hidden_pid", rank) ? int64_t(0x7ffffff0) : int64_t(::getpid());
     ctl->joined.fetch_add(1);
     c->ipc = x;
     c->rank = rank;

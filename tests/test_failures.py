@@ -305,3 +305,57 @@ def test_ipc_failure_is_sticky_and_finalize_releases(gpu, tmp_path):
     import glob
     assert not glob.glob(f"/dev/shm/dccl_ipc_{outs[0]['pid']}_*"), "rank 0's segment left behind"
     assert not list(tmp_path.iterdir()), list(tmp_path.iterdir())
+
+
+# ---------------------------------------------------------------------------------------------
+# a peer whose process this rank cannot see (another pid namespace, /proc hidepid)
+# ---------------------------------------------------------------------------------------------
+IPC_HIDDEN_CHILD = """
+import json, os
+import torch
+import dccl_amd
+W, r = int(os.environ["W"]), int(os.environ["RANK_ID"])
+torch.cuda.set_device(0)
+comm = dccl_amd.Comm.ipc(W, r)
+n = 1024 * W
+x = torch.full((n,), float(r + 1), device="cuda")
+st = torch.cuda.current_stream().cuda_stream
+rcs = []
+for _ in range(3):
+    x.fill_(float(r + 1))
+    torch.cuda.synchronize()
+    rcs.append(comm.all_reduce(x.data_ptr(), x.data_ptr(), n, 7, 0, st))
+    torch.cuda.synchronize()
+ok = bool(torch.all(x == float(W * (W + 1) // 2)))
+print(json.dumps({"rcs": rcs, "ok": ok, "finalize": comm.finalize()}))
+"""
+
+
+@pytest.mark.gpu
+def test_ipc_invisible_peer_turns_liveness_off(gpu, tmp_path):
+    """A rank whose peers cannot see its process (DCCL_FAULT_INJECT=hidden_pid:1 publishes a pid that does not
+    exist) must not be taken for dead: its peers turn the liveness check off for that communicator at join and
+    say so once on stderr, and every collective succeeds (before, any barrier wait over 100 ms became
+    ncclRemoteError)."""
+    import uuid
+    W, tag = 2, "ipchide_" + uuid.uuid4().hex[:10]
+    env = {**os.environ, "PYTHONPATH": ROOT, "W": str(W), "DCCL_BOOTSTRAP_TAG": tag, "DCCL_BOOTSTRAP_DIR": str(tmp_path),
+           "DCCL_FAULT_INJECT": "hidden_pid:1"}
+    env.pop("DCCL_IPC_TIMEOUT_S", None)
+    ps = [subprocess.Popen([sys.executable, "-c", textwrap.dedent(IPC_HIDDEN_CHILD)], env={**env, "RANK_ID": str(r)},
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(W)]
+    outs, errs = [], []
+    try:
+        for p in ps:
+            o, e = p.communicate(timeout=120)
+            assert p.returncode == 0, e[-2000:]
+            outs.append(json.loads(o.strip().splitlines()[-1]))
+            errs.append(e)
+    finally:
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert all(o["rcs"] == [0, 0, 0] and o["ok"] and o["finalize"] == 0 for o in outs), outs
+    assert "liveness check off for this communicator" in errs[0], errs[0][-2000:]
+    assert "liveness check off" not in errs[1], errs[1][-2000:]
