@@ -123,7 +123,7 @@ SEED = 0xDCC1
 PAIR_GAP = 4096  # bytes between the end of recv and the start of send in the pooled layout
 
 
-def operand_pair(n: int, dt: int, op: int, buffer_id: int, device, layout: str):
+def operand_pair(n: int, dt: int, op: int, buffer_id: int, device, layout: str, keep: list | None = None):
     """(send, recv) synthetic operands.  "pooled": both carved from ONE HBM allocation, recv first
     and send PAIR_GAP bytes past its end; "separate": two allocations (DCCL's own shape: scratchpad
     + user chunk).  Separately allocated 1 GiB operands land in one of two physical placement modes
@@ -137,6 +137,8 @@ def operand_pair(n: int, dt: int, op: int, buffer_id: int, device, layout: str):
         pool = torch.empty(2 * nbytes + PAIR_GAP, dtype=torch.uint8, device=device)
         recv = pool[:nbytes].view(tdt)
         send = pool[nbytes + PAIR_GAP:].view(tdt)
+        if keep is not None:  # the caller keeps the allocation for later legs (C3)
+            keep.append(pool)
     synth_into(send, n, dt, op, buffer_id)
     synth_into(recv, n, dt, op, buffer_id + 1)
     return send, recv
@@ -393,12 +395,15 @@ def host_staged_rate(nbytes: int, dt: int, op: int) -> dict:
             "bytes_per_operand": nbytes, "note": "pinned host operands; PCIe H2D 2N + D2H N bytes"}
 
 
-def config_c3(dev, stream, nbytes: int = 1 << 30, launches: int = 10) -> list:
+def config_c3(dev, stream, nbytes: int = 1 << 30, launches: int = 20, pool: torch.Tensor | None = None) -> list:
     """BASELINE config C3: every ncclRedOp_t x {fp16, bf16, fp32, int32, int64} on 1 GiB operands (pooled
     layout), each timed over `launches` back-to-back launches (HIP events on the launch stream) and its
-    result checked by verify_sample (3 + launches applications)."""
+    result checked by verify_sample (3 + launches applications).  `pool`: the headline's own allocation
+    (recv, then send PAIR_GAP bytes past it), so every dtype and op runs on the same buffers as the headline;
+    a re-allocated pool lands in another physical placement and runs ~1 point slower."""
     out = []
-    pool = torch.empty(2 * nbytes + PAIR_GAP, dtype=torch.uint8, device=dev)
+    if pool is None or pool.numel() < 2 * nbytes + PAIR_GAP:
+        pool = torch.empty(2 * nbytes + PAIR_GAP, dtype=torch.uint8, device=dev)
     names = {6: "f16", 9: "bf16", 7: "f32", 2: "i32", 4: "i64"}
     for dt in (6, 9, 7, 2, 4):
         esz = dccl_amd.size_of_type(dt)
@@ -1088,7 +1093,8 @@ def run_rank(a):
     nbytes = n * esz
 
     progress(f"world {world}, backend {backend}, {nbytes >> 20} MiB per operand on {dev}")
-    send, recv = operand_pair(n, dt, op, 2 * rank, dev, a.layout)
+    headline_pool = []
+    send, recv = operand_pair(n, dt, op, 2 * rank, dev, a.layout, keep=headline_pool)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     ps, pr = send.data_ptr(), recv.data_ptr()
@@ -1160,6 +1166,9 @@ def run_rank(a):
                                       "(every GPU ends with the full result); not in value"}
         del gathered, src
         progress(f"all-gather done: {tag * 1e3:.3f} ms")
+    # the headline's pooled allocation is kept for C3 (same buffers, every dtype and op; N = 1 only)
+    c3_pool = headline_pool[0] if (world == 1 and headline_pool and nbytes == 1 << 30 and not a.no_configs) else None
+    headline_pool.clear()
     # the other operand layout, timed briefly on every rank (reported, never in `value`)
     del send, recv
     send = recv = None
@@ -1215,7 +1224,8 @@ def run_rank(a):
             progress("C4: size sweep 4 KiB - 4 GiB")
             res["c4"] = config_c4(dev, stream)
             progress("C3: ops x dtypes at 1 GiB")
-            res["c3"] = config_c3(dev, stream)
+            res["c3"] = config_c3(dev, stream, pool=c3_pool)
+            c3_pool = None
             progress("ring step: scratchpad + user chunk, 512 MiB - 8 MiB")
             extra["ring_step"] = ring_step(dev, stream)
         if world == 1 and not a.no_host_staged:
