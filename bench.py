@@ -680,6 +680,7 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
                                  "backend": dist.get_backend(),
                                  "note": "the torch.distributed backend's own all_reduce (RCCL when the backend is "
                                          "nccl), informational: its combine is the backend's"}
+        out["sweep_busbw_gb_s"] = allreduce_sweep(comms, algo_env, world, rank, dev, st, iters)
         if rank == 0:
             progress("child: all_gather of every transport")
         out["dccl_allgather"] = allgather_compare({k: v for k, v in comms.items() if k != "grouped"}, world, rank,
@@ -700,6 +701,45 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
         every = [None] * world
         dist.all_gather_object(every, dccl_amd.ipc_stats())
         out["ipc_stats"] = {k: sum(d[k] for d in every) for k in every[0]}
+    return out
+
+
+def allreduce_sweep(comms: dict, algo_env: dict, world: int, rank: int, dev, st, iters: int) -> dict:
+    """fp32 Sum all-reduce bus bandwidth (GB/s, 2 (W-1)/W x bytes / time) per size for every namespace-dccl
+    algorithm and the torch.distributed backend's own all_reduce, timing only (the 256 MiB collective above is
+    the checked one): the data the first xGMI run decides the RCCL default by, per size.
+    Sizes from DCCL_BENCH_AR_SWEEP_MIB (the parent passes 1,16,64,256; 1,4 in a socket rehearsal)."""
+    sizes = [int(x) for x in os.environ.get("DCCL_BENCH_AR_SWEEP_MIB", "1,16,64,256").split(",") if x.strip()]
+    out = {}
+    for mib in sizes:
+        cnt = (mib << 20) // 4 // world * world
+        if cnt == 0:
+            continue
+        if rank == 0:
+            progress(f"child: all_reduce sweep, {mib} MiB")
+        buf = torch.rand(cnt, device=dev)
+        row = {}
+
+        def timed(call):
+            call()  # warm (first use of a size may map or grow a scratch)
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                call()
+            torch.cuda.synchronize(dev)
+            return (time.perf_counter() - t0) / iters
+
+        for name, comm in comms.items():
+            os.environ["DCCL_ALLREDUCE_ALGORITHM"] = algo_env[name]
+            t = timed(lambda: dccl_amd.check(comm.all_reduce(buf.data_ptr(), buf.data_ptr(), cnt, 7, 0,
+                                                             st.cuda_stream), name))
+            row[name] = round(2 * (world - 1) / world * cnt * 4 / t / 1e9, 1)
+        os.environ["DCCL_ALLREDUCE_ALGORITHM"] = "auto"
+        t = timed(lambda: dist.all_reduce(buf))
+        row["rccl"] = round(2 * (world - 1) / world * cnt * 4 / t / 1e9, 1)
+        out[str(mib)] = row
+        del buf
     return out
 
 
@@ -901,6 +941,7 @@ def collective_in_child(world: int, rank: int, local: int, backend: str, c5_gib:
            "DCCL_BOOTSTRAP_TAG": f"bench_child_{port[0]}",
            "DCCL_BENCH_C5_GIB": str(min(c5_gib, REHEARSAL_C5_GIB) if rehearsal else c5_gib),
            "DCCL_BENCH_AR_MIB": str(REHEARSAL_AR_MIB if rehearsal else 256),
+           "DCCL_BENCH_AR_SWEEP_MIB": "1,4" if rehearsal else "1,16,64,256",
            "DCCL_BENCH_CHILD_TIMEOUT_S": str(timeout)}
     torch.cuda.synchronize()
     progress(f"namespace-dccl all_reduce extras in a child process (port {port[0]}"
@@ -1046,6 +1087,8 @@ def allreduce_summary(ar) -> dict:
                                                   "broadcast_ms", "reduce_bit_exact", "reduce_ms") if k in ar[name]}
     if isinstance(ar.get("rccl_allreduce"), dict):
         out["rccl"] = {k: ar["rccl_allreduce"][k] for k in ("ms", "busbw_gb_s")}
+    if isinstance(ar.get("sweep_busbw_gb_s"), dict):
+        out["sweep_busbw_gb_s"] = ar["sweep_busbw_gb_s"]
     for key in ("dccl_allgather", "c5_allgather"):
         ag = ar.get(key)
         if isinstance(ag, dict):

@@ -136,6 +136,10 @@ def test_bench_rccl_two_ranks_one_gpu():
     # the grouped RCCL all-reduce and the IPC transport's counters
     assert s["fp32_grouped_bit_exact_vs_ring"] and s["grouped"]["int32_sum_bit_exact_vs_rccl"], s
     assert s["ipc_stats"]["alias_errors"] == 0 and s["ipc_stats"]["scratch_copies"] > 0, s
+    # the per-size all-reduce sweep (socket rehearsal: 1 and 4 MiB), every algorithm and RCCL's own
+    assert set(s["sweep_busbw_gb_s"]) == {"1", "4"}, s
+    assert all(set(r) == {"ring", "grouped", "direct", "rccl"} and min(r.values()) > 0
+               for r in s["sweep_busbw_gb_s"].values()), s
     assert s["dccl_allgather"]["direct"]["wrong_slices_all_ranks"] == 0, s
 
 

@@ -76,13 +76,14 @@ def test_allreduce_summary_keeps_the_flags():
     ar = {"count": 8, "ring": {"int32_sum_bit_exact_vs_rccl": True, "fp32_within_bound": True, "ms": 1.0,
                                "busbw_gb_s": 2.0, "fp32_max_abs_diff_vs_rccl": 0.0},
           "rccl_allreduce": {"ms": 1.5, "busbw_gb_s": 1.0, "backend": "nccl"},
-          "fp32_direct_bit_exact_vs_ring": True,
+          "fp32_direct_bit_exact_vs_ring": True, "sweep_busbw_gb_s": {"1": {"ring": 1.0, "rccl": 2.0}},
           "dccl_allgather": {"bytes_per_rank": 4, "direct": {"bit_exact": True, "ms": 0.1, "ms_each": [0.1],
                                                               "busbw_gb_s": 3.0}}}
     s = bench.allreduce_summary(ar)
     assert s["ring"] == {"int32_sum_bit_exact_vs_rccl": True, "fp32_within_bound": True, "ms": 1.0, "busbw_gb_s": 2.0}
     assert s["rccl"] == {"ms": 1.5, "busbw_gb_s": 1.0} and s["fp32_direct_bit_exact_vs_ring"]
     assert s["dccl_allgather"] == {"direct": {"bit_exact": True, "ms": 0.1, "busbw_gb_s": 3.0}}
+    assert s["sweep_busbw_gb_s"] == {"1": {"ring": 1.0, "rccl": 2.0}}
     assert bench.allreduce_summary({"error": "x"}) == {"error": "x"}
 
 
