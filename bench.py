@@ -734,10 +734,10 @@ def allreduce_sweep(comms: dict, algo_env: dict, world: int, rank: int, dev, st,
             os.environ["DCCL_ALLREDUCE_ALGORITHM"] = algo_env[name]
             t = timed(lambda: dccl_amd.check(comm.all_reduce(buf.data_ptr(), buf.data_ptr(), cnt, 7, 0,
                                                              st.cuda_stream), name))
-            row[name] = round(2 * (world - 1) / world * cnt * 4 / t / 1e9, 1)
+            row[name] = float(f"{2 * (world - 1) / world * cnt * 4 / t / 1e9:.3g}")
         os.environ["DCCL_ALLREDUCE_ALGORITHM"] = "auto"
         t = timed(lambda: dist.all_reduce(buf))
-        row["rccl"] = round(2 * (world - 1) / world * cnt * 4 / t / 1e9, 1)
+        row["rccl"] = float(f"{2 * (world - 1) / world * cnt * 4 / t / 1e9:.3g}")
         out[str(mib)] = row
         del buf
     return out
