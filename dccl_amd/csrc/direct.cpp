@@ -42,7 +42,7 @@ constexpr size_t kMaxOpenMappings = 256;
 constexpr size_t kMaxOpenBytes = size_t(64) << 30;
 // Exports this rank ended and its peers have not necessarily seen yet (see ShmSlot::retired).
 constexpr uint32_t kRetireRing = 256;
-// The communicator's scratch (unregistered inputs are copied there for the peers to read): at least the
+// The communicator's scratch (every input is copied there for the peers to read): at least the
 // reference's initial scratchpad (SCRATCHPAD_INI_SIZE, /root/reference/src/core/dccl.cpp:57), in 2 MiB
 // pages, grown by at least half when it grows.
 constexpr size_t kScratchMin = size_t(64) << 20;
@@ -55,14 +55,14 @@ constexpr size_t kScratchHeader = 256;
 struct Desc {
     unsigned char handle[kHandleBytes];
     uint64_t serial, off, size;  // size: of the exported allocation
-    uint64_t token[2];           // a scratch's token at its first bytes (0, 0: none, a registered buffer)
+    uint64_t token[2];           // the scratch's token at its first bytes (never 0, 0)
 };
 
 struct ShmSlot {
     Desc in, out;
     int64_t pid;     // this rank's process and its start time (bootstrap.hpp), for the barrier's liveness check
     uint64_t start;
-    // Exports this rank's process ended (deregistered, replaced scratch, freed allocations): serials in a
+    // Exports this rank's process ended (replaced scratch, finalized communicator): serials in a
     // ring, retired_n written last.  Every peer closes their mappings before it opens anything new.
     std::atomic<uint64_t> retired_n;
     uint64_t retired[kRetireRing];
@@ -100,7 +100,7 @@ struct IpcXport {
     uint32_t rank = 0, world = 0;
     double timeout_s = 0;  // 0: no limit (a dead peer is caught by the liveness check)
     bool liveness = true;   // peers' pids are visible here (checked at join)
-    // scratch: inputs that are not registered are copied here (one allocation, exported once)
+    // scratch: every input is copied here (one allocation, exported once)
     void* scratch = nullptr;        // allocation base: header (token), then scratch_bytes of data
     size_t scratch_bytes = 0;
     uint64_t token[2] = {0, 0};
@@ -844,8 +844,8 @@ bool direct_selected(const dcclComm* c) {
 
 // ncclAllReduce: the ring all-reduce (all_reduce_ring.cpp:8-79) leaves chunk r+1 reduced on rank r;
 // here rank r reduces that chunk from every rank's input in the ring's order, then pulls every other
-// chunk from the rank that reduced it.  On the IPC transport an unregistered `send` is read from the
-// scratch copy, and an unregistered `recv` is replaced by the scratch for the reduced chunk (reduced in
+// chunk from the rank that reduced it.  On the IPC transport `send` is read from the scratch copy, and
+// `recv` is replaced by the scratch for the reduced chunk (reduced in
 // place there: no other rank reads that chunk of anyone's input), which this rank then copies out.
 ncclResult_t direct_all_reduce(dcclComm* c, const void* send, void* recv, size_t count, int dtype, int op,
                                hipStream_t st) {

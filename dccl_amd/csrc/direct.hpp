@@ -13,12 +13,11 @@
 //
 // Two ways to see peer buffers:
 //   * in-process ranks (threads; comm.hpp): pointers are published through the Group;
-//   * the IPC transport (DCCL_TRANSPORT=ipc; one process per GPU): registered device memory
-//     (dcclRegisterCacheMemory) and each communicator's scratch are exported with hipIpcGetMemHandle
-//     (dmabuf) under serials the exporter never reuses, published in a POSIX shared-memory segment and
-//     opened once by each peer; an export ends only by a retirement written into that segment
-//     (ipc_cache.hpp).  Unregistered inputs are copied into the scratch.  Barriers spin on counters in
-//     the same segment and watch the peers' processes.
+//   * the IPC transport (DCCL_TRANSPORT=ipc; one process per GPU): each communicator's scratch is exported
+//     with hipIpcGetMemHandle (dmabuf) under serials the exporter never reuses, published in a POSIX
+//     shared-memory segment and opened once by each peer (its token verified); an export ends only by a
+//     retirement written into that segment (ipc_cache.hpp).  Every input is copied into the scratch.
+//     Barriers spin on counters in the same segment and watch the peers' processes.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -36,8 +35,8 @@ constexpr uint32_t kDirectMaxWorld = 8;  // one 8-GPU node; <= 8 copy pairs / ch
 // file in DCCL_BOOTSTRAP_DIR keyed by DCCL_BOOTSTRAP_TAG / MASTER_PORT) and leave.
 ncclResult_t ipc_join(dccl::dcclComm* c, uint32_t world, uint32_t rank);
 ncclResult_t ipc_leave(dccl::dcclComm* c);
-// dcclRegisterCacheMemory / dcclDeregisterCacheMemory of device memory on an IPC communicator: peers read a
-// registered range in place; any other buffer is copied into the communicator's scratch for them.
+// dcclRegisterCacheMemory / dcclDeregisterCacheMemory of device memory on an IPC communicator: validated and
+// tracked only (peers read every input through the communicator's scratch).
 ncclResult_t ipc_register(void* buffer, size_t size);
 ncclResult_t ipc_deregister(void* buffer);
 // The process's IPC counters (dccl_ipc_stats, include/dccl/dccl_comm.h): fills min(n, count) of them and
