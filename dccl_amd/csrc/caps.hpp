@@ -1,17 +1,11 @@
-// dccl_amd/csrc/caps.hpp — resident-wave caps of every capped combine launch, in one table, and the functions
-// that select them.  Pure host C++ (no HIP): tests/test_caps.py compiles it with g++ and checks every entry;
-// the static_asserts below check the table at every build.
-//
-// Why caps.  Every combine kernel is a one-wave (64-thread) block streaming 16-B vectors.  A CU holds up to
-// 32 such blocks; with k + 1 loads per lane in flight each, too many bytes are outstanding and the DRAM serves
-// the streams worse.  A launch asks for `bytes` of (unused) dynamic LDS per block, so a CU holds
-// floor(160 KiB / bytes) of them (lds_for_waves).  The values are NOMINAL wave counts: the 256-B rounding of
-// the LDS request makes some neighbours the same occupancy (8 and 9, 16 and 18).
-//
-// Rule for an entry: it stays only if it leads the simpler choice by >= 2 points (two boxes).
-// Round 5 removed the straddle size bands and the separate-allocation pair cap with its per-launch pointer
-// queries (+0.5..+2 points in narrow bands), and reset every size-row cell that did not lead the 1 GiB row by
-// 2 points (tools/ab_cases.py, profiles/r5_ab_caps.json).
+// dccl_amd/csrc/caps.hpp — resident-wave caps of every capped combine launch and the functions that select them.
+// Host-only C++: tests/test_caps.py compiles it with g++ and freezes every entry; table_ok() checks it at build.
+// Every combine kernel is a one-wave block streaming 16-B vectors; with k + 1 loads per lane in flight, too many
+// resident waves put too many bytes in flight for the DRAM.  A launch asks for `bytes` of unused dynamic LDS per
+// block, so a CU holds floor(160 KiB / bytes) of them; values are NOMINAL wave counts (the 256-B rounding makes
+// 8 and 9, 16 and 18 the same occupancy).  An entry stays only if it leads the simpler choice by >= 2 points on
+// two boxes (round 5 removed the straddle bands, the separate-allocation pair cap and every size-row
+// cell below that bar: tools/ab_cases.py, profiles/r5_ab_caps.json).
 #pragma once
 
 #include <cstddef>
@@ -34,17 +28,16 @@ inline constexpr int kUncapped = 32;  // 32 one-wave blocks per CU: the hardware
 inline constexpr size_t kLdsPerCu = size_t(160) << 10;
 inline constexpr size_t kMaxLdsPerBlock = size_t(64) << 10;
 
-// Size class by bytes per operand: 0, 1, 2 below 24, 48, 96 MiB; 3 (the 1 GiB row) above.  A smaller launch
-// has few tiles per resident wave and its tail dominates, so more waves win.
+// Size class by bytes per operand: 0, 1, 2 below 24, 48, 96 MiB; 3 (the 1 GiB row) above (small launches: few
+// tiles per resident wave, the tail dominates, more waves win).
 inline constexpr int kSizeClasses = 4;
 constexpr int size_class(size_t bytes) {
     return bytes < (size_t(24) << 20) ? 0 : bytes < (size_t(48) << 20) ? 1 : bytes < (size_t(96) << 20) ? 2 : 3;
 }
 
-// kWaves[kernel][size class][k]: nominal resident waves per CU (32 = uncapped; 0 = not used at that k; for the
-// phased classes 0 = the per-operand form).  The 1 GiB row is the best cap of sweeps at 1 GiB fp32 Sum (rounds
-// 1-3).  A smaller class keeps its own value only where it led the 1 GiB value by >= 2 points at 16 / 32 / 64
-// MiB (round-2 sweeps, confirmed by round 5's A/B of the 1 GiB row everywhere, profiles/r5_ab_caps.json).
+// kWaves[kernel][size class][k]: nominal resident waves per CU (32 = uncapped; 0 = not used at that k, or for
+// the phased classes the per-operand form).  1 GiB row: the best caps of rounds 1-3's sweeps; a smaller class
+// keeps its own value only where it led the 1 GiB value by >= 2 points (profiles/r5_ab_caps.json).
 inline constexpr unsigned char kWaves[kNumKernels][kSizeClasses][9] = {
     // k:  0  1   2   3   4   5   6   7   8
     {{0, 0, 32, 24, 16, 16, 16, 10, 9},  // kMulti            < 24 MiB
@@ -73,10 +66,8 @@ inline constexpr unsigned char kWaves[kNumKernels][kSizeClasses][9] = {
      {0, 0, 0, 16, 13, 13, 0, 13, 11}},
 };
 
-// kRun[kernel][k]: the tile-run order (reduce_kernels.hpp run_tile<RUN>: each XCD walks RUN consecutive tiles
-// of every group of 8 RUN blocks; 1 = block order).  Runs of 4 keep the line two neighbouring tiles share (lane
-// 63's extra load of an off-phase operand, a straddling source's partial line) in one L2 in 3 of 4 cases
-// (+2.0..+3.7 points on two boxes, r3_s10..s12).
+// kRun[kernel][k]: tile-run order (run_tile<RUN>: each XCD walks RUN consecutive tiles; 1 = block order).  Runs
+// of 4 keep the line two neighbouring tiles share in one L2 in 3 of 4 cases (+2.0..+3.7 points, round 3).
 inline constexpr unsigned char kRun[kNumKernels][9] = {
     {1, 1, 1, 1, 1, 1, 1, 1, 1},  // kMulti
     {1, 1, 1, 1, 1, 1, 1, 1, 1},  // kChain
@@ -104,12 +95,10 @@ constexpr bool phased_loads_first(bool chain, int k) {
     return waves(chain ? kChainPhasedFirst : kMultiPhasedFirst, k, size_t(1) << 30) > 0;
 }
 
-// ---- reduce_windows_kernel (k-way / chain into a destination read and written at its own 16-B phase) ----
-// From kWindowTunedBytes per operand the per-operand tile under 26 waves (sources in phase, k >= 3: +2.1..+3.5
-// points) or, sources off phase, the loads-first tile under 12-14 waves (k = 4..8: +0.5..+5.3; k = 3 per-operand,
-// 26: +1.9..+3.7) (DESIGN.md §3.4, 1 GiB fp32 Sum, three boxes, r4_s11..s13, r4_s17/s18).  From kWindowMidBytes,
-// sources off phase: one mid-size form, +3..+7 points over the phased kernels at 64 MiB (r4_s26..s28,
-// r5_ab_caps.json).  Every other launch: the per-operand tile, uncapped.
+// ---- reduce_windows_kernel (k-way / chain into a destination at its own 16-B phase) ----
+// From kWindowTunedBytes: per-operand tile under 26 waves (sources in phase, +2.1..+3.5 points) or, sources off
+// phase, the loads-first tile under 12-14 waves (+0.5..+5.3; k = 3 per-operand, 26).  From kWindowMidBytes with
+// sources off phase one mid-size form (+3..+7 over the phased kernels at 64 MiB).  Else per-operand, uncapped.
 inline constexpr size_t kWindowTunedBytes = size_t(96) << 20;
 inline constexpr size_t kWindowMidBytes = size_t(48) << 20;
 enum WindowClass : int { kWinInPhase = 0, kWinOffPhase, kNumWindowClasses };
@@ -129,8 +118,8 @@ constexpr bool window_mid(bool chain, int k, size_t bytes) {
     return k >= (chain ? 3 : 4) && k <= 8 && bytes >= kWindowMidBytes && bytes < kWindowTunedBytes;
 }
 // Element-aligned destinations with sources at other phases take reduce_windows_kernel instead of the phased
-// kernels where it led by >= 2 points on two boxes: from kWindowTunedBytes k-way k = 3..5, chain k = 4..7; in
-// the mid-size range with the destination 16-B aligned.
+// kernels where it led by >= 2 points: from kWindowTunedBytes at k-way k = 3..5, chain k = 4..7; mid-size with
+// the destination 16-B aligned.
 constexpr bool phased_via_windows(bool chain, int k, size_t bytes, bool dst16) {
     if (bytes >= kWindowTunedBytes) return k >= (chain ? 4 : 3) && k <= (chain ? 7 : 5);
     return dst16 && window_mid(chain, k, bytes);
@@ -153,15 +142,10 @@ constexpr bool table_ok() {
                 if (run != 1 && run != 2 && run != 4 && run != 8) return false;  // run_tile's groups
                 if (run != 1 && phased && w == 0) return false;                  // a run only for the loads-first form
             }
-    for (int c = 0; c < kNumWindowClasses; ++c)
-        for (int k = 0; k <= 8; ++k) {
-            const WindowForm f = kWindow[c][k];
-            if (f.order > 3 || f.first > 1 || f.waves < 7 || f.waves > kUncapped) return false;
-            if (f.first && f.waves == kUncapped) return false;  // the loads-first tile only under a cap
-            if (lds_for_waves(f.waves) > kMaxLdsPerBlock) return false;
-        }
-    for (int k = 3; k <= 7; ++k)  // the phased launches routed to the windows kernel take a tuned off-phase form
-        if (kWindow[kWinOffPhase][k].waves == kUncapped) return false;
+    for (const auto& row : kWindow)
+        for (const WindowForm& f : row)  // legal orders and caps; the loads-first tile only under a cap
+            if (f.order > 3 || f.first > 1 || f.waves < 7 || f.waves > kUncapped || (f.first && f.waves == kUncapped))
+                return false;
     return true;
 }
 static_assert(table_ok(), "every cap is a legal LDS request; runs and loads-first tiles only where capped");
