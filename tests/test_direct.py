@@ -549,3 +549,50 @@ def test_ipc_dead_peer_ends_wait(gpu):
     rc, dt, fin = results[0]
     assert rc in (2, 6), rc  # ncclRemoteError (or ncclSystemError)
     assert dt < 10.0, dt
+
+
+IPC_REGISTER_CHILD = r"""
+import json, os
+import torch
+import dccl_amd
+torch.cuda.set_device(0)
+comm = dccl_amd.Comm.ipc(1, 0)
+x = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
+p, out = x.data_ptr(), {}
+out["reg"] = comm.register(p, 1 << 20)
+out["reg_again"] = comm.register(p, 1 << 20)            # the same start again: counted
+out["past_end"] = comm.register(p, 1 << 40)              # past its allocation (torch's segment included)
+out["dereg"] = [comm.deregister(p), comm.deregister(p), comm.deregister(p)]  # twice, then unknown
+out["dereg_unknown"] = comm.deregister(p + 64)
+out["unaligned"] = comm.register(p + 1, 64)
+y = torch.full((1024,), 2.0, device="cuda")
+out["all_reduce"] = comm.all_reduce(y.data_ptr(), y.data_ptr(), 1024, 7, 0, 0)
+torch.cuda.synchronize()
+out["value_ok"] = bool(torch.all(y == 2.0))
+stats = dccl_amd.ipc_stats()
+out["exports_made"] = stats["exports_made"]
+out["registered_hits"] = stats["registered_hits"]
+out["finalize"] = comm.finalize()
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.gpu
+def test_ipc_registration_is_track_only(gpu, tmp_path):
+    """dcclRegisterCacheMemory of device memory on an IPC communicator (round 5): validated (a device allocation
+    of this process, the range inside it, 64-B aligned) and counted per start address, nothing exported;
+    deregistering an unknown start is ncclInvalidArgument (4)."""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {**os.environ, "PYTHONPATH": root, "DCCL_BOOTSTRAP_DIR": str(tmp_path),
+           "DCCL_BOOTSTRAP_TAG": "ipcreg_" + uuid.uuid4().hex[:10]}
+    p = subprocess.run([sys.executable, "-c", IPC_REGISTER_CHILD], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["reg"] == 0 and out["reg_again"] == 0 and out["past_end"] == 4, out
+    assert out["dereg"] == [0, 0, 4] and out["dereg_unknown"] == 4 and out["unaligned"] == 4, out
+    assert out["all_reduce"] == 0 and out["value_ok"] and out["finalize"] == 0, out
+    # registration exported nothing (and W = 1 runs no peer-read collective, so no scratch was exported either)
+    assert out["exports_made"] == 0 and out["registered_hits"] == 0, out
