@@ -258,7 +258,7 @@ def cpu_baseline(budget_s: float, nbytes: int) -> dict | None:
     n = nbytes // 4
     affinity = len(os.sched_getaffinity(0))
     quota = cgroup_cpu_quota()
-    granted = max(1, min(affinity, int(quota))) if quota else affinity
+    granted = granted_cpus()
 
     def slices(nthr):
         per = (n // nthr) // 16 * 16
@@ -377,22 +377,116 @@ def measured_traffic(nbytes: int, dt: int, op: int, launches: int = 5) -> dict:
                    "read = 2 x FETCH_SIZE x 1024 (gfx950 halving), write = WRITE_SIZE x 1024"}
 
 
-def host_staged_rate(nbytes: int, dt: int, op: int) -> dict:
-    """Operands in pinned host memory (Derecho's RDMA buffers): H2D + combine + D2H, pipelined."""
-    n = nbytes // dccl_amd.size_of_type(dt)
-    s = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-    r = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-    s.view(torch.float32).uniform_(-1, 1) if dt == 7 else s.random_()
-    r.zero_()
-    rc = dccl_amd.local_reduce_host(s.data_ptr(), r.data_ptr(), dt, n, op)
-    dccl_amd.check(rc, "dccl_local_reduce_host")
+HOST_SIZES = [4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30]
+HOST_ROTATE_BYTES = 256 << 20  # per operand: operand pairs rotated over this much memory, so no call finds its
+#                                operands in a cache (the L3 is 32 MiB per CCD), as a chunk that just arrived by RDMA
+
+
+def granted_cpus() -> int:
+    """CPUs this process may use: the cgroup quota (16 on the GPU box) capped by the affinity mask."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    return max(1, min(affinity, int(quota))) if quota else affinity
+
+
+def _gpu_host_us(ps: int, pr: int, n: int, nsets: int, stride: int, dt: int, op: int, min_s: float) -> tuple:
+    """Microseconds per dccl_local_reduce_host call (synchronous: staging, PCIe both ways, the combine), the
+    operand pairs rotated as in the CPU legs; the loop is Python over the ctypes entry point (its own cost,
+    well under a microsecond per call, is included)."""
+    f = dccl_amd.lib.dccl_local_reduce_host
+    for k in range(min(nsets, 3)):
+        dccl_amd.check(f(ps + k * stride, pr + k * stride, dt, n, op), "dccl_local_reduce_host")
     reps, t0 = 0, time.perf_counter()
-    while reps < 3 or time.perf_counter() - t0 < 1.0:
-        dccl_amd.check(dccl_amd.local_reduce_host(s.data_ptr(), r.data_ptr(), dt, n, op), "host")
+    while True:
+        k = reps % nsets
+        rc = f(ps + k * stride, pr + k * stride, dt, n, op)
+        if rc:
+            raise dccl_amd.DcclError(rc, "dccl_local_reduce_host")
         reps += 1
-    t = (time.perf_counter() - t0) / reps
-    return {"payload_gib_s": round(nbytes / t / GIB, 2), "ms": round(t * 1e3, 3),
-            "bytes_per_operand": nbytes, "note": "pinned host operands; PCIe H2D 2N + D2H N bytes"}
+        if reps >= 3 and (reps & 7 == 0 or n >= 1 << 18):
+            el = time.perf_counter() - t0
+            if el >= min_s:
+                return el / reps * 1e6, reps
+
+
+def host_crossover(dt: int = 7, op: int = 0, min_s: float = 0.25) -> dict:
+    """Where the host-resident GPU path pays.  For each payload size 4 KiB - 1 GiB, on
+    page-locked and on pageable host operands, on the SAME buffers: dccl_local_reduce_host (the product: H2D,
+    combine, D2H) against the oracle restatement of the reference's loop do_host_reduce
+    (internal_common.hpp:496-586, oracle/host_reduce.c, Release flags; timed in C by oracle/cpu_timing.c) on
+    1 core, as the reference runs it (one thread per rank), and on every core this process is granted.
+    Operand pairs rotate over HOST_ROTATE_BYTES so every call starts cold; `cpu1_hot_us` repeats one pair
+    (cache-resident up to tens of MiB) as the CPU's best case.  Every size's GPU result is checked bit for bit
+    against the oracle on the same inputs.  `crossover` = the smallest size from which the GPU path is faster
+    at that size and every larger one (null: never).  The oracle is the CPU baseline here, never the product."""
+    import oracle  # test infrastructure: the CPU baseline legs only
+    cores = granted_cpus()
+    esz = dccl_amd.size_of_type(dt)
+    top = HOST_SIZES[-1]
+    pin_s = torch.empty(top, dtype=torch.uint8).pin_memory()
+    pin_r = torch.empty(top, dtype=torch.uint8).pin_memory()
+    pin_s.view(torch.float32).uniform_(-1, 1)
+    pin_r.view(torch.float32).uniform_(-1, 1)
+    pag_s = oracle.aligned_empty(top, np.uint8, align=4096)
+    pag_r = oracle.aligned_empty(top, np.uint8, align=4096)
+    np.copyto(pag_s, pin_s.numpy())
+    np.copyto(pag_r, pin_r.numpy())
+    bufs = {"pinned": (pin_s.numpy(), pin_r.numpy()), "pageable": (pag_s, pag_r)}
+    npd = oracle.NP_DTYPES[dt]
+    rows = []
+    for size in HOST_SIZES:
+        n = size // esz
+        nsets = max(1, min(HOST_ROTATE_BYTES, top) // size)
+        row = {"bytes": size, "operand_pairs_rotated": nsets}
+        for kind, (s, r) in bufs.items():
+            ps, pr = s.ctypes.data, r.ctypes.data
+            want = r[:size].view(npd).copy()  # pair 0, checked bit for bit against the oracle
+            dccl_amd.check(dccl_amd.local_reduce_host(ps, pr, dt, n, op), "dccl_local_reduce_host")
+            oracle.expected_reduce(s[:size].view(npd), want, dt, op)
+            exact = r[:size].tobytes() == want.tobytes()
+            del want
+            gpu_us, gpu_reps = _gpu_host_us(ps, pr, n, nsets, size, dt, op, min_s)
+            c1, _ = oracle.time_host_reduce(ps, pr, n, dt, op, 1, nsets, size, min_s)
+            cn, _ = oracle.time_host_reduce(ps, pr, n, dt, op, cores, nsets, size, min_s)
+            rec = {"gpu_us": round(gpu_us, 2), "cpu1_us": round(c1 * 1e6, 2), "cpu_all_us": round(cn * 1e6, 2),
+                   "gpu_payload_gib_s": round(size / (gpu_us * 1e-6) / GIB, 2), "bit_exact": exact,
+                   "gpu_calls": gpu_reps}
+            if kind == "pinned" and size <= 64 << 20:
+                ch, _ = oracle.time_host_reduce(ps, pr, n, dt, op, 1, 1, 0, min_s)
+                rec["cpu1_hot_us"] = round(ch * 1e6, 2)
+            row[kind] = rec
+        rows.append(row)
+        progress(f"host crossover {size >> 10} KiB: pinned GPU {row['pinned']['gpu_us']} us, "
+                 f"CPU 1 core {row['pinned']['cpu1_us']} us, {cores} cores {row['pinned']['cpu_all_us']} us")
+    kinds = list(bufs)
+    del pin_s, pin_r, pag_s, pag_r, bufs
+
+    def crossover(kind, key):
+        win = None
+        for row in reversed(rows):
+            if key not in row[kind] or not row[kind]["gpu_us"] < row[kind][key]:
+                break
+            win = row["bytes"]
+        return win
+
+    f, reps, t0 = dccl_amd.lib.dccl_size_of_type, 0, time.perf_counter()
+    while reps < 200000:  # the Python loop's own cost per ctypes call, included in every gpu_us
+        f(dt)
+        reps += 1
+    call_us = (time.perf_counter() - t0) / reps * 1e6
+    return {
+        "python_call_overhead_us": round(call_us, 3),
+        "crossover": {kind: {"vs_1_core": crossover(kind, "cpu1_us"), "vs_1_core_hot": crossover(kind, "cpu1_hot_us"),
+                             f"vs_{cores}_cores": crossover(kind, "cpu_all_us")} for kind in kinds},
+        "cores": cores, "dtype": dt, "op": op,
+        "all_bit_exact": all(row[k]["bit_exact"] for row in rows for k in kinds),
+        "product_default_gpu_min_bytes": dccl_amd.host_reduce_gpu_min_bytes(dt),
+        "rows": rows,
+        "how": "same host buffers for every leg; GPU = dccl_local_reduce_host per call (synchronous); CPU = "
+               "oracle/host_reduce.c (restatement of internal_common.hpp:496-586, -O3 -mprefer-vector-width=512) "
+               "timed in C, 1 thread and `cores` threads (64-B aligned slices, spinning team); pairs rotated over "
+               f"{HOST_ROTATE_BYTES >> 20} MiB per operand (cold), cpu1_hot_us = one pair repeated",
+    }
 
 
 def config_c3(dev, stream, nbytes: int = 1 << 30, launches: int = 20, pool: torch.Tensor | None = None) -> list:
@@ -601,6 +695,19 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
     _native()
     os.environ.setdefault("DCCL_IPC_TIMEOUT_S", "60")
     transports = os.environ.get("DCCL_BENCH_AR_TRANSPORTS", "ring,direct").split(",")
+    # wall seconds per phase: returned as `phase_s`, and rewritten after every phase to
+    # DCCL_BENCH_PHASE_FILE by rank 0, so a child the watchdog kills still says how far it got
+    phases, last = {}, [time.perf_counter()]
+
+    def mark(name):
+        now = time.perf_counter()
+        phases[name] = round(now - last[0], 2)
+        last[0] = now
+        path = os.environ.get("DCCL_BENCH_PHASE_FILE")
+        if path and rank == 0:
+            with open(path, "w") as f:
+                json.dump(phases, f)
+
     uid = None
     if rank == 0 and "ring" in transports:
         try:
@@ -618,7 +725,8 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
     if "direct" in transports:
         comms["direct"] = dccl_amd.Comm.ipc(world, rank)
     algo_env = {"ring": "ring", "grouped": "grouped", "direct": "auto"}
-    out = {"count": count, "world": world, "bytes": count * 4}
+    out = {"count": count, "world": world, "bytes": count * 4, "phase_s": phases}
+    mark("init")
     try:
         st = torch.cuda.current_stream(dev)
         g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -653,6 +761,7 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
                 res.update(root_ops(comm, world, rank, dev, st, xi, ri, iters))
             out[name] = res
             yf_by[name] = yf
+            mark(f"allreduce_{name}")
         # same association order: the first all_reduce of every path must agree with the ring's bit for bit
         if "ring" in yf_by:
             first = {}
@@ -669,6 +778,7 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
                     out[f"fp32_{name}_bit_exact_vs_ring"] = bool(torch.equal(first["ring"].view(torch.int32),
                                                                              first[name].view(torch.int32)))
         os.environ["DCCL_ALLREDUCE_ALGORITHM"] = "auto"
+        mark("bit_exact_vs_ring")
         dist.barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
@@ -680,11 +790,14 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
                                  "backend": dist.get_backend(),
                                  "note": "the torch.distributed backend's own all_reduce (RCCL when the backend is "
                                          "nccl), informational: its combine is the backend's"}
+        mark("rccl_allreduce")
         out["sweep_busbw_gb_s"] = allreduce_sweep(comms, algo_env, world, rank, dev, st, iters)
+        mark("sweep")
         if rank == 0:
             progress("child: all_gather of every transport")
         out["dccl_allgather"] = allgather_compare({k: v for k, v in comms.items() if k != "grouped"}, world, rank,
                                                   dev, st, count, iters)
+        mark("allgather")
         # BASELINE C5's exchange step at its own size (the reduced shards of DCCL_BENCH_C5_GIB GiB of fp32,
         # moved as int32): the direct IPC all-gather beside RCCL's (the single-link ring is left out here)
         c5_gib = float(os.environ.get("DCCL_BENCH_C5_GIB", "0") or 0)
@@ -694,9 +807,11 @@ def dccl_allreduce_multi(world: int, rank: int, dev, count: int, iters: int = 5)
                 progress(f"child: C5's all_gather, {c5_gib:g} GiB")
             torch.cuda.empty_cache()
             out["c5_allgather"] = allgather_compare({"direct": comms["direct"]}, world, rank, dev, st, c5_count, 3)
+            mark("c5_allgather")
     finally:
         for comm in {id(c): c for c in comms.values()}.values():
             comm.finalize()
+    mark("finalize")
     if "direct" in comms:  # the IPC transport's counters, summed over the ranks (alias_errors must be 0)
         every = [None] * world
         dist.all_gather_object(every, dccl_amd.ipc_stats())
@@ -934,6 +1049,8 @@ def collective_in_child(world: int, rank: int, local: int, backend: str, c5_gib:
     # not the launcher's agent store (torchrun exports TORCHELASTIC_USE_AGENT_STORE): the child's rank 0
     # hosts its own store on the fresh port
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    import tempfile
+    phase_file = os.path.join(tempfile.gettempdir(), f"dccl_bench_phases_{os.getpid()}.json")
     rehearsal = socket_rehearsal(world, backend)
     timeout = REHEARSAL_CHILD_TIMEOUT_S if rehearsal else CHILD_TIMEOUT_S
     env = {**env, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port[0]), "RANK": str(rank),
@@ -942,19 +1059,37 @@ def collective_in_child(world: int, rank: int, local: int, backend: str, c5_gib:
            "DCCL_BENCH_C5_GIB": str(min(c5_gib, REHEARSAL_C5_GIB) if rehearsal else c5_gib),
            "DCCL_BENCH_AR_MIB": str(REHEARSAL_AR_MIB if rehearsal else 256),
            "DCCL_BENCH_AR_SWEEP_MIB": "1,4" if rehearsal else "1,16,64,256",
-           "DCCL_BENCH_CHILD_TIMEOUT_S": str(timeout)}
+           "DCCL_BENCH_CHILD_TIMEOUT_S": str(timeout), "DCCL_BENCH_PHASE_FILE": phase_file}
     torch.cuda.synchronize()
     progress(f"namespace-dccl all_reduce extras in a child process (port {port[0]}"
              + (f", socket rehearsal: {REHEARSAL_AR_MIB} MiB all-reduces, timeout {timeout:.0f}s)" if rehearsal else ")"))
     t0 = time.perf_counter()
+
+    def phases_so_far():
+        try:
+            with open(phase_file) as f:
+                return json.load(f)
+        except Exception:
+            return None
+        finally:
+            if os.path.exists(phase_file):
+                os.remove(phase_file)
+
     try:
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--collective-child"], env=env,
                            stdout=subprocess.PIPE, stderr=None, text=True, timeout=timeout)
     except subprocess.TimeoutExpired:
-        return {"error": f"child timed out after {timeout:.0f}s and was killed"}
-    progress(f"child exited with {p.returncode} after {time.perf_counter() - t0:.1f}s")
+        return {"error": f"child timed out after {timeout:.0f}s and was killed", "child_timeout_s": timeout,
+                "phase_s": phases_so_far()}
+    wall = time.perf_counter() - t0
+    progress(f"child exited with {p.returncode} after {wall:.1f}s")
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     res = json.loads(lines[-1]) if lines else {}
+    res.update(child_wall_s=round(wall, 1), child_timeout_s=timeout)
+    if "phase_s" not in res:
+        res["phase_s"] = phases_so_far()
+    else:
+        phases_so_far()  # remove the file
     if p.returncode != 0:
         res = {**res, "error": res.get("error", f"child exited with {p.returncode}")}
     return res
@@ -1079,7 +1214,8 @@ def allreduce_summary(ar) -> dict:
     """The bit-exactness flags and rates of dccl_allreduce (N > 1), small enough for the line's tail."""
     if not isinstance(ar, dict):
         return {"error": repr(ar)}
-    out = {k: ar[k] for k in ("error", "fp32_direct_bit_exact_vs_ring", "fp32_grouped_bit_exact_vs_ring") if k in ar}
+    out = {k: ar[k] for k in ("error", "fp32_direct_bit_exact_vs_ring", "fp32_grouped_bit_exact_vs_ring", "child_wall_s",
+                              "child_timeout_s", "phase_s") if k in ar}
     for name in ("ring", "grouped", "direct"):
         if isinstance(ar.get(name), dict):
             out[name] = {k: ar[name][k] for k in ("int32_sum_bit_exact_vs_rccl", "fp32_within_bound", "ms",
@@ -1209,8 +1345,12 @@ def run_rank(a):
                                       "(every GPU ends with the full result); not in value"}
         del gathered, src
         progress(f"all-gather done: {tag * 1e3:.3f} ms")
-    # the headline's pooled allocation is kept for C3 (same buffers, every dtype and op; N = 1 only)
-    c3_pool = headline_pool[0] if (world == 1 and headline_pool and nbytes == 1 << 30 and not a.no_configs) else None
+    # C3 runs here, on the headline's own pooled allocation (same buffers, every dtype and op; N = 1 only),
+    # before anything else is allocated: the pool is freed before the other-layout and C4 legs
+    c3 = None
+    if world == 1 and headline_pool and nbytes == 1 << 30 and not a.no_configs:
+        progress("C3: ops x dtypes at 1 GiB")
+        c3 = config_c3(dev, stream, pool=headline_pool[0])
     headline_pool.clear()
     # the other operand layout, timed briefly on every rank (reported, never in `value`)
     del send, recv
@@ -1266,13 +1406,25 @@ def run_rank(a):
         if world == 1 and not a.no_configs:
             progress("C4: size sweep 4 KiB - 4 GiB")
             res["c4"] = config_c4(dev, stream)
-            progress("C3: ops x dtypes at 1 GiB")
-            res["c3"] = config_c3(dev, stream, pool=c3_pool)
-            c3_pool = None
+            if c3 is None:
+                progress("C3: ops x dtypes at 1 GiB")
+                c3 = config_c3(dev, stream)
+            res["c3"] = c3
             progress("ring step: scratchpad + user chunk, 512 MiB - 8 MiB")
             extra["ring_step"] = ring_step(dev, stream)
         if world == 1 and not a.no_host_staged:
-            res["host_staged"] = host_staged_rate(nbytes, dt, op)
+            progress("host-resident operands: GPU path vs the CPU loop, 4 KiB - 1 GiB")
+            try:
+                hc = host_crossover()
+            except Exception as e:  # reported, never fatal to the line
+                hc = {"error": repr(e)}
+            top = hc["rows"][-1] if "rows" in hc else {"bytes": None, "pinned": {}, "pageable": {}}
+            res["host_staged"] = {"payload_gib_s": top["pinned"].get("gpu_payload_gib_s"),
+                                  "ms": round(top["pinned"].get("gpu_us", 0) / 1e3, 3), "bytes_per_operand": top["bytes"],
+                                  "pageable_payload_gib_s": top["pageable"].get("gpu_payload_gib_s"),
+                                  "note": "fp32 Sum, pinned host operands; PCIe H2D 2N + D2H N bytes "
+                                          "(the 1 GiB row of host_crossover)"}
+            res["host_crossover"] = hc
         if "allgather" in extra:
             res["allgather"] = extra["allgather"]
         if "dccl_allreduce" in extra:

@@ -96,6 +96,7 @@ def _load():
         "dccl_register_host_memory": (c_int, [c_void_p, c_size_t]),
         "dccl_deregister_host_memory": (c_int, [c_void_p]),
         "dccl_size_of_type": (c_size_t, [c_int]),
+        "dccl_host_reduce_gpu_min_bytes": (c_size_t, [c_int]),
         "dccl_result_string": (ctypes.c_char_p, [c_int]),
         "dccl_version": (c_int, []),
     }
@@ -141,6 +142,7 @@ EXPORTED_SYMBOLS = [
     "dccl_synth_fill", "dccl_synth_fill_range", "dccl_local_reduce_chain", "dccl_copy_multi",
     "dccl_comm_init_ipc", "dccl_reduce", "dccl_broadcast", "dccl_local_reduce_chain_host", "dccl_comm_init_p2p",
     "dccl_bootstrap_done", "dccl_comm_register", "dccl_comm_deregister", "dccl_ipc_stats",
+    "dccl_host_reduce_gpu_min_bytes",
 ]
 
 #: names of the dccl_ipc_stats counters, in order (include/dccl/dccl_comm.h); registered_hits,
@@ -203,6 +205,12 @@ def copy_multi(src_ptrs, dst_ptrs, nbytes: int, stream: int = 0) -> int:
     s = (ctypes.c_void_p * max(1, n))(*src_ptrs)
     d = (ctypes.c_void_p * max(1, n))(*dst_ptrs)
     return int(lib.dccl_copy_multi(s, d, n, int(nbytes), stream or None))
+
+
+def host_reduce_gpu_min_bytes(dtype: int) -> int:
+    """Bytes per operand from which dccl_local_reduce_host beats the reference's one-thread CPU loop (0: the
+    reference has no CPU loop for this dtype); a routing hint for callers that still hold that loop."""
+    return int(lib.dccl_host_reduce_gpu_min_bytes(int(dtype)))
 
 
 def local_reduce_host(send_ptr: int, recv_ptr: int, dtype: int, count: int, op: int) -> int:

@@ -5,9 +5,8 @@ C++ ``namespace dccl`` API (include/dccl/dccl.hpp).  Sources compile in parallel
 link is a plain ``hipcc -shared``.  No fast-math / FTZ flags: the combine must keep
 fp32/fp16 denormals (SURVEY.md §7 "Bit-exact semantics").
 
-Tools-only artefacts, never linked into the product library: the kernel variants under tuning
-(tools/tune/*.hip -> tools/lib/lib<name>.so), the dccl_cli harness and the plain-C ABI check, the PMC
-and native C4 workloads of bench.py (dccl_amd/bin/).
+Tools-only artefacts, never linked into the product library: the dccl_cli harness and the plain-C ABI
+check, the PMC, native C4 and host-crossover workloads of bench.py (dccl_amd/bin/).
 
     python dccl_amd/build.py [--force]      (by path: importing the package loads the library)
 """
@@ -33,8 +32,6 @@ PMC_SRC = os.path.join(ROOT, "tools", "pmc_combine.cpp")
 PMC_BIN = os.path.join(BIN_DIR, "pmc_combine")
 C4_SRC = os.path.join(ROOT, "tools", "c4_native.cpp")
 C4_BIN = os.path.join(BIN_DIR, "c4_native")
-TUNE_DIR = os.path.join(ROOT, "tools", "tune")
-TUNE_LIB_DIR = os.path.join(ROOT, "tools", "lib")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DCCL_OFFLOAD_ARCH", "gfx950")
 
@@ -74,25 +71,13 @@ def build(force: bool = False) -> str:
     if force:
         for f in os.listdir(OBJ_DIR):
             os.remove(os.path.join(OBJ_DIR, f))
-    tune_srcs = sorted(os.path.join(TUNE_DIR, f) for f in os.listdir(TUNE_DIR) if f.endswith(".hip")) \
-        if os.path.isdir(TUNE_DIR) else []
-    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs) + len(tune_srcs))) as ex:
-        tune_objs = [ex.submit(_compile, t) for t in tune_srcs]
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(_compile, srcs))
-        tune_objs = [t.result() for t in tune_objs]
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
         tmp = LIB + ".tmp"
         subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp,
                         "-Wl,-soname,libdccl_amd.so"], check=True)
         os.replace(tmp, LIB)
-    # kernel variants under tuning: one tools library per source, never part of the product library
-    os.makedirs(TUNE_LIB_DIR, exist_ok=True)
-    for src, obj in zip(tune_srcs, tune_objs):
-        name = os.path.splitext(os.path.basename(src))[0]
-        out = os.path.join(TUNE_LIB_DIR, f"lib{name}.so")
-        if force or not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(obj):
-            subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", obj, "-o", out + ".tmp"], check=True)
-            os.replace(out + ".tmp", out)
     # the dccl_cli harness (C++ on the namespace-dccl API), rpath'd to the in-tree library
     os.makedirs(BIN_DIR, exist_ok=True)
     if force or not os.path.exists(CLI) or os.path.getmtime(CLI) < max(os.path.getmtime(LIB),

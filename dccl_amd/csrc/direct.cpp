@@ -98,7 +98,7 @@ struct Range {
 struct IpcXport {
     ShmCtl* ctl = nullptr;
     uint32_t rank = 0, world = 0;
-    double timeout_s = 0;  // 0: no limit (a dead peer is caught by the liveness check)
+    double timeout_s = 0;  // barrier wait limit, 0: none (set by ipc_join; a dead peer is caught by the liveness check)
     bool liveness = true;   // peers' pids are visible here (checked at join)
     // scratch: every input is copied here (one allocation, exported once)
     void* scratch = nullptr;        // allocation base: header (token), then scratch_bytes of data
@@ -222,8 +222,8 @@ void apply_retirements(ProcCache& pc) {
 // completes with the flag up.  The flag is sticky (the transport is unusable after a failed collective,
 // like an aborted NCCL communicator).  A waiter checks every ~100 ms that its peers' processes still
 // exist, so a peer that died (a runtime abort, a kill) ends every other rank's wait with ncclRemoteError
-// at once.  A live peer may take as long as it likes between collectives (a checkpoint, an evaluation): the
-// wait has no limit unless DCCL_IPC_TIMEOUT_S sets one, or the liveness check is off (then 300 s).
+// at once.  A live peer may take up to 30 minutes between collectives (a checkpoint, an evaluation);
+// DCCL_IPC_TIMEOUT_S sets another limit (0: none); with the liveness check off the limit is 300 s.
 ncclResult_t shm_barrier(IpcXport* x, bool ok = true) {
     ShmCtl* s = x->ctl;
     if (!ok) s->abort.store(1, std::memory_order_relaxed);
@@ -708,11 +708,16 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
     x->world = world;
     x->seen.assign(world, 0);
     x->liveness = liveness_requested();
-    if (const char* t = std::getenv("DCCL_IPC_TIMEOUT_S")) {
+    // A live peer stuck for half an hour (a hung kernel, a blocked synchronise) ends the wait;
+    // DCCL_IPC_TIMEOUT_S sets another limit, 0 none at all (ranks that may pause longer between collectives).
+    x->timeout_s = 1800;
+    const char* t = std::getenv("DCCL_IPC_TIMEOUT_S");
+    const bool explicit_limit = t != nullptr && *t != 0;
+    if (explicit_limit) {
         const double v = std::strtod(t, nullptr);
-        if (v > 0) x->timeout_s = v;
+        x->timeout_s = v > 0 ? v : 0;
     }
-    if (!x->liveness && x->timeout_s <= 0) x->timeout_s = 300;  // no liveness check: a dead peer ends the wait
+    if (!x->liveness && (!explicit_limit || x->timeout_s <= 0)) x->timeout_s = 300;  // a dead peer ends the wait
     ShmSlot& me = ctl->slot[rank];
     me.start = proc_start_time(static_cast<long>(::getpid()));
     // tests only (DCCL_FAULT_INJECT=hidden_pid:<rank>): publish a pid no peer can see, as a rank in another pid
@@ -722,7 +727,16 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
     c->ipc = x;
     c->rank = rank;
     c->world = world;
-    const ncclResult_t rc = shm_barrier(x);  // everyone mapped the segment
+    // Everyone mapped the segment.  This wait runs with the liveness check off and bounded by the rendezvous
+    // timeout: a rank may wait here for a late joiner, and a peer whose process it cannot see would
+    // look dead to a check made before the visibility probe below.
+    const bool live = x->liveness;
+    const double limit = x->timeout_s;
+    x->liveness = false;
+    x->timeout_s = rdv_timeout_s();
+    const ncclResult_t rc = shm_barrier(x);
+    x->liveness = live;
+    x->timeout_s = limit;
     // Ranks that share /dev/shm but not a pid namespace (containers with --ipc=host), or a /proc mounted with
     // hidepid, cannot see each other's processes: a live peer would look dead.  Then this communicator goes
     // without the liveness check (and with the 300 s default limit), said once.
@@ -730,7 +744,7 @@ ncclResult_t ipc_join(dcclComm* c, uint32_t world, uint32_t rank) {
         for (uint32_t p = 0; p < world; ++p)
             if (p != rank && !peer_alive(ctl->slot[p])) {
                 x->liveness = false;
-                if (x->timeout_s <= 0) x->timeout_s = 300;
+                if (!explicit_limit || x->timeout_s <= 0) x->timeout_s = 300;
                 std::fprintf(stderr, "[dccl ipc %d] rank %u's process (pid %lld) is not visible from here: liveness "
                                      "check off for this communicator\n", ::getpid(), p, (long long)ctl->slot[p].pid);
                 break;

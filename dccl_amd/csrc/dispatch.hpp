@@ -39,6 +39,25 @@ inline int validate(int dtype, int op) {
     return DCCL_SUCCESS;
 }
 
+// Operand ranges [a, a + bytes) and [b, b + bytes) that share bytes without being the same array.  The
+// reference's loop (internal_common.hpp:550-560) walks such ranges in ascending order on one thread, so an
+// element it writes can be read again later as a source; no parallel launch reproduces that order, and the
+// boundary rejects the call with ncclInvalidArgument (SURVEY.md §8(b) "Ownership").  The same array
+// (a == b) stays allowed: every combine is element-wise, each output depends only on its own index.
+inline bool partial_overlap(const void* a, const void* b, size_t bytes) {
+    const uintptr_t x = reinterpret_cast<uintptr_t>(a), y = reinterpret_cast<uintptr_t>(b);
+    return x != y && (x < y ? y - x < bytes : x - y < bytes);
+}
+
+// The overlap rule of every combine entry point (include/dccl/dccl_reduce.h): each source against the
+// destination, and `own` (chain forms; nullptr otherwise) against the destination.
+inline bool sources_overlap_destination(const void* const* sends, int nsend, const void* own, const void* dst,
+                                        size_t bytes) {
+    for (int k = 0; k < nsend; ++k)
+        if (partial_overlap(sends[k], dst, bytes)) return true;
+    return own != nullptr && partial_overlap(own, dst, bytes);
+}
+
 template <typename Fn, typename T, typename... A>
 inline int dispatch_op(int op, A&&... a) {
     switch (op) {

@@ -410,6 +410,7 @@ extern "C" int dccl_local_reduce_host(const void* send, void* recv, int dtype, s
     if (v != DCCL_SUCCESS) return v;
     if (count == 0) return DCCL_SUCCESS;
     if (send == nullptr || recv == nullptr) return DCCL_INVALID_ARGUMENT;
+    if (partial_overlap(send, recv, count * size_of_dtype(dtype))) return DCCL_INVALID_ARGUMENT;
     int dev = -1;
     if (hipGetDevice(&dev) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
     Stager* st = t_stagers.get(dev);
@@ -430,6 +431,8 @@ extern "C" int dccl_local_reduce_chain_host(const void* const* sends, int nsend,
     if (own == nullptr || dst == nullptr) return DCCL_INVALID_ARGUMENT;
     for (int k = 0; k < nsend; ++k)
         if (sends[k] == nullptr) return DCCL_INVALID_ARGUMENT;
+    if (sources_overlap_destination(sends, nsend, own, dst, count * size_of_dtype(dtype)))
+        return DCCL_INVALID_ARGUMENT;
     int dev = -1;
     if (hipGetDevice(&dev) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
     Stager* st = t_stagers.get(dev);
@@ -450,6 +453,20 @@ extern "C" int dccl_register_host_memory(void* buffer, size_t size) {
 extern "C" int dccl_deregister_host_memory(void* buffer) {
     if (buffer == nullptr) return DCCL_INVALID_ARGUMENT;
     return hipHostUnregister(buffer) == hipSuccess ? DCCL_SUCCESS : DCCL_UNHANDLED_DEVICE_ERROR;
+}
+
+// The measured crossover of dccl_local_reduce_host against the reference's one-thread loop (DESIGN.md §4,
+// bench.py `host_crossover`, page-locked fp32 Sum operands, cold caches).  The loop's rate is in bytes for
+// every dtype it vectorises, so one byte threshold serves them all.
+constexpr size_t kHostGpuMinBytes = size_t(4) << 20;
+
+extern "C" size_t dccl_host_reduce_gpu_min_bytes(int dtype) {
+    if (dtype == kFloat16 || dtype == kBfloat16 || size_of_dtype(dtype) == 0) return 0;  // no reference CPU loop
+    static const size_t v = [] {
+        const char* e = std::getenv("DCCL_HOST_GPU_MIN_BYTES");
+        return e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : kHostGpuMinBytes;
+    }();
+    return v;
 }
 
 extern "C" size_t dccl_size_of_type(int dtype) { return size_of_dtype(dtype); }

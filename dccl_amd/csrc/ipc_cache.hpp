@@ -161,11 +161,13 @@ public:
         return kOk;
     }
 
-    // Drop one use taken by acquire(); a retired mapping is closed with its last use.
+    // Drop one use taken by acquire(); a retired mapping is closed with its last use, and so is a suspect one
+    // (if its export really ended, nothing would acquire it again and it would pin the peer's freed
+    // pages until trim; a live export is simply reopened and verified by its next acquire).
     void release(int64_t pid, uint64_t serial) {
         auto it = map_.find(Key{pid, serial});
         if (it == map_.end() || it->second.users == 0) return;
-        if (--it->second.users == 0 && it->second.retired) close_entry(it);
+        if (--it->second.users == 0 && (it->second.retired || it->second.suspect)) close_entry(it);
     }
 
     // The exporter ended export (pid, serial): close its mapping now, or with its last use.

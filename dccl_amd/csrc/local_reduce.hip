@@ -273,6 +273,7 @@ extern "C" int dccl_local_reduce(const void* send, void* recv, int dtype, size_t
     if (v != DCCL_SUCCESS) return v;
     if (count == 0) return DCCL_SUCCESS;
     if (send == nullptr || recv == nullptr) return DCCL_INVALID_ARGUMENT;
+    if (partial_overlap(send, recv, count * size_of_dtype(dtype))) return DCCL_INVALID_ARGUMENT;
     return dispatch<ReduceFn>(dtype, op, send, recv, count, static_cast<hipStream_t>(stream));
 }
 
@@ -285,6 +286,8 @@ extern "C" int dccl_local_reduce_multi(const void* const* sends, int nsend, void
     if (recv == nullptr) return DCCL_INVALID_ARGUMENT;
     for (int k = 0; k < nsend; ++k)
         if (sends[k] == nullptr) return DCCL_INVALID_ARGUMENT;
+    if (sources_overlap_destination(sends, nsend, nullptr, recv, count * size_of_dtype(dtype)))
+        return DCCL_INVALID_ARGUMENT;
     return dispatch<ReduceMultiFn>(dtype, op, sends, nsend, recv, count, static_cast<hipStream_t>(stream));
 }
 
@@ -297,6 +300,8 @@ extern "C" int dccl_local_reduce_chain(const void* const* sends, int nsend, cons
     if (own == nullptr || dst == nullptr) return DCCL_INVALID_ARGUMENT;
     for (int k = 0; k < nsend; ++k)
         if (sends[k] == nullptr) return DCCL_INVALID_ARGUMENT;
+    if (sources_overlap_destination(sends, nsend, own, dst, count * size_of_dtype(dtype)))
+        return DCCL_INVALID_ARGUMENT;
     return dispatch<ReduceChainFn>(dtype, op, sends, nsend, own, dst, count, static_cast<hipStream_t>(stream));
 }
 
@@ -309,6 +314,14 @@ extern "C" int dccl_copy_multi(const void* const* srcs, void* const* dsts, int n
         cl.src[y] = static_cast<const unsigned char*>(srcs[y]);
         cl.dst[y] = static_cast<unsigned char*>(dsts[y]);
     }
+    // a pair's dst may be its own src (a no-op copy); it may share no other byte with any src or dst
+    for (int y = 0; y < npairs; ++y)
+        for (int z = 0; z < npairs; ++z) {
+            if (z == y ? partial_overlap(srcs[z], dsts[y], bytes) : (partial_overlap(srcs[z], dsts[y], bytes) ||
+                                                                     srcs[z] == dsts[y]))
+                return DCCL_INVALID_ARGUMENT;
+            if (z > y && (partial_overlap(dsts[z], dsts[y], bytes) || dsts[z] == dsts[y])) return DCCL_INVALID_ARGUMENT;
+        }
     const auto st = static_cast<hipStream_t>(stream);
     size_t gx = ceil_div(bytes / 16 + 1, 64);
     if (gx > (size_t(1) << 20)) gx = size_t(1) << 20;

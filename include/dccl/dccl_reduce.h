@@ -13,7 +13,16 @@
  * fp16/bf16 widen to fp32 and round back to nearest-even.  Avg returns
  * ncclInvalidUsage (5), any other op or an unknown dtype ncclInvalidArgument (4),
  * a HIP failure ncclUnhandledCudaError (1).  count == 0 is a successful no-op.
- * send == recv is allowed (element-wise, so trivially well defined).
+ *
+ * Aliasing (SURVEY.md §8(b) "Ownership"), the same rule at every combine entry point below:
+ *   - an operand may BE the destination (send == recv; a k-way source == recv; a chain source or
+ *     own == dst): every combine is element-wise, so each output depends only on its own index;
+ *   - an operand whose count*sizeof(dtype) bytes PARTIALLY overlap the destination's (shared bytes,
+ *     different start) returns ncclInvalidArgument (4) before anything is launched.  The reference's
+ *     one-thread ascending loop (/root/reference/src/core/internal_common.hpp:550-560) gives such a call
+ *     an order-dependent answer that no parallel kernel reproduces.
+ *   Sources may overlap each other freely (they are only read).  dccl_copy_multi: a pair's dst may equal
+ *   its own src; no dst may share a byte with another pair's src or dst.
  */
 #ifndef DCCL_REDUCE_H_
 #define DCCL_REDUCE_H_
@@ -101,6 +110,18 @@ int dccl_local_reduce_host(const void* send, void* recv, int dtype, size_t count
  */
 int dccl_local_reduce_chain_host(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
                                  size_t count, int op);
+
+/*
+ * Routing hint for host-resident chunks: the payload size (bytes per operand) from which
+ * dccl_local_reduce_host beats the reference's own one-thread CPU loop do_host_reduce<DT>
+ * (/root/reference/src/core/internal_common.hpp:496-586) on MI355X, measured on page-locked operands by
+ * bench.py's `host_crossover` leg.  A caller keeps do_host_reduce below it (INTEGRATION.md
+ * §1).  0 for dtypes the reference's host loop cannot combine (bf16; fp16 has host operators only in CUDA
+ * builds), an unknown dtype included: the GPU path is then the only one.  DCCL_HOST_GPU_MIN_BYTES overrides
+ * the measured value for every dtype the reference's loop supports.  This is advice for the caller: the
+ * library itself never combines on the CPU.
+ */
+size_t dccl_host_reduce_gpu_min_bytes(int dtype);
 
 /* Page-lock a host range for direct DMA by dccl_local_reduce_host
  * (the role of dcclRegisterCacheMemory, /root/reference/src/core/dccl.cpp:503-549). */

@@ -69,8 +69,24 @@ def restatement():
         lib.oracle_synth_fill.restype = ctypes.c_int
         lib.oracle_synth_fill.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t]
+        lib.oracle_time_host_reduce.restype = ctypes.c_double
+        lib.oracle_time_host_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                                ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_double, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
         _cache["rs"] = lib
     return _cache["rs"]
+
+
+def time_host_reduce(send_ptr: int, recv_ptr: int, count: int, dtype: int, op: int, nthreads: int = 1,
+                     nsets: int = 1, stride: int = 0, min_seconds: float = 0.25, min_reps: int = 3) -> tuple:
+    """(seconds per combine, calls) of the restatement timed in C (cpu_timing.c): `nsets` operand pairs
+    `stride` bytes apart in rotation, each combine split over `nthreads` threads.  Bench CPU baseline only."""
+    reps = ctypes.c_size_t(0)
+    t = restatement().oracle_time_host_reduce(send_ptr, recv_ptr, nsets, stride, count, dtype, op, nthreads,
+                                              min_seconds, min_reps, ctypes.byref(reps))
+    if t < 0:
+        raise RuntimeError(f"oracle_time_host_reduce failed ({t})")
+    return t, int(reps.value)
 
 
 def compile_benchflags(outdir: str) -> str | None:

@@ -177,8 +177,12 @@ void test_retire_pid() {
     // in use: suspect, not retired (it may be a live export another collective is reading)
     CHECK(c.find(100, 3) != nullptr && !c.find(100, 3)->retired && c.find(100, 3)->suspect);
     CHECK(c.find(200, 1) != nullptr && !c.find(200, 1)->retired && !c.find(200, 1)->suspect);
+    c.release(100, 3);  // a suspect mapping closes with its last use
+    CHECK(c.find(100, 3) == nullptr && rt.bad_closes == 0);
+    bool opened = false;  // a live export is reopened and handed out for verification
+    CHECK(c.acquire(100, 3, handle(3), 4096, &a, 15, &opened) == kOk && opened && c.find(100, 3)->users == 1);
     c.release(100, 3);
-    CHECK(c.find(100, 3) != nullptr && rt.bad_closes == 0);
+    CHECK(c.find(100, 3) != nullptr && rt.bad_closes == 0);  // verified and trusted: kept
 }
 
 // a retirement-log overflow while a mapping is in use.  A concurrent acquire of the same live

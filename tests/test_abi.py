@@ -73,6 +73,45 @@ def test_validation_without_gpu():
     assert d.local_reduce_chain_host([0], 8, 8, 7, 16, 0) == 4       # NULL send
 
 
+@pytest.mark.parametrize("dt", [0, 6, 7, 8])
+def test_partial_overlap_rejected_without_gpu(dt):
+    """The aliasing contract of include/dccl/dccl_reduce.h: an operand that shares bytes
+    with the destination without starting at the same address returns ncclInvalidArgument at every combine
+    entry point, before any HIP call (so it answers here, with no GPU).  Overlap by one element and by all
+    but one, in both directions; sources only read may overlap each other."""
+    import dccl_amd as d
+    esz, n = d.size_of_type(dt), 64
+    base = 1 << 40  # never dereferenced: the check is pointer arithmetic ahead of any launch
+    dst = base + 4096
+    shifts = [esz, -esz, (n - 1) * esz, -(n - 1) * esz]
+    for sh in shifts:
+        src = dst + sh
+        assert d.local_reduce(src, dst, dt, n, 0) == 4, sh
+        assert d.local_reduce_host(src, dst, dt, n, 0) == 4, sh
+        far = base + (1 << 30)
+        for k in (1, 3, 8):
+            srcs = [far + j * n * esz for j in range(k - 1)] + [src]
+            assert d.local_reduce_multi(srcs, dst, dt, n, 2) == 4, (sh, k)
+            assert d.local_reduce_chain(srcs, far + (1 << 20), dst, dt, n, 3) == 4, (sh, k)
+            assert d.local_reduce_chain_host(srcs, far + (1 << 20), dst, dt, n, 3) == 4, (sh, k)
+        # own against dst
+        assert d.local_reduce_chain([far], src, dst, dt, n, 0) == 4, sh
+        assert d.local_reduce_chain_host([far], src, dst, dt, n, 0) == 4, sh
+        # copy_multi: a dst overlapping its own src, another pair's src, or another pair's dst
+        nb = n * esz
+        assert d.copy_multi([src], [dst], nb) == 4, sh
+        assert d.copy_multi([far, src], [dst, far + (1 << 20)], nb) == 4, sh
+        assert d.copy_multi([far, far + (1 << 20)], [dst, src], nb) == 4, sh
+    # validation order is unchanged: dtype and op first, then null pointers, then overlap
+    assert d.local_reduce(dst + esz, dst, 10, n, 0) == 4
+    assert d.local_reduce(dst + esz, dst, dt, n, 4) == 5
+    assert d.local_reduce(dst + esz, dst, dt, 0, 0) == 0  # count 0: nothing overlaps
+    # adjacent ranges (the bench's pooled layout, the ring's chunk k and k+1) pass validation: without a GPU
+    # the launch itself then fails with a device error, not ncclInvalidArgument
+    assert d.local_reduce(dst + n * esz, dst, dt, n, 0) not in (0, 4)
+    assert d.local_reduce(dst - n * esz, dst, dt, n, 0) not in (0, 4)
+
+
 def test_enum_values_match_reference_header():
     """Numeric enum values are the reference's (include/dccl/dccl.hpp:59-112)."""
     import dccl_amd as d

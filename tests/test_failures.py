@@ -262,8 +262,11 @@ IPC_FAIL_CHILD = """
 import glob, json, os
 import torch
 import dccl_amd
+import time
 W, r = int(os.environ["W"]), int(os.environ["RANK_ID"])
 torch.cuda.set_device(0)
+if r == int(os.environ.get("LATE_RANK", "-1")):  # joins late: its peers wait at the join barrier meanwhile
+    time.sleep(float(os.environ["LATE_S"]))
 comm = dccl_amd.Comm.ipc(W, r)
 n = 1024 * W
 x = torch.full((n,), float(r + 1), device="cuda")
@@ -314,8 +317,11 @@ IPC_HIDDEN_CHILD = """
 import json, os
 import torch
 import dccl_amd
+import time
 W, r = int(os.environ["W"]), int(os.environ["RANK_ID"])
 torch.cuda.set_device(0)
+if r == int(os.environ.get("LATE_RANK", "-1")):  # joins late: its peers wait at the join barrier meanwhile
+    time.sleep(float(os.environ["LATE_S"]))
 comm = dccl_amd.Comm.ipc(W, r)
 n = 1024 * W
 x = torch.full((n,), float(r + 1), device="cuda")
@@ -332,15 +338,20 @@ print(json.dumps({"rcs": rcs, "ok": ok, "finalize": comm.finalize()}))
 
 
 @pytest.mark.gpu
-def test_ipc_invisible_peer_turns_liveness_off(gpu, tmp_path):
+@pytest.mark.parametrize("W,late", [(2, None), (3, 2), (4, 0)])
+def test_ipc_invisible_peer_turns_liveness_off(gpu, tmp_path, W, late):
     """A rank whose peers cannot see its process (DCCL_FAULT_INJECT=hidden_pid:1 publishes a pid that does not
     exist) must not be taken for dead: its peers turn the liveness check off for that communicator at join and
     say so once on stderr, and every collective succeeds (before, any barrier wait over 100 ms became
-    ncclRemoteError)."""
+    ncclRemoteError).  With a rank joining 700 ms late, the others wait at the join barrier after the hidden
+    rank has published its pid: that wait runs without the liveness check, or it would take the
+    hidden rank for dead and abort every rank's init."""
     import uuid
-    W, tag = 2, "ipchide_" + uuid.uuid4().hex[:10]
+    tag = "ipchide_" + uuid.uuid4().hex[:10]
     env = {**os.environ, "PYTHONPATH": ROOT, "W": str(W), "DCCL_BOOTSTRAP_TAG": tag, "DCCL_BOOTSTRAP_DIR": str(tmp_path),
            "DCCL_FAULT_INJECT": "hidden_pid:1"}
+    if late is not None:
+        env.update(LATE_RANK=str(late), LATE_S="0.7")
     env.pop("DCCL_IPC_TIMEOUT_S", None)
     ps = [subprocess.Popen([sys.executable, "-c", textwrap.dedent(IPC_HIDDEN_CHILD)], env={**env, "RANK_ID": str(r)},
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(W)]
@@ -357,5 +368,8 @@ def test_ipc_invisible_peer_turns_liveness_off(gpu, tmp_path):
                 p.kill()
                 p.wait()
     assert all(o["rcs"] == [0, 0, 0] and o["ok"] and o["finalize"] == 0 for o in outs), outs
-    assert "liveness check off for this communicator" in errs[0], errs[0][-2000:]
-    assert "liveness check off" not in errs[1], errs[1][-2000:]
+    for p in range(W):  # every rank but the hidden one sees an invisible peer; the hidden rank sees everyone
+        if p == 1:
+            assert "liveness check off" not in errs[p], errs[p][-2000:]
+        else:
+            assert "liveness check off for this communicator" in errs[p], (p, errs[p][-2000:])

@@ -247,6 +247,67 @@ def test_aliasing_send_is_recv(dccl, off):
             assert not t[:off].any() and not t[off + s.nbytes:].any()
 
 
+@pytest.mark.parametrize("entry", ["pair", "multi", "chain_src", "chain_own", "host", "chain_host", "copy"])
+def test_partial_overlap_contract(dccl, entry):
+    """VERDICT r5 item 2, on the GPU: every combine entry point returns ncclInvalidArgument for an operand
+    overlapping the destination by one element (either direction) and leaves the destination untouched; the
+    same operands one element further apart (adjacent, no shared byte) combine bit-exactly against the
+    oracle."""
+    dt, n, op = 7, 4099, 0
+    esz = 4
+    rng = np.random.default_rng(77)
+    host = entry in ("host", "chain_host")
+    dev = "cpu" if host else "cuda"
+    for sh in (-(n - 1), n - 1, -n, n):  # elements between the destination's start and the operand's
+        buf = torch.zeros(3 * n, dtype=torch.float32, device=dev)
+        if host:
+            buf = buf.pin_memory()
+        vals = rng.standard_normal(3 * n).astype(np.float32)
+        buf.copy_(torch.from_numpy(vals))
+        other = torch.from_numpy(rng.standard_normal(n).astype(np.float32)).to(dev)
+        if host:
+            other = other.pin_memory()
+        d0 = n  # destination: elements [n, 2n)
+        dptr, optr = buf.data_ptr() + d0 * esz, buf.data_ptr() + (d0 + sh) * esz
+        before = buf.cpu().numpy().copy()
+        if entry == "pair":
+            rc = dccl.local_reduce(optr, dptr, dt, n, op, 0)
+        elif entry == "multi":
+            rc = dccl.local_reduce_multi([other.data_ptr(), optr], dptr, dt, n, op, 0)
+        elif entry == "chain_src":
+            rc = dccl.local_reduce_chain([other.data_ptr(), optr], other.data_ptr(), dptr, dt, n, op, 0)
+        elif entry == "chain_own":
+            rc = dccl.local_reduce_chain([other.data_ptr()], optr, dptr, dt, n, op, 0)
+        elif entry == "host":
+            rc = dccl.local_reduce_host(optr, dptr, dt, n, op)
+        elif entry == "chain_host":
+            rc = dccl.local_reduce_chain_host([other.data_ptr()], optr, dptr, dt, n, op)
+        else:
+            rc = dccl.copy_multi([optr], [dptr], n * esz, 0)
+        torch.cuda.synchronize()
+        after = buf.cpu().numpy()
+        if abs(sh) < n:
+            assert rc == 4, (entry, sh, rc)
+            assert after.tobytes() == before.tobytes(), (entry, sh)
+            continue
+        assert rc == 0, (entry, sh, rc)
+        src = before[d0 + sh:d0 + sh + n]
+        o = other.cpu().numpy()
+        if entry in ("pair", "host"):
+            want = oracle.combine(src, before[d0:d0 + n], dt, op)
+        elif entry == "multi":
+            want = oracle.combine(src, oracle.combine(o, before[d0:d0 + n], dt, op), dt, op)
+        elif entry == "chain_src":  # dst = op(own, op(s1, s0)), own = s0 = other
+            want = oracle.combine(oracle.combine(o, src, dt, op), o, dt, op)
+        elif entry in ("chain_own", "chain_host"):  # dst = op(own, s0)
+            want = oracle.combine(o, src, dt, op)
+        else:
+            want = src
+        assert fp_equal(after[d0:d0 + n], want, dt), (entry, sh)
+        rest = np.concatenate([after[:d0], after[d0 + n:]]), np.concatenate([before[:d0], before[d0 + n:]])
+        assert rest[0].tobytes() == rest[1].tobytes(), (entry, sh)
+
+
 def test_stream_ordering(dccl):
     """Launches on a user stream are ordered behind prior work on that stream."""
     st = torch.cuda.Stream()

@@ -45,6 +45,16 @@ static void cpu_checks(void) {
     CHECK(dccl_synth_fill(NULL, 7, 16, 0, 1, 0, NULL) == DCCL_INVALID_ARGUMENT);
     CHECK(dccl_copy_multi(NULL, NULL, 0, 16, NULL) == DCCL_SUCCESS);
     CHECK(dccl_all_reduce(a, b, 4, 7, 0, NULL, NULL) == DCCL_INVALID_ARGUMENT); /* null communicator */
+    /* partial overlap with the destination (one element apart) is rejected before any device work */
+    float c[8] = {0};
+    CHECK(dccl_local_reduce(c + 1, c, 7, 4, 0, NULL) == DCCL_INVALID_ARGUMENT);
+    CHECK(dccl_local_reduce_host(c, c + 1, 7, 4, 0) == DCCL_INVALID_ARGUMENT);
+    const void* ov[1] = {c + 1};
+    CHECK(dccl_local_reduce_multi(ov, 1, c, 7, 4, 0, NULL) == DCCL_INVALID_ARGUMENT);
+    CHECK(dccl_local_reduce_chain(sends, 1, c + 3, c, 7, 4, 0, NULL) == DCCL_INVALID_ARGUMENT);
+    CHECK(dccl_local_reduce_chain_host(ov, 1, a, c, 7, 4, 0) == DCCL_INVALID_ARGUMENT);
+    /* routing hint: the reference has no host loop for bf16 / fp16 */
+    CHECK(dccl_host_reduce_gpu_min_bytes(9) == 0 && dccl_host_reduce_gpu_min_bytes(6) == 0);
 }
 
 static void gpu_checks(void) {
