@@ -378,8 +378,10 @@ def measured_traffic(nbytes: int, dt: int, op: int, launches: int = 5) -> dict:
 
 
 HOST_SIZES = [4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30]
-HOST_ROTATE_BYTES = 256 << 20  # per operand: operand pairs rotated over this much memory, so no call finds its
-#                                operands in a cache (the L3 is 32 MiB per CCD), as a chunk that just arrived by RDMA
+HOST_ROTATE_BYTES = 1 << 30  # per operand: operand pairs rotated over this much memory, so no call finds its operands
+#                              in a cache (the L3 is 32 MiB per CCD, 512 MiB over a 2-socket EPYC 9575F host's 16 CCDs,
+#                              which a 16-thread leg spread over both sockets can fill), as a chunk that just arrived
+#                              by RDMA
 
 
 def granted_cpus() -> int:
@@ -409,12 +411,54 @@ def _gpu_host_us(ps: int, pr: int, n: int, nsets: int, stride: int, dt: int, op:
                 return el / reps * 1e6, reps
 
 
+def numa_nodes_of(addr: int) -> dict | None:
+    """Pages per NUMA node of the mapping that holds `addr` (/proc/self/numa_maps), None when unreadable."""
+    try:
+        for line in open("/proc/self/numa_maps"):
+            parts = line.split()
+            start = int(parts[0], 16)
+            if start <= addr and any(p.startswith("N") and "=" in p for p in parts):
+                nodes = {p.split("=")[0]: int(p.split("=")[1]) for p in parts if p[0] == "N" and p[1:2].isdigit()}
+                kb = next((int(p.split("=")[1]) for p in parts if p.startswith("kernelpagesize_kB=")), 4)
+                if start + sum(nodes.values()) * kb * 1024 > addr:
+                    return nodes
+    except Exception:
+        return None
+    return None
+
+
+def node_cpus() -> dict:
+    """{NUMA node: CPUs of this process's affinity mask on it}, from /sys (empty when unreadable)."""
+    allowed, out = os.sched_getaffinity(0), {}
+    base = "/sys/devices/system/node"
+    try:
+        for d in sorted(os.listdir(base)):
+            if not (d.startswith("node") and d[4:].isdigit()):
+                continue
+            cpus = set()
+            for part in open(os.path.join(base, d, "cpulist")).read().strip().split(","):
+                if part:
+                    lo, _, hi = part.partition("-")
+                    cpus.update(range(int(lo), int(hi or lo) + 1))
+            if cpus & allowed:
+                out[int(d[4:])] = sorted(cpus & allowed)
+    except Exception:
+        return {}
+    return out
+
+
 def host_crossover(dt: int = 7, op: int = 0, min_s: float = 0.25) -> dict:
-    """Where the host-resident GPU path pays.  For each payload size 4 KiB - 1 GiB, on
-    page-locked and on pageable host operands, on the SAME buffers: dccl_local_reduce_host (the product: H2D,
+    """Where the host-resident GPU path pays.  For each payload size 4 KiB - 1 GiB, on three
+    kinds of host operands, on the SAME buffers: dccl_local_reduce_host (the product: H2D,
     combine, D2H) against the oracle restatement of the reference's loop do_host_reduce
     (internal_common.hpp:496-586, oracle/host_reduce.c, Release flags; timed in C by oracle/cpu_timing.c) on
     1 core, as the reference runs it (one thread per rank), and on every core this process is granted.
+    Kinds: `registered` = ordinary malloc'ed memory page-locked in place by dccl_register_host_memory (DCCL's
+    configuration: Derecho's RDMA buffers registered through dcclRegisterCacheMemory, dccl.cpp:503-549),
+    `pinned` = hipHostMalloc memory (torch pin_memory), `pageable` = malloc'ed memory (bounced by the GPU path).
+    The 1-core legs run on a CPU of the NUMA node that holds the buffer (`cpu1_us`, the CPU's best case: a rank
+    thread placed by its memory) and on a CPU of another node (`cpu1_remote_us`): an unpinned thread lands on
+    either, and the remote socket's rate is ~1.6x lower.
     Operand pairs rotate over HOST_ROTATE_BYTES so every call starts cold; `cpu1_hot_us` repeats one pair
     (cache-resident up to tens of MiB) as the CPU's best case.  Every size's GPU result is checked bit for bit
     against the oracle on the same inputs.  `crossover` = the smallest size from which the GPU path is faster
@@ -429,9 +473,35 @@ def host_crossover(dt: int = 7, op: int = 0, min_s: float = 0.25) -> dict:
     pin_r.view(torch.float32).uniform_(-1, 1)
     pag_s = oracle.aligned_empty(top, np.uint8, align=4096)
     pag_r = oracle.aligned_empty(top, np.uint8, align=4096)
-    np.copyto(pag_s, pin_s.numpy())
-    np.copyto(pag_r, pin_r.numpy())
-    bufs = {"pinned": (pin_s.numpy(), pin_r.numpy()), "pageable": (pag_s, pag_r)}
+    reg_s = oracle.aligned_empty(top, np.uint8, align=4096)
+    reg_r = oracle.aligned_empty(top, np.uint8, align=4096)
+    for dst, src in ((pag_s, pin_s), (pag_r, pin_r), (reg_s, pin_s), (reg_r, pin_r)):
+        np.copyto(dst, src.numpy())
+    for b in (reg_s, reg_r):
+        dccl_amd.check(dccl_amd.register_host_memory(b.ctypes.data, top), "dccl_register_host_memory")
+    bufs = {"registered": (reg_s, reg_r), "pinned": (pin_s.numpy(), pin_r.numpy()), "pageable": (pag_s, pag_r)}
+    placement = {kind: numa_nodes_of(s.ctypes.data) for kind, (s, _) in bufs.items()}
+    nodes = node_cpus()
+    full_affinity = os.sched_getaffinity(0)
+
+    def cpu_pick(kind, local):  # a CPU on (local) or off (remote) the node holding the buffer, None if unknown
+        pages = placement.get(kind) or {}
+        if not pages or len(nodes) < (1 if local else 2):
+            return None
+        home = int(max(pages, key=pages.get)[1:])
+        cands = [c for nd, cs in nodes.items() if (nd == home) == local for c in cs]
+        return cands[len(cands) // 2] if cands else None
+
+    def time_cpu1(kind, local, ps, pr, n, nsets, stride, budget):
+        cpu = cpu_pick(kind, local)
+        if cpu is None and not local:
+            return None
+        try:
+            if cpu is not None:
+                os.sched_setaffinity(0, {cpu})
+            return oracle.time_host_reduce(ps, pr, n, dt, op, 1, nsets, stride, budget)[0]
+        finally:
+            os.sched_setaffinity(0, full_affinity)
     npd = oracle.NP_DTYPES[dt]
     rows = []
     for size in HOST_SIZES:
@@ -445,26 +515,38 @@ def host_crossover(dt: int = 7, op: int = 0, min_s: float = 0.25) -> dict:
             oracle.expected_reduce(s[:size].view(npd), want, dt, op)
             exact = r[:size].tobytes() == want.tobytes()
             del want
-            gpu_us, gpu_reps = _gpu_host_us(ps, pr, n, nsets, size, dt, op, min_s)
-            c1, _ = oracle.time_host_reduce(ps, pr, n, dt, op, 1, nsets, size, min_s)
-            cn, _ = oracle.time_host_reduce(ps, pr, n, dt, op, cores, nsets, size, min_s)
-            rec = {"gpu_us": round(gpu_us, 2), "cpu1_us": round(c1 * 1e6, 2), "cpu_all_us": round(cn * 1e6, 2),
-                   "gpu_payload_gib_s": round(size / (gpu_us * 1e-6) / GIB, 2), "bit_exact": exact,
-                   "gpu_calls": gpu_reps}
-            if kind == "pinned" and size <= 64 << 20:
-                ch, _ = oracle.time_host_reduce(ps, pr, n, dt, op, 1, 1, 0, min_s)
-                rec["cpu1_hot_us"] = round(ch * 1e6, 2)
+            # every leg three times, interleaved, each trial a third of the budget; the fastest trial of each leg
+            # is kept (the host's CPUs and memory are shared with the node's other GPUs' jobs)
+            legs = {"gpu_us": lambda: _gpu_host_us(ps, pr, n, nsets, size, dt, op, min_s / 3)[0] * 1e-6,
+                    "cpu1_us": lambda: time_cpu1(kind, True, ps, pr, n, nsets, size, min_s / 3),
+                    "cpu1_remote_us": lambda: time_cpu1(kind, False, ps, pr, n, nsets, size, min_s / 3),
+                    "cpu_all_us": lambda: oracle.time_host_reduce(ps, pr, n, dt, op, cores, nsets, size,
+                                                                  min_s / 3)[0]}
+            if kind == "registered" and size <= 64 << 20:
+                legs["cpu1_hot_us"] = lambda: time_cpu1(kind, True, ps, pr, n, 1, 0, min_s / 3)
+            trials = {k: [] for k in legs}
+            for _ in range(3):
+                for k, fn in legs.items():
+                    trials[k].append(fn())
+            rec = {k: round(min(v) * 1e6, 2) for k, v in trials.items() if None not in v}
+            rec["spread"] = {k: round(max(v) / min(v), 3) for k, v in trials.items() if None not in v}
+            rec.update(gpu_payload_gib_s=round(size / (rec["gpu_us"] * 1e-6) / GIB, 2), bit_exact=exact)
             row[kind] = rec
         rows.append(row)
-        progress(f"host crossover {size >> 10} KiB: pinned GPU {row['pinned']['gpu_us']} us, "
-                 f"CPU 1 core {row['pinned']['cpu1_us']} us, {cores} cores {row['pinned']['cpu_all_us']} us")
+        progress(f"host crossover {size >> 10} KiB, registered: GPU {row['registered']['gpu_us']} us, "
+                 f"CPU 1 core {row['registered']['cpu1_us']} us (other node "
+                 f"{row['registered'].get('cpu1_remote_us')} us), {cores} cores {row['registered']['cpu_all_us']} us")
     kinds = list(bufs)
-    del pin_s, pin_r, pag_s, pag_r, bufs
+    for b in (reg_s, reg_r):
+        dccl_amd.check(dccl_amd.deregister_host_memory(b.ctypes.data), "dccl_deregister_host_memory")
+    del pin_s, pin_r, pag_s, pag_r, reg_s, reg_r, bufs
 
     def crossover(kind, key):
         win = None
         for row in reversed(rows):
-            if key not in row[kind] or not row[kind]["gpu_us"] < row[kind][key]:
+            if key not in row[kind]:  # cpu1_hot_us: only up to 64 MiB (larger pairs do not stay in a cache)
+                continue
+            if not row[kind]["gpu_us"] < row[kind][key]:
                 break
             win = row["bytes"]
         return win
@@ -477,15 +559,18 @@ def host_crossover(dt: int = 7, op: int = 0, min_s: float = 0.25) -> dict:
     return {
         "python_call_overhead_us": round(call_us, 3),
         "crossover": {kind: {"vs_1_core": crossover(kind, "cpu1_us"), "vs_1_core_hot": crossover(kind, "cpu1_hot_us"),
+                             "vs_1_core_remote_node": crossover(kind, "cpu1_remote_us"),
                              f"vs_{cores}_cores": crossover(kind, "cpu_all_us")} for kind in kinds},
-        "cores": cores, "dtype": dt, "op": op,
+        "cores": cores, "dtype": dt, "op": op, "numa_pages_by_kind": placement,
+        "cpu1_cpus": {kind: {"local": cpu_pick(kind, True), "remote": cpu_pick(kind, False)} for kind in kinds},
         "all_bit_exact": all(row[k]["bit_exact"] for row in rows for k in kinds),
         "product_default_gpu_min_bytes": dccl_amd.host_reduce_gpu_min_bytes(dt),
         "rows": rows,
         "how": "same host buffers for every leg; GPU = dccl_local_reduce_host per call (synchronous); CPU = "
                "oracle/host_reduce.c (restatement of internal_common.hpp:496-586, -O3 -mprefer-vector-width=512) "
                "timed in C, 1 thread and `cores` threads (64-B aligned slices, spinning team); pairs rotated over "
-               f"{HOST_ROTATE_BYTES >> 20} MiB per operand (cold), cpu1_hot_us = one pair repeated",
+               f"{HOST_ROTATE_BYTES >> 20} MiB per operand (cold), cpu1_hot_us = one pair repeated (registered "
+               "kind, up to 64 MiB)",
     }
 
 
@@ -1418,10 +1503,11 @@ def run_rank(a):
                 hc = host_crossover()
             except Exception as e:  # reported, never fatal to the line
                 hc = {"error": repr(e)}
-            top = hc["rows"][-1] if "rows" in hc else {"bytes": None, "pinned": {}, "pageable": {}}
+            top = hc["rows"][-1] if "rows" in hc else {"bytes": None, "pinned": {}, "pageable": {}, "registered": {}}
             res["host_staged"] = {"payload_gib_s": top["pinned"].get("gpu_payload_gib_s"),
                                   "ms": round(top["pinned"].get("gpu_us", 0) / 1e3, 3), "bytes_per_operand": top["bytes"],
                                   "pageable_payload_gib_s": top["pageable"].get("gpu_payload_gib_s"),
+                                  "registered_payload_gib_s": top["registered"].get("gpu_payload_gib_s"),
                                   "note": "fp32 Sum, pinned host operands; PCIe H2D 2N + D2H N bytes "
                                           "(the 1 GiB row of host_crossover)"}
             res["host_crossover"] = hc

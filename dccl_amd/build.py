@@ -6,7 +6,7 @@ link is a plain ``hipcc -shared``.  No fast-math / FTZ flags: the combine must k
 fp32/fp16 denormals (SURVEY.md §7 "Bit-exact semantics").
 
 Tools-only artefacts, never linked into the product library: the dccl_cli harness and the plain-C ABI
-check, the PMC, native C4 and host-crossover workloads of bench.py (dccl_amd/bin/).
+check, the PMC and native C4 workloads of bench.py (dccl_amd/bin/).
 
     python dccl_amd/build.py [--force]      (by path: importing the package loads the library)
 """

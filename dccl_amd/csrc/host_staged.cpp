@@ -456,9 +456,9 @@ extern "C" int dccl_deregister_host_memory(void* buffer) {
 }
 
 // The measured crossover of dccl_local_reduce_host against the reference's one-thread loop (DESIGN.md §4,
-// bench.py `host_crossover`, page-locked fp32 Sum operands, cold caches).  The loop's rate is in bytes for
+// bench.py `host_crossover`, registered fp32 Sum operands, cold caches; profiles/r6_host_crossover.json).  The loop's rate is in bytes for
 // every dtype it vectorises, so one byte threshold serves them all.
-constexpr size_t kHostGpuMinBytes = size_t(4) << 20;
+constexpr size_t kHostGpuMinBytes = size_t(256) << 20;
 
 extern "C" size_t dccl_host_reduce_gpu_min_bytes(int dtype) {
     if (dtype == kFloat16 || dtype == kBfloat16 || size_of_dtype(dtype) == 0) return 0;  // no reference CPU loop
