@@ -141,6 +141,31 @@ def test_bench_rccl_two_ranks_one_gpu():
     assert all(set(r) == {"ring", "grouped", "direct", "rccl"} and min(r.values()) > 0
                for r in s["sweep_busbw_gb_s"].values()), s
     assert s["dccl_allgather"]["direct"]["wrong_slices_all_ranks"] == 0, s
+    # the child's wall time per phase, against its watchdog
+    assert s["child_wall_s"] < s["child_timeout_s"], s
+    assert {"init", "allreduce_ring", "allreduce_grouped", "allreduce_direct", "sweep", "allgather",
+            "finalize"} <= set(s["phase_s"]), s["phase_s"]
+
+
+def test_host_crossover_leg(monkeypatch):
+    """bench.py's host_crossover leg, on small sizes: every kind of host operand (registered,
+    pinned, pageable) and every leg timed on the same buffers, the GPU results bit-exact against the oracle, the
+    crossover keys present, the registration undone."""
+    import bench
+    import dccl_amd
+    bench._native()
+    monkeypatch.setattr(bench, "HOST_SIZES", [4 << 10, 1 << 20, 16 << 20])
+    monkeypatch.setattr(bench, "HOST_ROTATE_BYTES", 64 << 20)
+    res = bench.host_crossover(min_s=0.03)
+    assert res["all_bit_exact"] is True, res
+    assert [r["bytes"] for r in res["rows"]] == [4 << 10, 1 << 20, 16 << 20]
+    for row in res["rows"]:
+        for kind in ("registered", "pinned", "pageable"):
+            rec = row[kind]
+            assert rec["gpu_us"] > 0 and rec["cpu1_us"] > 0 and rec["cpu_all_us"] > 0, rec
+    assert set(res["crossover"]) == {"registered", "pinned", "pageable"}
+    assert res["product_default_gpu_min_bytes"] == dccl_amd.host_reduce_gpu_min_bytes(7) > 0
+    assert dccl_amd.host_reduce_gpu_min_bytes(9) == 0 and dccl_amd.host_reduce_gpu_min_bytes(6) == 0
 
 
 def test_bench_single_gpu_line():
