@@ -34,6 +34,11 @@
 #include "dispatch.hpp"
 
 namespace dccl_amd {
+
+// dccl_local_reduce under a cap on its one-wave blocks (local_reduce.hip)
+int local_reduce_capped(const void* send, void* recv, int dtype, size_t count, int op, hipStream_t stream,
+                        size_t grid_cap);
+
 namespace {
 
 constexpr int kSlots = 3;
@@ -226,6 +231,21 @@ size_t zero_copy_max() {
     return e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : ~size_t(0);
 }
 
+// One-wave blocks of a zero-copy combine, each striding over the 1 KiB tiles.  The device combine's grid (one block
+// per tile) issues every read of a PCIe-bound launch at once and leaves its writes to a burst at the end, so the
+// link's host->device and device->host directions take turns; a few hundred striding waves keep both busy
+// together.  dccl_local_reduce_host per call on MI355X, fp32 Sum, registered / hipHostMalloc operands, best of
+// three (profiles/r6_zero_copy_waves.json): 512 waves against one block per tile, 4 MiB 220 -> 196 us, 16 MiB
+// 733 -> 682 us, 1 GiB 40.2 -> 37.5 ms (57 GB/s host->device); flat from 320 to 768 waves, slower at 128 and
+// from 1024.  DCCL_HOST_ZEROCOPY_WAVES overrides (0: one block per tile).
+size_t zero_copy_waves() {
+    static const size_t v = [] {
+        const char* e = std::getenv("DCCL_HOST_ZEROCOPY_WAVES");
+        return e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : size_t(512);
+    }();
+    return v;
+}
+
 int Stager::run_zero_copy(const unsigned char* send, unsigned char* recv, void* dsend, void* drecv, int dtype,
                           size_t count, int op) {
     const size_t bytes = count * size_of_dtype(dtype);
@@ -240,7 +260,7 @@ int Stager::run_zero_copy(const unsigned char* send, unsigned char* recv, void* 
         bounce(sl.h_recv, recv, bytes);
         if (hipHostGetDevicePointer(&drecv, sl.h_recv, 0) != hipSuccess) return DCCL_UNHANDLED_DEVICE_ERROR;
     }
-    int rc = dccl_local_reduce(dsend, drecv, dtype, count, op, comp_);
+    int rc = local_reduce_capped(dsend, drecv, dtype, count, op, comp_, zero_copy_waves());
     if (hipStreamSynchronize(comp_) != hipSuccess && rc == DCCL_SUCCESS) rc = DCCL_UNHANDLED_DEVICE_ERROR;
     if (rc == DCCL_SUCCESS && bounce_recv) bounce(recv, sl.h_recv, bytes);
     return rc;
@@ -458,7 +478,7 @@ extern "C" int dccl_deregister_host_memory(void* buffer) {
 // The measured crossover of dccl_local_reduce_host against the reference's one-thread loop (DESIGN.md §4,
 // bench.py `host_crossover`, registered fp32 Sum operands, cold caches; profiles/r6_host_crossover.json).  The loop's rate is in bytes for
 // every dtype it vectorises, so one byte threshold serves them all.
-constexpr size_t kHostGpuMinBytes = size_t(256) << 20;
+constexpr size_t kHostGpuMinBytes = size_t(64) << 20;
 
 extern "C" size_t dccl_host_reduce_gpu_min_bytes(int dtype) {
     if (dtype == kFloat16 || dtype == kBfloat16 || size_of_dtype(dtype) == 0) return 0;  // no reference CPU loop

@@ -59,8 +59,12 @@ size_t recv_align() {
     }();
     return v;
 }
+// grid_cap (a multiple of 8; 0 = none): at most this many one-wave blocks, each striding over the tiles.  The
+// zero-copy combine of host operands takes it (host_staged.cpp): uncapped, every wave of a PCIe-bound launch
+// issues its reads at once and the writes follow in one burst at the end, so the link's two directions work one
+// after the other instead of together.
 template <typename T, int OP>
-int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream) {
+int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream, size_t grid_cap = 0) {
     const auto s = static_cast<const unsigned char*>(send);
     const auto r = static_cast<unsigned char*>(recv);
     const uintptr_t as = reinterpret_cast<uintptr_t>(send), ar = reinterpret_cast<uintptr_t>(recv);
@@ -69,6 +73,7 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
         const size_t nvec = count / Pack<T>::N;
         size_t grid = ceil_div(ceil_div(nvec, size_t(64)), size_t(8)) * 8;  // a multiple of 8 (kMaxGrid is one)
         if (grid == 0) grid = 8;
+        if (grid_cap && grid > grid_cap) grid = grid_cap;
         unsigned p = unsigned(as & 15);
         int order = kOrderGroup;  // one front, shared lines in one L2: +4.5 points over the XCD ranges (round 3)
         void* args[] = {const_cast<unsigned char**>(&s), &p, const_cast<unsigned char**>(&r),
@@ -78,17 +83,21 @@ int reduce_typed(const void* send, void* recv, size_t count, hipStream_t stream)
     if (as % sizeof(T)) {  // an element-aligned recv and a send at any byte address: the shifted kernel
         const Split sp = split_for_vectors<T>(ar, count, align);
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);
-        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, false, kShiftRun>(s, r, count, stream, align)
-                         : launch_shift<T, OP, ShiftPolicy, false, 0, false, kShiftRun>(s, r, count, stream, align);
+        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, false, kShiftRun>(s, r, count, stream,
+                                                                                                align, 0, grid_cap)
+                         : launch_shift<T, OP, ShiftPolicy, false, 0, false, kShiftRun>(s, r, count, stream, align, 0,
+                                                                                       grid_cap);
     }
     const Split sp = split_for_vectors<T>(ar, count, align);
     if ((as ^ ar) & 15) {
         const uintptr_t a = (as + sp.head * sizeof(T)) & ~uintptr_t(15);  // the shifted kernel's send vectors
-        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, true, kShiftRun>(s, r, count, stream, align)
-                         : launch_shift<T, OP, ShiftPolicy, false, 0, true, kShiftRun>(s, r, count, stream, align);
+        return (a & 127) ? launch_shift<T, OP, ShiftStraddlePolicy, false, 0, true, kShiftRun>(s, r, count, stream,
+                                                                                               align, 0, grid_cap)
+                         : launch_shift<T, OP, ShiftPolicy, false, 0, true, kShiftRun>(s, r, count, stream, align, 0,
+                                                                                      grid_cap);
     }
-    if ((as ^ ar) & 127) return launch_vec<T, OP, StraddleCfg>(s, r, sp, stream);
-    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream);
+    if ((as ^ ar) & 127) return launch_vec<T, OP, StraddleCfg>(s, r, sp, stream, grid_cap);
+    return launch_vec<T, OP, DefaultCfg>(s, r, sp, stream, grid_cap);
 }
 
 // k-way combine: every resident wave keeps k+1 16-B loads per lane in flight, so the resident waves
@@ -251,8 +260,8 @@ struct ReduceChainFn {
 
 struct ReduceFn {
     template <typename T, int OP>
-    static int run(const void* send, void* recv, size_t count, hipStream_t stream) {
-        return reduce_typed<T, OP>(send, recv, count, stream);
+    static int run(const void* send, void* recv, size_t count, hipStream_t stream, size_t grid_cap) {
+        return reduce_typed<T, OP>(send, recv, count, stream, grid_cap);
     }
 };
 
@@ -268,13 +277,22 @@ struct ReduceMultiFn {
 
 using namespace dccl_amd;
 
-extern "C" int dccl_local_reduce(const void* send, void* recv, int dtype, size_t count, int op, void* stream) {
+namespace dccl_amd {
+// dccl_local_reduce with at most grid_cap one-wave blocks (a multiple of 8; 0 = none): the zero-copy combine of
+// host operands (host_staged.cpp).  Not exported.
+int local_reduce_capped(const void* send, void* recv, int dtype, size_t count, int op, hipStream_t stream,
+                        size_t grid_cap) {
     const int v = validate(dtype, op);
     if (v != DCCL_SUCCESS) return v;
     if (count == 0) return DCCL_SUCCESS;
     if (send == nullptr || recv == nullptr) return DCCL_INVALID_ARGUMENT;
     if (partial_overlap(send, recv, count * size_of_dtype(dtype))) return DCCL_INVALID_ARGUMENT;
-    return dispatch<ReduceFn>(dtype, op, send, recv, count, static_cast<hipStream_t>(stream));
+    return dispatch<ReduceFn>(dtype, op, send, recv, count, stream, grid_cap / 8 * 8);
+}
+}  // namespace dccl_amd
+
+extern "C" int dccl_local_reduce(const void* send, void* recv, int dtype, size_t count, int op, void* stream) {
+    return local_reduce_capped(send, recv, dtype, count, op, static_cast<hipStream_t>(stream), 0);
 }
 
 extern "C" int dccl_local_reduce_multi(const void* const* sends, int nsend, void* recv, int dtype, size_t count,

@@ -774,11 +774,12 @@ int launch_vec(const unsigned char* s, unsigned char* r, Split sp, hipStream_t s
 // address, SEND_ALIGNED false): the shifted vector kernel.
 template <typename T, int OP, int POLICY, bool XCD, int TAG = 0, bool SEND_ALIGNED = true, int RUN = 1>
 int launch_shift(const unsigned char* s, unsigned char* r, size_t count, hipStream_t stream, size_t align = 16,
-                 size_t lds_bytes = 0) {
+                 size_t lds_bytes = 0, size_t grid_cap = 0) {
     Split sp = split_for_vectors<T>(reinterpret_cast<uintptr_t>(r), count, align);
     unsigned p = unsigned((reinterpret_cast<uintptr_t>(s) + sp.head * sizeof(T)) & 15);
     size_t grid = ceil_div(sp.nvec, size_t(64));
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    if (grid_cap && grid > grid_cap) grid = grid_cap;
     void* args[] = {&s, &r, &sp.head, &sp.nvec, &sp.tail, &p};
     return launch(reinterpret_cast<const void*>(&reduce_shift_kernel<T, OP, POLICY, XCD, TAG, SEND_ALIGNED, RUN>), grid,
                   args, stream, 64, lds_bytes);

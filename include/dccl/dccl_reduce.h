@@ -114,7 +114,7 @@ int dccl_local_reduce_chain_host(const void* const* sends, int nsend, const void
 /*
  * Routing hint for host-resident chunks: the payload size (bytes per operand) from which
  * dccl_local_reduce_host beats the reference's own one-thread CPU loop do_host_reduce<DT>
- * (/root/reference/src/core/internal_common.hpp:496-586) on MI355X: 256 MiB, measured by bench.py's
+ * (/root/reference/src/core/internal_common.hpp:496-586) on MI355X, measured by bench.py's
  * `host_crossover` leg on buffers registered with dccl_register_host_memory against one core on the
  * buffers' NUMA node.  A caller keeps do_host_reduce below it; pageable
  * chunks never beat that loop.  0 for dtypes the reference's host loop cannot combine (bf16; fp16 has host
