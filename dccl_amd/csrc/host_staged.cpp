@@ -35,9 +35,11 @@
 
 namespace dccl_amd {
 
-// dccl_local_reduce under a cap on its one-wave blocks (local_reduce.hip)
+// dccl_local_reduce / dccl_local_reduce_chain under a cap on their one-wave blocks (local_reduce.hip)
 int local_reduce_capped(const void* send, void* recv, int dtype, size_t count, int op, hipStream_t stream,
                         size_t grid_cap);
+int local_reduce_chain_capped(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
+                              size_t count, int op, hipStream_t stream, size_t grid_cap);
 
 namespace {
 
@@ -327,6 +329,19 @@ int Stager::run(const unsigned char* send, unsigned char* recv, int dtype, size_
     return rc;
 }
 
+// One-wave blocks of a zero-copy chain combine (zero_copy_waves' rule; in-phase launches only).  Per call on MI355X,
+// fp32 Sum, k = 1 / 3 / 7 sources of 64 MiB, 256 waves against one block per tile (profiles/r6_chain_host_waves.json):
+// registered operands 2742 -> 2457, 5223 -> 4770, 10531 -> 9458 us; staged pageable ones 4057 -> 3586, 6260 -> 5796,
+// 11391 -> 10793 us; 512 and 1024 waves within noise of 256 for registered operands.  DCCL_HOST_CHAIN_WAVES
+// overrides (0: one block per tile).
+size_t chain_waves() {
+    static const size_t v = [] {
+        const char* e = std::getenv("DCCL_HOST_CHAIN_WAVES");
+        return e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : size_t(256);
+    }();
+    return v;
+}
+
 // Host chain combine, the host twin of dccl_local_reduce_chain.  Operands that are not page-locked are
 // bounced into pinned staging and one zero-copy chain kernel per piece reads them over PCIe in the
 // ring's order; the result is copied back.  Pieces alternate between two halves of the staging area, so
@@ -345,7 +360,7 @@ int Stager::run_chain(const void* const* sends, int nsend, const void* own, void
     const bool stage_own = a_own == nullptr || a_dst == nullptr;
     int rc = DCCL_SUCCESS;
     if (all_pinned && !stage_own) {  // everything page-locked: one kernel, nothing staged
-        rc = dccl_local_reduce_chain(as, nsend, a_own, a_dst, dtype, count, op, comp_);
+        rc = local_reduce_chain_capped(as, nsend, a_own, a_dst, dtype, count, op, comp_, chain_waves());
         if (hipStreamSynchronize(comp_) != hipSuccess && rc == DCCL_SUCCESS) rc = DCCL_UNHANDLED_DEVICE_ERROR;
         return rc;
     }
@@ -397,7 +412,7 @@ int Stager::run_chain(const void* const* sends, int nsend, const void* own, void
             down = static_cast<const unsigned char*>(a_own) + o;
             ddst = static_cast<unsigned char*>(a_dst) + o;
         }
-        rc = dccl_local_reduce_chain(ds, nsend, down, ddst, dtype, n, op, comp_);
+        rc = local_reduce_chain_capped(ds, nsend, down, ddst, dtype, n, op, comp_, chain_waves());
         if (rc == DCCL_SUCCESS && hipEventRecord(chain_ev_[j % 2], comp_) != hipSuccess)
             rc = DCCL_UNHANDLED_DEVICE_ERROR;
         if (rc == DCCL_SUCCESS) launched = j + 1;

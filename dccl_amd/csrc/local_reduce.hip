@@ -197,20 +197,24 @@ __global__ __launch_bounds__(64) void copy_multi_kernel(CopyList cl, int npairs,
 }
 
 template <typename T, int OP, int K>
-int launch_chain_vec(SendList sl, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream) {
+int launch_chain_vec(SendList sl, const unsigned char* own, unsigned char* d, Split sp, hipStream_t stream,
+                     size_t grid_cap) {
     using C = DefaultCfg;
     size_t grid = ceil_div(sp.nvec, C::TILE);
     if (grid == 0 && (sp.head + sp.tail) > 0) grid = 1;
+    if (grid_cap && grid > grid_cap) grid = grid_cap;
     void* args[] = {&sl, &own, &d, &sp.head, &sp.nvec, &sp.tail};
     return launch(reinterpret_cast<const void*>(&reduce_chain_vec_kernel<T, OP, K, C>), grid, args, stream, C::BLOCK,
                   caps::lds(caps::kChain, K, sp.nvec * 16));
 }
 
+// grid_cap: as reduce_typed's, for the zero-copy host chain combine; it applies to the in-phase launches (the host
+// staging keeps every operand 256-B aligned), the other alignment classes keep their own grids.
 template <typename T, int OP>
 int reduce_chain_typed(const void* const* sends, int nsend, const void* own, void* dst, size_t count,
-                       hipStream_t stream) {
+                       hipStream_t stream, size_t grid_cap) {
     // dst = op(own, s0) in place is the pairwise combine recv = op(recv, send) with recv = own = dst
-    if (nsend == 1 && own == dst) return reduce_typed<T, OP>(sends[0], dst, count, stream);
+    if (nsend == 1 && own == dst) return reduce_typed<T, OP>(sends[0], dst, count, stream, grid_cap);
     SendList sl{};
     const uintptr_t ad = reinterpret_cast<uintptr_t>(dst), ao = reinterpret_cast<uintptr_t>(own);
     bool src_off = false;  // some source at another 16-B phase than dst
@@ -248,13 +252,15 @@ int reduce_chain_typed(const void* const* sends, int nsend, const void* own, voi
     }
     const Split sp = split_for_vectors<T>(ad, count, recv_align());
     if (any_straddles(sl, nsend, sp.head * sizeof(T))) return chain_straddle_typed<T, OP>(sl, nsend, o, d, sp, stream);
-    return with_k<1, 8>(nsend, [&](auto K) { return launch_chain_vec<T, OP, K.value>(sl, o, d, sp, stream); });
+    return with_k<1, 8>(nsend,
+                        [&](auto K) { return launch_chain_vec<T, OP, K.value>(sl, o, d, sp, stream, grid_cap); });
 }
 
 struct ReduceChainFn {
     template <typename T, int OP>
-    static int run(const void* const* sends, int nsend, const void* own, void* dst, size_t count, hipStream_t stream) {
-        return reduce_chain_typed<T, OP>(sends, nsend, own, dst, count, stream);
+    static int run(const void* const* sends, int nsend, const void* own, void* dst, size_t count, hipStream_t stream,
+                   size_t grid_cap) {
+        return reduce_chain_typed<T, OP>(sends, nsend, own, dst, count, stream, grid_cap);
     }
 };
 
@@ -309,8 +315,11 @@ extern "C" int dccl_local_reduce_multi(const void* const* sends, int nsend, void
     return dispatch<ReduceMultiFn>(dtype, op, sends, nsend, recv, count, static_cast<hipStream_t>(stream));
 }
 
-extern "C" int dccl_local_reduce_chain(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
-                                       size_t count, int op, void* stream) {
+namespace dccl_amd {
+// dccl_local_reduce_chain with the in-phase launches capped at grid_cap one-wave blocks (a multiple of 8; 0 =
+// none): the zero-copy host chain combine (host_staged.cpp).  Not exported.
+int local_reduce_chain_capped(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
+                              size_t count, int op, hipStream_t stream, size_t grid_cap) {
     const int v = validate(dtype, op);
     if (v != DCCL_SUCCESS) return v;
     if (nsend < 1 || nsend > 8 || sends == nullptr) return DCCL_INVALID_ARGUMENT;
@@ -320,7 +329,13 @@ extern "C" int dccl_local_reduce_chain(const void* const* sends, int nsend, cons
         if (sends[k] == nullptr) return DCCL_INVALID_ARGUMENT;
     if (sources_overlap_destination(sends, nsend, own, dst, count * size_of_dtype(dtype)))
         return DCCL_INVALID_ARGUMENT;
-    return dispatch<ReduceChainFn>(dtype, op, sends, nsend, own, dst, count, static_cast<hipStream_t>(stream));
+    return dispatch<ReduceChainFn>(dtype, op, sends, nsend, own, dst, count, stream, grid_cap / 8 * 8);
+}
+}  // namespace dccl_amd
+
+extern "C" int dccl_local_reduce_chain(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
+                                       size_t count, int op, void* stream) {
+    return local_reduce_chain_capped(sends, nsend, own, dst, dtype, count, op, static_cast<hipStream_t>(stream), 0);
 }
 
 extern "C" int dccl_copy_multi(const void* const* srcs, void* const* dsts, int npairs, size_t bytes, void* stream) {
