@@ -35,11 +35,13 @@
 
 namespace dccl_amd {
 
-// dccl_local_reduce / dccl_local_reduce_chain under a cap on their one-wave blocks (local_reduce.hip)
-int local_reduce_capped(const void* send, void* recv, int dtype, size_t count, int op, hipStream_t stream,
-                        size_t grid_cap);
-int local_reduce_chain_capped(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
-                              size_t count, int op, hipStream_t stream, size_t grid_cap);
+// dccl_local_reduce / dccl_local_reduce_chain under a cap on their one-wave blocks (local_reduce.hip; hidden)
+__attribute__((visibility("hidden"))) int local_reduce_capped(const void* send, void* recv, int dtype, size_t count,
+                                                              int op, hipStream_t stream, size_t grid_cap);
+__attribute__((visibility("hidden"))) int local_reduce_chain_capped(const void* const* sends, int nsend,
+                                                                    const void* own, void* dst, int dtype,
+                                                                    size_t count, int op, hipStream_t stream,
+                                                                    size_t grid_cap);
 
 namespace {
 
@@ -490,9 +492,10 @@ extern "C" int dccl_deregister_host_memory(void* buffer) {
     return hipHostUnregister(buffer) == hipSuccess ? DCCL_SUCCESS : DCCL_UNHANDLED_DEVICE_ERROR;
 }
 
-// The measured crossover of dccl_local_reduce_host against the reference's one-thread loop (DESIGN.md §4,
-// bench.py `host_crossover`, registered fp32 Sum operands, cold caches; profiles/r6_host_crossover.json).  The loop's rate is in bytes for
-// every dtype it vectorises, so one byte threshold serves them all.
+// The measured crossover of dccl_local_reduce_host against the reference's one-thread loop on a core of the
+// buffers' NUMA node (bench.py `host_crossover`, registered fp32 Sum operands, cold caches;
+// profiles/r6_host_crossover.json).  The loop's rate is in bytes for every dtype it vectorises, so one byte
+// threshold serves them all.
 constexpr size_t kHostGpuMinBytes = size_t(64) << 20;
 
 extern "C" size_t dccl_host_reduce_gpu_min_bytes(int dtype) {

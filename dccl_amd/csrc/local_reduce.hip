@@ -285,8 +285,8 @@ using namespace dccl_amd;
 
 namespace dccl_amd {
 // dccl_local_reduce with at most grid_cap one-wave blocks (a multiple of 8; 0 = none): the zero-copy combine of
-// host operands (host_staged.cpp).  Not exported.
-int local_reduce_capped(const void* send, void* recv, int dtype, size_t count, int op, hipStream_t stream,
+// host operands (host_staged.cpp).  Hidden: not part of the library's ABI.
+__attribute__((visibility("hidden"))) int local_reduce_capped(const void* send, void* recv, int dtype, size_t count, int op, hipStream_t stream,
                         size_t grid_cap) {
     const int v = validate(dtype, op);
     if (v != DCCL_SUCCESS) return v;
@@ -317,8 +317,8 @@ extern "C" int dccl_local_reduce_multi(const void* const* sends, int nsend, void
 
 namespace dccl_amd {
 // dccl_local_reduce_chain with the in-phase launches capped at grid_cap one-wave blocks (a multiple of 8; 0 =
-// none): the zero-copy host chain combine (host_staged.cpp).  Not exported.
-int local_reduce_chain_capped(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
+// none): the zero-copy host chain combine (host_staged.cpp).  Hidden: not part of the library's ABI.
+__attribute__((visibility("hidden"))) int local_reduce_chain_capped(const void* const* sends, int nsend, const void* own, void* dst, int dtype,
                               size_t count, int op, hipStream_t stream, size_t grid_cap) {
     const int v = validate(dtype, op);
     if (v != DCCL_SUCCESS) return v;
