@@ -592,6 +592,73 @@ def test_host_staged_byte_offsets(dccl, pinned):
             assert sb[soff:soff + s.nbytes].tobytes() == s.tobytes()
 
 
+ZERO_COPY_CAP_CHILD = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+import dccl_amd, oracle
+from tests.test_gpu_parity import rand_inputs, expected
+from tests.test_oracle import fp_equal
+torch.cuda.set_device(0)
+rng = np.random.default_rng(404)
+bad = []
+# every pairwise kernel class over PCIe (aligned, line-straddling, shifted, byte-shifted send, misaligned recv),
+# sizes with a partial last tile, head and tail scalars, and many tiles per striding wave
+for dt, n, soff, roff in [(7, 3 * 65536 + 5, 0, 0), (7, 70001, 64, 0), (7, 70001, 4, 0), (2, 50003, 1, 0),
+                          (8, 40001, 0, 3), (6, 90001, 2, 6), (0, 300007, 5, 0)]:
+    s, r = rand_inputs(rng, dt, n)
+    op = int(rng.integers(0, 4))
+    want = expected(s, r, dt, op)
+    sb = np.zeros(s.nbytes + 256, np.uint8); rb = np.zeros(r.nbytes + 256, np.uint8)
+    sb[soff:soff + s.nbytes] = s.view(np.uint8); rb[roff:roff + r.nbytes] = r.view(np.uint8)
+    for x in (sb, rb):
+        assert dccl_amd.register_host_memory(x.ctypes.data, x.nbytes) == 0
+    rc = dccl_amd.local_reduce_host(sb.ctypes.data + soff, rb.ctypes.data + roff, dt, n, op)
+    for x in (sb, rb):
+        dccl_amd.deregister_host_memory(x.ctypes.data)
+    got = rb[roff:roff + r.nbytes].view(r.dtype)
+    if rc != 0 or not fp_equal(got, want, dt) or rb[:roff].any() or rb[roff + r.nbytes:].any():
+        bad.append(("pair", dt, n, soff, roff, rc))
+# the host chain combine, staged (pageable) and in place on registered operands
+for dt, n, k in [(7, 200003, 3), (4, 100001, 7), (9, 150001, 1)]:
+    srcs = [rand_inputs(rng, dt, n)[0] for _ in range(k)]
+    own = rand_inputs(rng, dt, n)[0]
+    op = int(rng.integers(0, 4))
+    want = srcs[0].copy()
+    for j in range(1, k):
+        want = expected(want, srcs[j], dt, op)
+    want = expected(want, own, dt, op)
+    for registered in (False, True):
+        o = own.copy()
+        regs = srcs + [o] if registered else []
+        for x in regs:
+            assert dccl_amd.register_host_memory(x.ctypes.data, x.nbytes) == 0
+        rc = dccl_amd.local_reduce_chain_host([x.ctypes.data for x in srcs], o.ctypes.data, o.ctypes.data, dt, n, op)
+        for x in regs:
+            dccl_amd.deregister_host_memory(x.ctypes.data)
+        if rc != 0 or not fp_equal(o, want, dt):
+            bad.append(("chain", dt, n, k, registered, rc))
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+"""
+
+
+@pytest.mark.parametrize("waves", ["8", "512", "0"])
+def test_host_zero_copy_wave_caps(waves):
+    """The zero-copy host combines under their wave caps (DCCL_HOST_ZEROCOPY_WAVES / DCCL_HOST_CHAIN_WAVES, read
+    once per process, so each cap runs in a child): 8 waves (hundreds of tiles per striding wave), the default
+    512 and none; every pairwise kernel class and the chain, bit-exact against the oracle, nothing written
+    outside the destination."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {**os.environ, "DCCL_HOST_ZEROCOPY_WAVES": waves, "DCCL_HOST_CHAIN_WAVES": waves, "PYTHONPATH": root}
+    p = subprocess.run([sys.executable, "-c", ZERO_COPY_CAP_CHILD, root], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+
+
 @pytest.mark.parametrize("threads", ["1", "3", "8"])
 def test_host_staged_copy_threads(dccl, threads, monkeypatch):
     """Pageable bounce copies split over DCCL_HOST_COPY_THREADS threads: odd byte counts, every slice
