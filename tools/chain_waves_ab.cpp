@@ -1,4 +1,6 @@
-// tools/chain_waves_ab.cpp — A/B of the host chain combine's wave cap (DCCL_HOST_CHAIN_WAVES), the shipped 256 (host_staged.cpp chain_waves): dccl_local_reduce_chain_host per call, registered and pageable operands.
+// tools/chain_waves_ab.cpp — A/B of the host chain combine's wave cap (DCCL_HOST_CHAIN_WAVES; the shipped 256 is
+// host_staged.cpp's chain_waves): dccl_local_reduce_chain_host per call, registered and pageable operands
+// (profiles/r6_chain_host_waves.json).
 //   hipcc -std=c++17 -O2 -I include tools/chain_waves_ab.cpp -o /tmp/ab -L dccl_amd/lib -ldccl_amd -Wl,-rpath,$PWD/dccl_amd/lib
 //   for c in 0 256 512 1024; do DCCL_...WAVES=$c /tmp/ab; done     (one JSON line per case)
 #include <hip/hip_runtime.h>

@@ -1,4 +1,6 @@
-// tools/host_waves_ab.cpp — A/B of the zero-copy host combine's wave cap (DCCL_HOST_ZEROCOPY_WAVES), the shipped 512 (host_staged.cpp zero_copy_waves): dccl_local_reduce_host per call vs size, registered and hipHostMalloc operands.
+// tools/host_waves_ab.cpp — A/B of the zero-copy host combine's wave cap (DCCL_HOST_ZEROCOPY_WAVES; the shipped
+// 512 is host_staged.cpp's zero_copy_waves): dccl_local_reduce_host per call vs size, registered and hipHostMalloc
+// operands (profiles/r6_zero_copy_waves.json).
 //   hipcc -std=c++17 -O2 -I include tools/host_waves_ab.cpp -o /tmp/ab -L dccl_amd/lib -ldccl_amd -Wl,-rpath,$PWD/dccl_amd/lib
 //   for c in 0 256 512 1024; do DCCL_...WAVES=$c /tmp/ab; done     (one JSON line per case)
 #include <hip/hip_runtime.h>
